@@ -1,0 +1,254 @@
+/*
+ * soarm_sim.h — C ABI of the MI355X-native batched SO-ARM101 simulator.
+ *
+ * This is the drop-in boundary for the reference's hot path
+ * (SURVEY.md §8b).  In the reference, the Python layer calls MuJoCo's C engine
+ * through its Python bindings:
+ *
+ *   mujoco.MjModel.from_xml_path(xml)        SOARM101/SOARM101_Env.py:34
+ *   mujoco.MjData(model)                     SOARM101/SOARM101_Env.py:43
+ *   mujoco.mj_resetData(model, data)         SOARM101/SOARM101_Env.py:87
+ *   mujoco.mj_forward(model, data)           SOARM101/SOARM101_Env.py:102
+ *   mujoco.mj_step(model, data)  (x frame_skip) SOARM101/SOARM101_Env.py:131-132
+ *   data.site_xpos / data.qpos  (obs)        SOARM101/SOARM101_Env.py:71-75
+ *   dm_control qpos_from_site_pose (IK)      control/TrajectoryGenerator.py:96-107
+ *
+ * Each of those is replaced by one batched entry point below that runs on a
+ * whole batch of environments (envs) on one GPU.  Plain C types only: device
+ * pointers are passed as raw pointers, sizes as ints, streams as void*
+ * (a hipStream_t; NULL = the default stream).  Every function returns 0 on
+ * success or a negative SIM_E* code; sim_last_error() returns a thread-local
+ * message for the last failure.
+ *
+ * Memory: the library owns the model constants (one device copy per
+ * sim_batch) and its scratch.  Env state is caller-owned device memory laid out
+ * structure-of-arrays, [field][env] (so lane i of a wave reads env i: coalesced).
+ * Nothing inside sim_step/sim_reset allocates, synchronises or copies between
+ * host and device, so a caller may capture them in a hipGraph.
+ */
+#ifndef SOARM_SIM_H
+#define SOARM_SIM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- capacity of the compiled model (MuJoCo mjModel subset) ---- */
+#define SIM_MAXBODY 12
+#define SIM_MAXJNT 12
+#define SIM_MAXDOF 16
+#define SIM_MAXQ 20
+#define SIM_MAXGEOM 40
+#define SIM_MAXPAIR 160
+#define SIM_MAXSITE 4
+#define SIM_MAXU 8
+#define SIM_MAXOBSQ 8
+#define SIM_MAXCON 16 /* contacts kept per env per substep */
+
+/* MuJoCo enum values (mjtJoint, mjtGeom) */
+enum { SIM_JNT_FREE = 0, SIM_JNT_BALL = 1, SIM_JNT_SLIDE = 2, SIM_JNT_HINGE = 3 };
+enum { SIM_GEOM_PLANE = 0, SIM_GEOM_SPHERE = 2, SIM_GEOM_BOX = 6, SIM_GEOM_MESH = 7 };
+
+/* error codes */
+enum {
+  SIM_OK = 0,
+  SIM_E_ARG = -1,      /* bad argument / shape */
+  SIM_E_MODEL = -2,    /* model outside what the kernels support */
+  SIM_E_HIP = -3,      /* HIP runtime error */
+  SIM_E_NODEVICE = -4, /* no GPU visible */
+};
+
+/* per-env status bits (sim_state.status) */
+enum {
+  SIM_ST_BADQPOS = 1,   /* mj_checkPos: non-finite or |qpos| > 1e10 -> env auto-reset */
+  SIM_ST_BADQVEL = 2,   /* mj_checkVel */
+  SIM_ST_BADQACC = 4,   /* mj_checkAcc */
+  SIM_ST_CONOVERFLOW = 8 /* more than SIM_MAXCON contacts in a substep (extra dropped) */
+};
+
+/*
+ * Compiled model.  Field names and meanings follow MuJoCo's mjModel
+ * (mjmodel.h) so the MJCF compiler (lerobot-mujoco-sim2real_amd/mjcf.py) and
+ * the oracle read the same numbers.  Quaternions are (w, x, y, z).
+ */
+typedef struct sim_model_desc {
+  int32_t nbody, njnt, nq, nv, nu, ngeom, nsite, npair;
+  int32_t nhullvert, nhulladj; /* lengths of the hull arrays passed beside */
+
+  /* mjOption */
+  double timestep;
+  double gravity[3];
+  double impratio;
+  double tolerance;      /* solver: stop when the cost improvement is below this */
+  int32_t iterations;    /* solver: max PGS sweeps */
+  int32_t disable_contact; /* mjDSBL_CONTACT */
+  int32_t disable_eulerdamp;
+  int32_t _pad0;
+
+  /* bodies (0 = world) */
+  int32_t body_parentid[SIM_MAXBODY];
+  int32_t body_rootid[SIM_MAXBODY];
+  int32_t body_weldid[SIM_MAXBODY];
+  int32_t body_jntnum[SIM_MAXBODY];
+  int32_t body_jntadr[SIM_MAXBODY];
+  int32_t body_dofnum[SIM_MAXBODY];
+  int32_t body_dofadr[SIM_MAXBODY];
+  double body_pos[SIM_MAXBODY][3];
+  double body_quat[SIM_MAXBODY][4];
+  double body_ipos[SIM_MAXBODY][3];
+  double body_iquat[SIM_MAXBODY][4];
+  double body_mass[SIM_MAXBODY];
+  double body_inertia[SIM_MAXBODY][3]; /* principal moments */
+  double body_invweight0[SIM_MAXBODY][2];
+
+  /* joints */
+  int32_t jnt_type[SIM_MAXJNT];
+  int32_t jnt_bodyid[SIM_MAXJNT];
+  int32_t jnt_qposadr[SIM_MAXJNT];
+  int32_t jnt_dofadr[SIM_MAXJNT];
+  int32_t jnt_limited[SIM_MAXJNT];
+  int32_t _pad1;
+  double jnt_pos[SIM_MAXJNT][3];
+  double jnt_axis[SIM_MAXJNT][3];
+  double jnt_range[SIM_MAXJNT][2];
+  double jnt_solref[SIM_MAXJNT][2];
+  double jnt_solimp[SIM_MAXJNT][5];
+  double jnt_margin[SIM_MAXJNT];
+  double qpos0[SIM_MAXQ];
+
+  /* dofs */
+  int32_t dof_bodyid[SIM_MAXDOF];
+  int32_t dof_jntid[SIM_MAXDOF];
+  int32_t dof_parentid[SIM_MAXDOF];
+  double dof_armature[SIM_MAXDOF];
+  double dof_damping[SIM_MAXDOF];
+  double dof_frictionloss[SIM_MAXDOF];
+  double dof_invweight0[SIM_MAXDOF];
+  double dof_solref[SIM_MAXDOF][2];
+  double dof_solimp[SIM_MAXDOF][5];
+
+  /* geoms (only collidable geoms are compiled in; visual ones are dropped) */
+  int32_t geom_type[SIM_MAXGEOM];
+  int32_t geom_bodyid[SIM_MAXGEOM];
+  int32_t geom_condim[SIM_MAXGEOM];
+  int32_t geom_hulladr[SIM_MAXGEOM]; /* first vertex in hull_vert (mesh only, else -1) */
+  int32_t geom_hullnum[SIM_MAXGEOM];
+  int32_t _pad2;
+  double geom_pos[SIM_MAXGEOM][3];
+  double geom_quat[SIM_MAXGEOM][4];
+  double geom_size[SIM_MAXGEOM][3];
+  double geom_friction[SIM_MAXGEOM][3];
+  double geom_solref[SIM_MAXGEOM][2];
+  double geom_solimp[SIM_MAXGEOM][5];
+  double geom_margin[SIM_MAXGEOM];
+  double geom_rbound[SIM_MAXGEOM];     /* bounding-sphere radius about geom_aabb centre */
+  double geom_aabb[SIM_MAXGEOM][6];    /* local-frame box: centre(3), half-size(3) */
+
+  /* candidate collision pairs, in MuJoCo's deterministic contact order */
+  int32_t pair_geom1[SIM_MAXPAIR];
+  int32_t pair_geom2[SIM_MAXPAIR];
+
+  /* sites */
+  int32_t site_bodyid[SIM_MAXSITE];
+  double site_pos[SIM_MAXSITE][3];
+  double site_quat[SIM_MAXSITE][4];
+
+  /* actuators: joint transmission, fixed gain, affine bias (mjGAIN_FIXED/mjBIAS_AFFINE) */
+  int32_t actuator_trnid[SIM_MAXU]; /* joint id */
+  int32_t actuator_ctrllimited[SIM_MAXU];
+  int32_t actuator_forcelimited[SIM_MAXU];
+  double actuator_gear[SIM_MAXU];
+  double actuator_gainprm[SIM_MAXU];    /* gainprm[0] */
+  double actuator_biasprm[SIM_MAXU][3];
+  double actuator_ctrlrange[SIM_MAXU][2];
+  double actuator_forcerange[SIM_MAXU][2];
+
+  /* observation recipe (SOARM101Env._get_state, SOARM101_Env.py:69-75):
+     obs = [site_xpos[obs_site] (3), qpos[obs_qadr[0..obs_nq-1]]] */
+  int32_t obs_site;
+  int32_t obs_nq;
+  int32_t obs_qadr[SIM_MAXOBSQ];
+  int32_t nact; /* how many leading ctrl entries an action writes (udim = 5) */
+  int32_t _pad3;
+} sim_model_desc;
+
+/* DLS-IK options (dm_control qpos_from_site_pose semantics) */
+typedef struct sim_ik_opts {
+  double tol;                 /* 1e-6 */
+  double regularization_threshold; /* 0.1 */
+  double regularization_strength;  /* 1e-2 */
+  double max_update_norm;     /* 2.0 */
+  double progress_thresh;     /* 20.0 */
+  int32_t max_steps;          /* 100 */
+  int32_t site;               /* site id */
+  int32_t ndof;               /* number of leading dofs moved (5) */
+  int32_t _pad;
+} sim_ik_opts;
+
+/* Env state: caller-owned DEVICE buffers, SoA [field][n_envs]. */
+typedef struct sim_state {
+  float* qpos;            /* [nq][N]  */
+  float* qvel;            /* [nv][N]  */
+  float* qacc_warmstart;  /* [nv][N]  */
+  float* ctrl;            /* [nu][N]  */
+  int32_t* status;        /* [N]      SIM_ST_* bits, OR-ed since last reset */
+  float* ncon;            /* [N]      running contact-count sum (for contacts/env/substep) */
+} sim_state;
+
+/* Optional per-env domain-randomisation parameters (DEVICE, [N] each; NULL = nominal). */
+typedef struct sim_params {
+  const float* mass_scale;     /* body mass (and inertia) x scale, all bodies */
+  const float* friction;       /* sliding friction of every collidable geom */
+  const float* damping_scale;  /* dof damping x scale */
+} sim_params;
+
+typedef struct sim_model sim_model;
+typedef struct sim_batch sim_batch;
+
+const char* sim_last_error(void);
+const char* sim_version(void);
+
+/* replaces MjModel.from_xml_path (compilation itself happens in mjcf.py);
+   hull_vert [nhullvert][3], hull_adr [nhullvert+1] CSR, hull_adj [nhulladj] local ids */
+int sim_model_create(const sim_model_desc* desc, const float* hull_vert, const int32_t* hull_adr,
+                     const int32_t* hull_adj, sim_model** out);
+void sim_model_free(sim_model* m);
+
+/* replaces MjData(model) for n_envs envs on `device` (HIP ordinal) */
+int sim_batch_create(const sim_model* m, int n_envs, int device, sim_batch** out);
+void sim_batch_free(sim_batch* b);
+int sim_batch_set_params(sim_batch* b, const sim_params* p);
+
+/* replaces mj_resetData + qpos/qvel overwrite + mj_forward (SOARM101_Env.py:87-102)
+   for envs with mask[i] != 0 (mask NULL = all).  init_qpos/init_qvel are
+   [obs_nq][N] SoA device arrays written into qpos[obs_qadr]/qvel (NULL ->
+   qpos drawn U(-0.3, 0.3) from Philox4x32-10 keyed by (seed, env_offset + i),
+   qvel 0).  extra_qpos [nq][N] (or NULL) overrides the whole qpos0 first
+   (used for the build-defined cube pose).  obs [N][3+obs_nq] row-major. */
+int sim_reset(sim_batch* b, const sim_state* s, const float* init_qpos, const float* init_qvel,
+              const float* extra_qpos, uint64_t seed, int64_t env_offset, const uint8_t* mask,
+              float* obs, void* stream);
+
+/* replaces ctrl[:nact] = action; frame_skip x mj_step; _get_state
+   (SOARM101_Env.py:128-135).  action [N][nact] row-major, obs [N][3+obs_nq]. */
+int sim_step(sim_batch* b, const sim_state* s, const float* action, int frame_skip, float* obs,
+             void* stream);
+
+/* one plain mj_step-equivalent on the current ctrl, no obs (frame_skip substeps) */
+int sim_substeps(sim_batch* b, const sim_state* s, int nsub, void* stream);
+
+/* observation only (mj_kinematics + _get_state) */
+int sim_observe(sim_batch* b, const sim_state* s, float* obs, void* stream);
+
+/* replaces dm_control qpos_from_site_pose, position-only (control/TrajectoryGenerator.py:96-107):
+   target [N][3], q [nq][N] SoA in/out (warm start), ok [N] (1 = converged), iters [N] or NULL */
+int sim_ik_dls(sim_batch* b, const float* target, float* q, int32_t* ok, int32_t* iters,
+               const sim_ik_opts* opts, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SOARM_SIM_H */
