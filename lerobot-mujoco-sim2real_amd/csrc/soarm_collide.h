@@ -1,0 +1,611 @@
+// soarm_collide.h — per-env collision for the fused step kernel (gfx950).
+//
+// Restates mj_collision for the hot-path scenes:
+//   * the candidate pairs are the compiler's static list in MuJoCo's contact
+//     order; every lane walks the same list, so the pair loop and the
+//     geom/body lookups are wave-uniform;
+//   * midphase: bounding sphere + world AABB about each geom's collision box;
+//   * narrowphase: MPR penetration (hull / box vs hull, tolerance 1e-6,
+//     <= 50 refinement steps), box-box SAT + face clipping (<= 4 contacts),
+//     plane-box corners (<= 4), plane-hull deepest vertex;
+//   * hull support = steepest-ascent hill climbing on the hull vertex graph
+//     (L2-resident float4 vertices, CSR adjacency).
+// Geom world poses for the lane are staged once per substep in LDS laid out
+// [slot][lane] (consecutive lanes -> consecutive banks); contacts are appended
+// in pair order into the lane's LDS contact list.
+#pragma once
+#include "soarm_step.h"
+
+namespace soarm {
+
+constexpr int CON_MAXG = 16;  // collidable geoms supported by the contact kernel
+constexpr float FEPS = 1.1920929e-07f;
+constexpr float MPR_TOLF = 1e-6f;
+constexpr int MPR_ITERS = 50;
+
+// LDS views (per block of 64 lanes)
+struct GeomLds {
+  float (*a)[64];  // [CON_MAXG * 12][64]: pos(3), R(9)
+  int lane;
+  DEVI float& pos(int g, int k) const { return a[g * 12 + k][lane]; }
+  DEVI float& R(int g, int k) const { return a[g * 12 + 3 + k][lane]; }
+};
+struct ConLds {
+  float (*a)[64];  // [SIM_MAXCON * 8][64]: dist, pos(3), n(3), pair
+  int lane;
+  DEVI float& dist(int c) const { return a[c * 8][lane]; }
+  DEVI float& pos(int c, int k) const { return a[c * 8 + 1 + k][lane]; }
+  DEVI float& n(int c, int k) const { return a[c * 8 + 4 + k][lane]; }
+  DEVI int pair(int c) const { return __float_as_int(a[c * 8 + 7][lane]); }
+  DEVI void set_pair(int c, int p) const { a[c * 8 + 7][lane] = __int_as_float(p); }
+};
+
+struct GeomPose {
+  float p[3], R[9];
+};
+
+DEVI void load_pose(const GeomLds& G, int g, GeomPose& o) {
+#pragma unroll
+  for (int k = 0; k < 3; k++) o.p[k] = G.pos(g, k);
+#pragma unroll
+  for (int k = 0; k < 9; k++) o.R[k] = G.R(g, k);
+}
+
+// hill-climbing support on a mesh hull; returns the local vertex
+DEVI float3 hull_support(const DModel& m, int g, const float l[3]) {
+  const float4* v = m.hull_vert + m.geom_hulladr[g];
+  const int32_t* adr = m.hull_adr + m.geom_hulladr[g];
+  const int nvert = m.geom_hullnum[g];
+  int cur = 0;
+  float4 cv = v[0];
+  float cd = l[0] * cv.x + l[1] * cv.y + l[2] * cv.z;
+  for (int guard = 0; guard < nvert; guard++) {
+    int nxt = cur;
+    float nd = cd;
+    const int a0 = adr[cur], a1 = adr[cur + 1];
+    for (int a = a0; a < a1; a++) {
+      const int u = m.hull_adj[a];
+      const float4 w = v[u];
+      const float s = l[0] * w.x + l[1] * w.y + l[2] * w.z;
+      if (s > nd) nd = s, nxt = u;
+    }
+    if (nxt == cur) break;
+    cur = nxt;
+    cd = nd;
+  }
+  cv = v[cur];
+  return make_float3(cv.x, cv.y, cv.z);
+}
+
+// world support point of geom g (type uniform across the wave)
+DEVI void support(const DModel& m, int g, const GeomPose& P, const float d[3], float out[3]) {
+  float l[3];
+  mtv(l, P.R, d);
+  float p[3] = {0, 0, 0};
+  const int t = m.geom_type[g];
+  if (t == SIM_GEOM_BOX) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) p[k] = (l[k] >= 0.f ? 1.f : -1.f) * m.geom_size[g][k];
+  } else if (t == SIM_GEOM_MESH) {
+    const float3 v = hull_support(m, g, l);
+    p[0] = v.x, p[1] = v.y, p[2] = v.z;
+  }
+  float w[3];
+  mv(w, P.R, p);
+  out[0] = P.p[0] + w[0], out[1] = P.p[1] + w[1], out[2] = P.p[2] + w[2];
+}
+
+DEVI void geom_center(const DModel& m, int g, const GeomPose& P, float c[3]) {
+  const float lc[3] = {m.geom_center[g][0], m.geom_center[g][1], m.geom_center[g][2]};
+  float w[3];
+  mv(w, P.R, lc);
+  c[0] = P.p[0] + w[0], c[1] = P.p[1] + w[1], c[2] = P.p[2] + w[2];
+}
+
+// ---------------------------------------------------------------------- MPR
+struct MSup {
+  float v[3], v1[3], v2[3];
+};
+struct MPair {
+  const DModel& m;
+  int g1, g2;
+  const GeomPose &P1, &P2;
+  DEVI void sup(const float d[3], MSup& s) const {
+    const float nd[3] = {-d[0], -d[1], -d[2]};
+    support(m, g1, P1, d, s.v1);
+    support(m, g2, P2, nd, s.v2);
+    s.v[0] = s.v1[0] - s.v2[0], s.v[1] = s.v1[1] - s.v2[1], s.v[2] = s.v1[2] - s.v2[2];
+  }
+};
+DEVI bool fz(float x) { return fabsf(x) < FEPS; }
+DEVI void nrm(float a[3]) {
+  const float n2 = dot3(a, a);
+  if (n2 > 0.f) {
+    const float s = rsqrtf(n2);
+    a[0] *= s, a[1] *= s, a[2] *= s;
+  }
+}
+DEVI void sub(float r[3], const float a[3], const float b[3]) {
+  r[0] = a[0] - b[0], r[1] = a[1] - b[1], r[2] = a[2] - b[2];
+}
+DEVI void portal_dir(const MSup p[4], float d[3]) {
+  float a[3], b[3];
+  sub(a, p[2].v, p[1].v);
+  sub(b, p[3].v, p[1].v);
+  cross(d, a, b);
+  nrm(d);
+}
+DEVI bool reach_tol(const MSup p[4], const MSup& v4, const float d[3]) {
+  const float d4 = dot3(v4.v, d);
+  const float mn = fminf(fminf(d4 - dot3(p[1].v, d), d4 - dot3(p[2].v, d)), d4 - dot3(p[3].v, d));
+  return mn <= MPR_TOLF;
+}
+DEVI void expand(MSup p[4], const MSup& v4) {
+  float x[3];
+  cross(x, v4.v, p[0].v);
+  if (dot3(p[1].v, x) > 0.f) {
+    if (dot3(p[2].v, x) > 0.f)
+      p[1] = v4;
+    else
+      p[3] = v4;
+  } else {
+    if (dot3(p[3].v, x) > 0.f)
+      p[2] = v4;
+    else
+      p[1] = v4;
+  }
+}
+// -1 separated, 0 portal, 1 origin on v1, 2 origin on segment v0-v1
+DEVI int discover(const MPair& P, MSup p[4]) {
+  float c1[3], c2[3], d[3], va[3], vb[3];
+  geom_center(P.m, P.g1, P.P1, c1);
+  geom_center(P.m, P.g2, P.P2, c2);
+#pragma unroll
+  for (int k = 0; k < 3; k++) p[0].v1[k] = c1[k], p[0].v2[k] = c2[k], p[0].v[k] = c1[k] - c2[k];
+  if (fz(p[0].v[0]) && fz(p[0].v[1]) && fz(p[0].v[2])) p[0].v[0] += 10.f * FEPS;
+  d[0] = -p[0].v[0], d[1] = -p[0].v[1], d[2] = -p[0].v[2];
+  nrm(d);
+  P.sup(d, p[1]);
+  float dt = dot3(p[1].v, d);
+  if (fz(dt) || dt < 0.f) return -1;
+  cross(d, p[0].v, p[1].v);
+  if (fz(dot3(d, d))) {
+    if (fz(p[1].v[0]) && fz(p[1].v[1]) && fz(p[1].v[2])) return 1;
+    return 2;
+  }
+  nrm(d);
+  P.sup(d, p[2]);
+  dt = dot3(p[2].v, d);
+  if (fz(dt) || dt < 0.f) return -1;
+  sub(va, p[1].v, p[0].v);
+  sub(vb, p[2].v, p[0].v);
+  cross(d, va, vb);
+  nrm(d);
+  if (dot3(d, p[0].v) > 0.f) {
+    const MSup t = p[1];
+    p[1] = p[2];
+    p[2] = t;
+    d[0] = -d[0], d[1] = -d[1], d[2] = -d[2];
+  }
+  for (int guard = 0; guard < 1000; guard++) {
+    P.sup(d, p[3]);
+    dt = dot3(p[3].v, d);
+    if (fz(dt) || dt < 0.f) return -1;
+    bool cont = false;
+    cross(va, p[1].v, p[3].v);
+    dt = dot3(va, p[0].v);
+    if (dt < 0.f && !fz(dt)) {
+      p[2] = p[3];
+      cont = true;
+    }
+    if (!cont) {
+      cross(va, p[3].v, p[2].v);
+      dt = dot3(va, p[0].v);
+      if (dt < 0.f && !fz(dt)) {
+        p[1] = p[3];
+        cont = true;
+      }
+    }
+    if (!cont) return 0;
+    sub(va, p[1].v, p[0].v);
+    sub(vb, p[2].v, p[0].v);
+    cross(d, va, vb);
+    nrm(d);
+  }
+  return -1;
+}
+DEVI void closest_tri(const float a[3], const float b[3], const float c[3], float o[3]) {
+  float ab[3], ac[3];
+  sub(ab, b, a);
+  sub(ac, c, a);
+  const float ap[3] = {-a[0], -a[1], -a[2]};
+  const float d1 = dot3(ab, ap), d2 = dot3(ac, ap);
+  if (d1 <= 0.f && d2 <= 0.f) {
+    o[0] = a[0], o[1] = a[1], o[2] = a[2];
+    return;
+  }
+  const float bp[3] = {-b[0], -b[1], -b[2]};
+  const float d3 = dot3(ab, bp), d4 = dot3(ac, bp);
+  if (d3 >= 0.f && d4 <= d3) {
+    o[0] = b[0], o[1] = b[1], o[2] = b[2];
+    return;
+  }
+  const float vc = d1 * d4 - d3 * d2;
+  if (vc <= 0.f && d1 >= 0.f && d3 <= 0.f) {
+    const float v = d1 / (d1 - d3);
+#pragma unroll
+    for (int k = 0; k < 3; k++) o[k] = a[k] + v * ab[k];
+    return;
+  }
+  const float cp[3] = {-c[0], -c[1], -c[2]};
+  const float d5 = dot3(ab, cp), d6 = dot3(ac, cp);
+  if (d6 >= 0.f && d5 <= d6) {
+    o[0] = c[0], o[1] = c[1], o[2] = c[2];
+    return;
+  }
+  const float vb = d5 * d2 - d1 * d6;
+  if (vb <= 0.f && d2 >= 0.f && d6 <= 0.f) {
+    const float w = d2 / (d2 - d6);
+#pragma unroll
+    for (int k = 0; k < 3; k++) o[k] = a[k] + w * ac[k];
+    return;
+  }
+  const float va = d3 * d6 - d5 * d4;
+  if (va <= 0.f && (d4 - d3) >= 0.f && (d5 - d6) >= 0.f) {
+    const float w = (d4 - d3) / ((d4 - d3) + (d5 - d6));
+#pragma unroll
+    for (int k = 0; k < 3; k++) o[k] = b[k] + w * (c[k] - b[k]);
+    return;
+  }
+  const float den = 1.f / (va + vb + vc);
+  const float v = vb * den, w = vc * den;
+#pragma unroll
+  for (int k = 0; k < 3; k++) o[k] = a[k] + ab[k] * v + ac[k] * w;
+}
+DEVI void portal_pos(const MSup p[4], float pos[3]) {
+  float d[3], x[3], b[4];
+  portal_dir(p, d);
+  cross(x, p[1].v, p[2].v);
+  b[0] = dot3(x, p[3].v);
+  cross(x, p[3].v, p[2].v);
+  b[1] = dot3(x, p[0].v);
+  cross(x, p[0].v, p[1].v);
+  b[2] = dot3(x, p[3].v);
+  cross(x, p[2].v, p[1].v);
+  b[3] = dot3(x, p[0].v);
+  float sum = b[0] + b[1] + b[2] + b[3];
+  if (fz(sum) || sum < 0.f) {
+    b[0] = 0.f;
+    cross(x, p[2].v, p[3].v);
+    b[1] = dot3(x, d);
+    cross(x, p[3].v, p[1].v);
+    b[2] = dot3(x, d);
+    cross(x, p[1].v, p[2].v);
+    b[3] = dot3(x, d);
+    sum = b[1] + b[2] + b[3];
+  }
+  const float inv = 1.f / sum;
+  float s1[3] = {0, 0, 0}, s2[3] = {0, 0, 0};
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+#pragma unroll
+    for (int k = 0; k < 3; k++) s1[k] += b[i] * p[i].v1[k], s2[k] += b[i] * p[i].v2[k];
+#pragma unroll
+  for (int k = 0; k < 3; k++) pos[k] = 0.5f * (s1[k] + s2[k]) * inv;
+}
+// returns 1 with depth/dir(geom1->geom2)/pos when penetrating
+DEVI int mpr(const MPair& P, float& depth, float dir[3], float pos[3]) {
+  MSup p[4];
+  const int res = discover(P, p);
+  if (res < 0 || res == 1) return 0;
+  if (res == 2) {
+    depth = sqrtf(dot3(p[1].v, p[1].v));
+#pragma unroll
+    for (int k = 0; k < 3; k++) dir[k] = p[1].v[k], pos[k] = 0.5f * (p[1].v1[k] + p[1].v2[k]);
+    nrm(dir);
+    return depth > 0.f;
+  }
+  // refine the portal until it contains the origin
+  for (int it = 0;; it++) {
+    if (it >= 1000) return 0;
+    float d[3];
+    portal_dir(p, d);
+    const float dt = dot3(d, p[1].v);
+    if (fz(dt) || dt > 0.f) break;
+    MSup v4;
+    P.sup(d, v4);
+    const float d4 = dot3(v4.v, d);
+    if (!(fz(d4) || d4 > 0.f) || reach_tol(p, v4, d)) return 0;
+    expand(p, v4);
+  }
+  // penetration: expand towards the boundary
+  for (int it = 0;; it++) {
+    float d[3];
+    portal_dir(p, d);
+    MSup v4;
+    P.sup(d, v4);
+    if (reach_tol(p, v4, d) || it > MPR_ITERS) {
+      float w[3];
+      closest_tri(p[1].v, p[2].v, p[3].v, w);
+      depth = sqrtf(dot3(w, w));
+      if (fz(depth)) return 0;
+      const float inv = 1.f / depth;
+      dir[0] = w[0] * inv, dir[1] = w[1] * inv, dir[2] = w[2] * inv;
+      portal_pos(p, pos);
+      return 1;
+    }
+    expand(p, v4);
+  }
+}
+
+// ------------------------------------------------------------- primitives
+DEVI int emit(const ConLds& C, int& ncon, int& status, int pair, float dist, const float pos[3],
+              const float n[3]) {
+  if (ncon >= SIM_MAXCON) {
+    status |= SIM_ST_CONOVERFLOW;
+    return 0;
+  }
+  C.dist(ncon) = dist;
+#pragma unroll
+  for (int k = 0; k < 3; k++) C.pos(ncon, k) = pos[k], C.n(ncon, k) = n[k];
+  C.set_pair(ncon, pair);
+  ncon++;
+  return 1;
+}
+
+DEVI void plane_box(const DModel& m, int gp, int gb, const GeomPose& Pp, const GeomPose& Pb,
+                    const ConLds& C, int& ncon, int& status, int pair) {
+  const float n[3] = {Pp.R[2], Pp.R[5], Pp.R[8]};
+  int cnt = 0;
+  for (int i = 0; i < 8 && cnt < 4; i++) {
+    const float l[3] = {(i & 1 ? 1.f : -1.f) * m.geom_size[gb][0], (i & 2 ? 1.f : -1.f) * m.geom_size[gb][1],
+                        (i & 4 ? 1.f : -1.f) * m.geom_size[gb][2]};
+    float w[3], rel[3];
+    mv(w, Pb.R, l);
+    const float p[3] = {Pb.p[0] + w[0], Pb.p[1] + w[1], Pb.p[2] + w[2]};
+    sub(rel, p, Pp.p);
+    const float dist = dot3(rel, n);
+    if (dist < 0.f) {
+      const float pos[3] = {p[0] - 0.5f * dist * n[0], p[1] - 0.5f * dist * n[1], p[2] - 0.5f * dist * n[2]};
+      emit(C, ncon, status, pair, dist, pos, n);
+      cnt++;
+    }
+  }
+}
+
+DEVI void plane_convex(const DModel& m, int gp, int g, const GeomPose& Pp, const GeomPose& Pg,
+                       const ConLds& C, int& ncon, int& status, int pair) {
+  const float n[3] = {Pp.R[2], Pp.R[5], Pp.R[8]};
+  const float nn[3] = {-n[0], -n[1], -n[2]};
+  float p[3], rel[3];
+  support(m, g, Pg, nn, p);
+  sub(rel, p, Pp.p);
+  const float dist = dot3(rel, n);
+  if (dist >= 0.f) return;
+  const float pos[3] = {p[0] - 0.5f * dist * n[0], p[1] - 0.5f * dist * n[1], p[2] - 0.5f * dist * n[2]};
+  emit(C, ncon, status, pair, dist, pos, n);
+}
+
+DEVI int clip_poly(const float in[][3], int n, float out[][3], const float o[3], const float a[3], float lim) {
+  int k = 0;
+  for (int i = 0; i < n; i++) {
+    const float* P = in[i];
+    const float* Q = in[(i + 1) % n];
+    float rp[3], rq[3];
+    sub(rp, P, o);
+    sub(rq, Q, o);
+    const float sp = dot3(rp, a) - lim, sq = dot3(rq, a) - lim;
+    if (sp <= 0.f) {
+      out[k][0] = P[0], out[k][1] = P[1], out[k][2] = P[2];
+      k++;
+    }
+    if ((sp < 0.f && sq > 0.f) || (sp > 0.f && sq < 0.f)) {
+      const float t = sp / (sp - sq);
+      out[k][0] = P[0] + t * (Q[0] - P[0]), out[k][1] = P[1] + t * (Q[1] - P[1]),
+      out[k][2] = P[2] + t * (Q[2] - P[2]);
+      k++;
+    }
+  }
+  return k;
+}
+
+DEVI void box_box(const DModel& m, int g1, int g2, const GeomPose& P1, const GeomPose& P2,
+                  const ConLds& C, int& ncon, int& status, int pair) {
+  const float *h1 = m.geom_size[g1], *h2 = m.geom_size[g2];
+  float A[3][3], B[3][3], t[3];
+#pragma unroll
+  for (int k = 0; k < 3; k++)
+#pragma unroll
+    for (int e = 0; e < 3; e++) A[k][e] = P1.R[3 * e + k], B[k][e] = P2.R[3 * e + k];
+  sub(t, P2.p, P1.p);
+  float best = 3.0e38f, bn[3] = {0, 0, 0};
+  int bcode = -1;
+  for (int code = 0; code < 15; code++) {
+    float L[3];
+    if (code < 3)
+      L[0] = A[code][0], L[1] = A[code][1], L[2] = A[code][2];
+    else if (code < 6)
+      L[0] = B[code - 3][0], L[1] = B[code - 3][1], L[2] = B[code - 3][2];
+    else
+      cross(L, A[(code - 6) / 3], B[(code - 6) % 3]);
+    const float ln = sqrtf(dot3(L, L));
+    if (ln < 1e-6f) continue;
+    L[0] /= ln, L[1] /= ln, L[2] /= ln;
+    float r1 = 0.f, r2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < 3; k++) r1 += h1[k] * fabsf(dot3(A[k], L)), r2 += h2[k] * fabsf(dot3(B[k], L));
+    const float tl = dot3(t, L);
+    const float ov = r1 + r2 - fabsf(tl);
+    if (ov < 0.f) return;
+    const float score = code < 6 ? ov : ov * 1.05f + 1e-9f;
+    if (score < best) {
+      best = score;
+      bcode = code;
+      const float sg = tl < 0.f ? -1.f : 1.f;
+      bn[0] = sg * L[0], bn[1] = sg * L[1], bn[2] = sg * L[2];
+    }
+  }
+  if (bcode < 0) return;
+  if (bcode < 6) {
+    const bool ref1 = bcode < 3;
+    const int fa = ref1 ? bcode : bcode - 3;
+    const float* cr = ref1 ? P1.p : P2.p;
+    const float* ci = ref1 ? P2.p : P1.p;
+    const float(*Ar)[3] = ref1 ? A : B;
+    const float(*Ai)[3] = ref1 ? B : A;
+    const float* hr = ref1 ? h1 : h2;
+    const float* hi = ref1 ? h2 : h1;
+    float nr[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) nr[k] = ref1 ? bn[k] : -bn[k];
+    float fc[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) fc[k] = cr[k] + nr[k] * hr[fa];
+    int ia = 0;
+    float bd = 0.f;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      const float dd = fabsf(dot3(Ai[k], nr));
+      if (dd > bd) bd = dd, ia = k;
+    }
+    const float s = dot3(Ai[ia], nr) > 0.f ? -1.f : 1.f;
+    const int u = (ia + 1) % 3, v = (ia + 2) % 3;
+    float poly[16][3], tmp[16][3];
+    const float su[4] = {1, -1, -1, 1}, sv[4] = {1, 1, -1, -1};
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+#pragma unroll
+      for (int k = 0; k < 3; k++)
+        poly[q][k] = ci[k] + s * hi[ia] * Ai[ia][k] + su[q] * hi[u] * Ai[u][k] + sv[q] * hi[v] * Ai[v][k];
+    int n = 4;
+    const int ra = (fa + 1) % 3, rb = (fa + 2) % 3;
+    float na[3];
+    n = clip_poly(poly, n, tmp, fc, Ar[ra], hr[ra]);
+    na[0] = -Ar[ra][0], na[1] = -Ar[ra][1], na[2] = -Ar[ra][2];
+    n = clip_poly(tmp, n, poly, fc, na, hr[ra]);
+    n = clip_poly(poly, n, tmp, fc, Ar[rb], hr[rb]);
+    na[0] = -Ar[rb][0], na[1] = -Ar[rb][1], na[2] = -Ar[rb][2];
+    n = clip_poly(tmp, n, poly, fc, na, hr[rb]);
+    float dep[16];
+    int idx[16], mcnt = 0;
+    for (int q = 0; q < n; q++) {
+      float rel[3];
+      sub(rel, poly[q], fc);
+      const float sd = dot3(rel, nr);
+      if (sd < 0.f) dep[mcnt] = sd, idx[mcnt] = q, mcnt++;
+    }
+    for (int a = 1; a < mcnt; a++)
+      for (int b = a; b > 0 && dep[b] < dep[b - 1]; b--) {
+        const float td = dep[b];
+        dep[b] = dep[b - 1], dep[b - 1] = td;
+        const int ti = idx[b];
+        idx[b] = idx[b - 1], idx[b - 1] = ti;
+      }
+    for (int q = 0; q < mcnt && q < 4; q++) {
+      const float* pp = poly[idx[q]];
+      const float pos[3] = {pp[0] - 0.5f * dep[q] * nr[0], pp[1] - 0.5f * dep[q] * nr[1],
+                            pp[2] - 0.5f * dep[q] * nr[2]};
+      emit(C, ncon, status, pair, dep[q], pos, bn);
+    }
+    return;
+  }
+  // edge-edge
+  const int ea = (bcode - 6) / 3, eb = (bcode - 6) % 3;
+  float p1[3] = {P1.p[0], P1.p[1], P1.p[2]}, p2[3] = {P2.p[0], P2.p[1], P2.p[2]};
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    if (k != ea) {
+      const float sg = dot3(A[k], bn) > 0.f ? 1.f : -1.f;
+#pragma unroll
+      for (int e = 0; e < 3; e++) p1[e] += sg * h1[k] * A[k][e];
+    }
+    if (k != eb) {
+      const float sg = dot3(B[k], bn) > 0.f ? -1.f : 1.f;
+#pragma unroll
+      for (int e = 0; e < 3; e++) p2[e] += sg * h2[k] * B[k][e];
+    }
+  }
+  float r[3];
+  sub(r, p1, p2);
+  const float b = dot3(A[ea], B[eb]), c = dot3(A[ea], r), f = dot3(B[eb], r);
+  const float den = 1.f - b * b;
+  float sp = den > 1e-12f ? (b * f - c) / den : 0.f;
+  float tp = b * sp + f;
+  sp = fminf(fmaxf(sp, -h1[ea]), h1[ea]);
+  tp = fminf(fmaxf(tp, -h2[eb]), h2[eb]);
+  float pos[3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) pos[k] = 0.5f * (p1[k] + sp * A[ea][k] + p2[k] + tp * B[eb][k]);
+  emit(C, ncon, status, pair, -best / 1.05f, pos, bn);
+}
+
+// mj_collision for one lane: stage geom poses, walk the pair list
+template <int NA, int NF>
+DEVI int collide(Sim<NA, NF>& S, const GeomLds& G, const ConLds& C) {
+  const DModel& m = *S.mp;
+  constexpr int NB = Sim<NA, NF>::NB;
+  for (int g = 0; g < m.ngeom; g++) {
+    const int b = m.geom_bodyid[g];  // wave-uniform
+    float bp[3] = {0, 0, 0}, bR[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+#pragma unroll
+    for (int k = 1; k < NB; k++)
+      if (k == b) {
+#pragma unroll
+        for (int e = 0; e < 3; e++) bp[e] = S.xpos[k][e];
+#pragma unroll
+        for (int e = 0; e < 9; e++) bR[e] = S.xmat[k][e];
+      }
+    const float gp[3] = {m.geom_pos[g][0], m.geom_pos[g][1], m.geom_pos[g][2]};
+    float w[3], R[9];
+    mv(w, bR, gp);
+    mm(R, bR, m.geom_mat[g]);
+#pragma unroll
+    for (int e = 0; e < 3; e++) G.pos(g, e) = bp[e] + w[e];
+#pragma unroll
+    for (int e = 0; e < 9; e++) G.R(g, e) = R[e];
+  }
+  int ncon = 0;
+  for (int p = 0; p < m.npair; p++) {
+    const int g1 = m.pair_geom1[p], g2 = m.pair_geom2[p];
+    const int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
+    GeomPose P1, P2;
+    load_pose(G, g1, P1);
+    load_pose(G, g2, P2);
+    if (m.geom_rbound[g1] > 0.f && m.geom_rbound[g2] > 0.f) {
+      float c1[3], c2[3], r[3];
+      geom_center(m, g1, P1, c1);
+      geom_center(m, g2, P2, c2);
+      sub(r, c1, c2);
+      const float mg = m.pair_margin[p];
+      const float rr = m.geom_rbound[g1] + m.geom_rbound[g2] + mg;
+      if (dot3(r, r) > rr * rr) continue;
+      bool sep = false;
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        const float e1 = fabsf(P1.R[3 * k]) * m.geom_half[g1][0] + fabsf(P1.R[3 * k + 1]) * m.geom_half[g1][1] +
+                         fabsf(P1.R[3 * k + 2]) * m.geom_half[g1][2];
+        const float e2 = fabsf(P2.R[3 * k]) * m.geom_half[g2][0] + fabsf(P2.R[3 * k + 1]) * m.geom_half[g2][1] +
+                         fabsf(P2.R[3 * k + 2]) * m.geom_half[g2][2];
+        sep |= fabsf(r[k]) > e1 + e2 + mg;
+      }
+      if (sep) continue;
+    }
+    if (t1 == SIM_GEOM_PLANE) {
+      if (t2 == SIM_GEOM_BOX)
+        plane_box(m, g1, g2, P1, P2, C, ncon, S.status, p);
+      else if (t2 == SIM_GEOM_MESH)
+        plane_convex(m, g1, g2, P1, P2, C, ncon, S.status, p);
+      continue;
+    }
+    if (t1 == SIM_GEOM_BOX && t2 == SIM_GEOM_BOX) {
+      box_box(m, g1, g2, P1, P2, C, ncon, S.status, p);
+      continue;
+    }
+    MPair mp{m, g1, g2, P1, P2};
+    float depth, dir[3], pos[3];
+    if (mpr(mp, depth, dir, pos)) emit(C, ncon, S.status, p, -depth, pos, dir);
+  }
+  return ncon;
+}
+
+}  // namespace soarm

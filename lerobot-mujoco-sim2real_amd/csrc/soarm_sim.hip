@@ -1,0 +1,643 @@
+// soarm_sim.hip — C ABI (include/soarm_sim.h) + kernels of the MI355X batched
+// SO-ARM101 simulator.  Build: hipcc --offload-arch=gfx950 -O3 -shared -fPIC.
+//
+//   k_step   : ctrl[:nact] = action; frame_skip x mj_step; obs     (SOARM101_Env.py:108-142)
+//   k_reset  : mj_resetData + init qpos/qvel + mj_forward + obs     (SOARM101_Env.py:77-106)
+//   k_observe: mj_kinematics + _get_state                           (SOARM101_Env.py:69-75)
+//   k_ik     : batched damped-least-squares site IK                 (control/TrajectoryGenerator.py:96-107)
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+#include "../../include/soarm_sim.h"
+#include "soarm_collide.h"
+#include "soarm_pgs.h"
+
+using namespace soarm;
+
+// ------------------------------------------------------------------ errors
+static thread_local std::string g_err;
+static int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+#define HIPCHECK(x)                                                                   \
+  do {                                                                                \
+    hipError_t e_ = (x);                                                              \
+    if (e_ != hipSuccess) return fail(SIM_E_HIP, std::string(#x ": ") + hipGetErrorString(e_)); \
+  } while (0)
+
+struct sim_model {
+  sim_model_desc desc;
+  DModel dm;  // host copy; hull pointers filled per batch
+  std::vector<float4> hull_vert;
+  std::vector<int32_t> hull_adr, hull_adj;
+  int na = 0, nf = 0;
+};
+
+struct sim_batch {
+  const sim_model* model = nullptr;
+  int n = 0, device = 0;
+  DModel* d_model = nullptr;
+  float4* d_hv = nullptr;
+  int32_t *d_hadr = nullptr, *d_hadj = nullptr;
+  float* d_scratch = nullptr;  // contact rows, [slot][env]
+  size_t scratch_floats = 0;
+  sim_params params{nullptr, nullptr, nullptr};
+};
+
+// ------------------------------------------------------------- Philox4x32-10
+struct u4 {
+  uint32_t x, y, z, w;
+};
+__host__ __device__ inline u4 philox(u4 c, uint32_t k0, uint32_t k1) {
+  for (int r = 0; r < 10; r++) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
+    const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    c = u4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+__host__ __device__ inline float u01(uint32_t x) { return (float)(x >> 8) * (1.0f / 16777216.0f); }
+
+// -------------------------------------------------------------------- kernels
+template <int NA, int NF>
+DEVI void load_state(Sim<NA, NF>& S, const sim_state& st, int n, int e) {
+  constexpr int NQ = Sim<NA, NF>::NQ, NV = Sim<NA, NF>::NV;
+#pragma unroll
+  for (int i = 0; i < NQ; i++) S.qpos[i] = st.qpos[(size_t)i * n + e];
+#pragma unroll
+  for (int i = 0; i < NV; i++) {
+    S.qvel[i] = st.qvel[(size_t)i * n + e];
+    S.warm[i] = st.qacc_warmstart[(size_t)i * n + e];
+  }
+#pragma unroll
+  for (int i = 0; i < NA; i++) S.ctrl[i] = (i < S.mp->nu) ? st.ctrl[(size_t)i * n + e] : 0.f;
+  S.status = st.status[e];
+}
+template <int NA, int NF>
+DEVI void store_state(const Sim<NA, NF>& S, const sim_state& st, int n, int e) {
+  constexpr int NQ = Sim<NA, NF>::NQ, NV = Sim<NA, NF>::NV;
+#pragma unroll
+  for (int i = 0; i < NQ; i++) st.qpos[(size_t)i * n + e] = S.qpos[i];
+#pragma unroll
+  for (int i = 0; i < NV; i++) {
+    st.qvel[(size_t)i * n + e] = S.qvel[i];
+    st.qacc_warmstart[(size_t)i * n + e] = S.warm[i];
+  }
+#pragma unroll
+  for (int i = 0; i < NA; i++)
+    if (i < S.mp->nu) st.ctrl[(size_t)i * n + e] = S.ctrl[i];
+  st.status[e] = S.status;
+}
+template <int NA, int NF>
+DEVI void write_obs(const Sim<NA, NF>& S, float* obs, int e) {
+  constexpr int NQ = Sim<NA, NF>::NQ;
+  const int no = 3 + S.mp->obs_nq;
+  float* o = obs + (size_t)e * no;
+  o[0] = S.ee[0], o[1] = S.ee[1], o[2] = S.ee[2];
+  for (int k = 0; k < S.mp->obs_nq; k++) {
+    const int a = S.mp->obs_qadr[k];
+    float v = 0.f;
+#pragma unroll
+    for (int i = 0; i < NQ; i++)
+      if (i == a) v = S.qpos[i];
+    o[3 + k] = v;
+  }
+}
+
+// one mj_forward (position + velocity + acceleration stages)
+template <int NA, int NF, bool CON>
+DEVI int forward(Sim<NA, NF>& S, const GeomLds& G, const ConLds& C, const ContactRows<NA, NF>& cr) {
+  S.kinematics();
+  S.com_crb();
+  S.factor();
+  int ncon = 0;
+  if constexpr (CON) ncon = collide<NA, NF>(S, G, C);
+  S.smooth_forces();
+  solve_constraints<NA, NF, CON>(S, C, ncon, cr);
+  return ncon;
+}
+
+template <int NA, int NF, bool CON>
+__global__ __launch_bounds__(64) void k_step(const DModel* __restrict__ dm, int n, int nsub,
+                                             sim_state st, const float* __restrict__ action,
+                                             float* __restrict__ obs, sim_params pp,
+                                             float* __restrict__ scratch) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const DModel& m = *dm;
+  Sim<NA, NF> S(dm, pp.mass_scale ? pp.mass_scale[e] : 1.f, pp.friction ? pp.friction[e] : -1.f,
+                pp.damping_scale ? pp.damping_scale[e] : 1.f);
+  load_state(S, st, n, e);
+  if (action) {
+#pragma unroll
+    for (int k = 0; k < NA; k++)
+      if (k < m.nact) S.ctrl[k] = action[(size_t)e * m.nact + k];
+  }
+  __shared__ float s_geom[CON ? CON_MAXG * 12 : 1][64];
+  __shared__ float s_con[CON ? SIM_MAXCON * 8 : 1][64];
+  const GeomLds G{s_geom, (int)threadIdx.x};
+  const ConLds C{s_con, (int)threadIdx.x};
+  ContactRows<NA, NF> cr{scratch + e, n};
+  float ncon_acc = 0.f;
+  for (int s = 0; s < nsub; s++) {
+    S.relaunder();
+    S.check_state();
+    ncon_acc += forward<NA, NF, CON>(S, G, C, cr);
+    if (S.acc_bad()) {
+      S.soft_reset(SIM_ST_BADQACC);
+      forward<NA, NF, CON>(S, G, C, cr);
+    }
+    S.integrate();
+  }
+  store_state(S, st, n, e);
+  if (st.ncon) st.ncon[e] += ncon_acc;
+  if (obs) write_obs(S, obs, e);
+}
+
+template <int NA, int NF>
+__global__ __launch_bounds__(64) void k_reset(const DModel* __restrict__ dm, int n, sim_state st,
+                                              const float* __restrict__ init_qpos,
+                                              const float* __restrict__ init_qvel,
+                                              const float* __restrict__ extra_qpos, uint32_t k0,
+                                              uint32_t k1, long long env_offset,
+                                              const uint8_t* __restrict__ mask,
+                                              float* __restrict__ obs) {
+  constexpr int NQ = Sim<NA, NF>::NQ, NV = Sim<NA, NF>::NV;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  if (mask && !mask[e]) return;
+  const DModel& m = *dm;
+  Sim<NA, NF> S(dm, 1.f, -1.f, 1.f);
+#pragma unroll
+  for (int i = 0; i < NQ; i++) S.qpos[i] = extra_qpos ? extra_qpos[(size_t)i * n + e] : m.qpos0[i];
+#pragma unroll
+  for (int i = 0; i < NV; i++) S.qvel[i] = S.warm[i] = 0.f;
+#pragma unroll
+  for (int i = 0; i < NA; i++) S.ctrl[i] = 0.f;
+  S.status = 0;
+  // SOARM101_Env.py:90-99: qpos[joint_ids] = U(-0.3, 0.3) (or options), qvel[joint_ids] = 0 (or options)
+  const unsigned long long gid = (unsigned long long)(env_offset + e);
+  u4 r0 = philox(u4{(uint32_t)gid, (uint32_t)(gid >> 32), 0u, 0u}, k0, k1);
+  u4 r1 = philox(u4{(uint32_t)gid, (uint32_t)(gid >> 32), 1u, 0u}, k0, k1);
+  const uint32_t rr[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+  for (int k = 0; k < m.obs_nq; k++) {
+    const int a = m.obs_qadr[k];  // arm joint: qpos address == dof address
+    const float qv = init_qpos ? init_qpos[(size_t)k * n + e] : -0.3f + 0.6f * u01(rr[k & 7]);
+    const float vv = init_qvel ? init_qvel[(size_t)k * n + e] : 0.f;
+#pragma unroll
+    for (int i = 0; i < NQ; i++)
+      if (i == a) S.qpos[i] = qv;
+#pragma unroll
+    for (int i = 0; i < NV; i++)
+      if (i == a) S.qvel[i] = vv;
+  }
+  S.kinematics();
+  store_state(S, st, n, e);
+  if (st.ncon) st.ncon[e] = 0.f;
+  if (obs) write_obs(S, obs, e);
+}
+
+template <int NA, int NF>
+__global__ __launch_bounds__(64) void k_observe(const DModel* __restrict__ dm, int n, sim_state st,
+                                                float* __restrict__ obs) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  Sim<NA, NF> S(dm, 1.f, -1.f, 1.f);
+  load_state(S, st, n, e);
+  S.kinematics();
+  write_obs(S, obs, e);
+}
+
+// ------------------------------------------------------------ DLS site IK
+// dm_control qpos_from_site_pose, position only (target_quat=None at
+// Koopman_MPC.py:252), joints = the first `ndof` arm hinges:
+//   err = target - site_xpos;  stop (success) if |err| < tol
+//   J = site jacobian (3 x ndof);  reg = strength if |err| > threshold else 0
+//   dq = J' (J J' + reg I)^-1 err  (== (J'J + reg I)^-1 J' err; reg = 0 -> min-norm)
+//   stop (fail) if |err| / |dq| > progress_thresh;  clip |dq| <= max_update_norm
+//   q += dq  (hinges: mj_integratePos is plain addition; joint ranges not enforced)
+template <int NA>
+__global__ __launch_bounds__(64) void k_ik(const DModel* __restrict__ dm, int n,
+                                           const float* __restrict__ target, float* __restrict__ q,
+                                           int32_t* __restrict__ ok, int32_t* __restrict__ iters,
+                                           sim_ik_opts o) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const DModel& m = *dm;
+  Sim<NA, 0> S(dm, 1.f, -1.f, 1.f);
+#pragma unroll
+  for (int i = 0; i < NA; i++) S.qpos[i] = q[(size_t)i * n + e];
+  const float tx = target[3 * (size_t)e], ty = target[3 * (size_t)e + 1], tz = target[3 * (size_t)e + 2];
+  int success = 0, it = 0;
+  for (; it < o.max_steps; it++) {
+    S.kinematics();
+    const float err[3] = {tx - S.ee[0], ty - S.ee[1], tz - S.ee[2]};
+    const float en = sqrtf(dot3(err, err));
+    if (en < (float)o.tol) {
+      success = 1;
+      break;
+    }
+    // site jacobian: hinge i moves the site iff its body is an ancestor of the site body
+    const int sb = m.site_bodyid[m.obs_site];
+    float J[3][NA];
+#pragma unroll
+    for (int i = 0; i < NA; i++) {
+      float r[3] = {S.ee[0] - S.anchor[i][0], S.ee[1] - S.anchor[i][1], S.ee[2] - S.anchor[i][2]};
+      float c[3];
+      cross(c, S.axis[i], r);
+      const bool use = (i < o.ndof) && (sb >= i + 2);
+#pragma unroll
+      for (int k = 0; k < 3; k++) J[k][i] = use ? c[k] : 0.f;
+    }
+    const float reg = en > (float)o.regularization_threshold ? (float)o.regularization_strength : 0.f;
+    // A = J J' + reg I (3x3 SPD), solve A y = err, dq = J' y
+    float A[6];
+    A[0] = reg, A[1] = 0, A[2] = reg, A[3] = 0, A[4] = 0, A[5] = reg;  // packed lower: 00,10,11,20,21,22
+#pragma unroll
+    for (int i = 0; i < NA; i++) {
+      A[0] += J[0][i] * J[0][i];
+      A[1] += J[1][i] * J[0][i];
+      A[2] += J[1][i] * J[1][i];
+      A[3] += J[2][i] * J[0][i];
+      A[4] += J[2][i] * J[1][i];
+      A[5] += J[2][i] * J[2][i];
+    }
+    float Ad[3], y[3];
+    ldl_factor<3>(A, Ad);
+    ldl_solve<3>(A, Ad, y, err);
+    float dq[NA], dn2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NA; i++) {
+      dq[i] = J[0][i] * y[0] + J[1][i] * y[1] + J[2][i] * y[2];
+      dn2 += dq[i] * dq[i];
+    }
+    const float dn = sqrtf(dn2);
+    if (en / dn > (float)o.progress_thresh) break;
+    if (dn > (float)o.max_update_norm) {
+      const float s = (float)o.max_update_norm / dn;
+#pragma unroll
+      for (int i = 0; i < NA; i++) dq[i] *= s;
+    }
+#pragma unroll
+    for (int i = 0; i < NA; i++) S.qpos[i] += dq[i];
+  }
+#pragma unroll
+  for (int i = 0; i < NA; i++) q[(size_t)i * n + e] = S.qpos[i];
+  if (ok) ok[e] = success;
+  if (iters) iters[e] = it;
+}
+
+// ------------------------------------------------------------- dispatch
+// Supported topologies: arm chain of NA=6 hinges, NF in {0, 1} free bodies.
+template <class F>
+static void dispatch_nf(int nf, F&& f) {
+  if (nf == 0)
+    f(std::integral_constant<int, 0>{});
+  else
+    f(std::integral_constant<int, 1>{});
+}
+
+static inline dim3 grid_for(int n) { return dim3((n + 63) / 64); }
+
+// ------------------------------------------------------------------ model
+static float host_impedance(const double* si, double pos, double margin) {
+  double dmin = std::fmin(std::fmax(si[0], 1e-4), 0.9999), dmax = std::fmin(std::fmax(si[1], 1e-4), 0.9999);
+  if (dmin == dmax || si[2] <= 1e-15) return 0.5 * (dmin + dmax);
+  double x = std::fabs((pos - margin) / si[2]);
+  if (x >= 1) return dmax;
+  if (x <= 0) return dmin;
+  double y = si[4] == 1 ? x
+             : x <= si[3] ? std::pow(x, si[4]) / std::pow(si[3], si[4] - 1)
+                          : 1 - std::pow(1 - x, si[4]) / std::pow(1 - si[3], si[4] - 1);
+  return dmin + y * (dmax - dmin);
+}
+static void host_KB(const double* solref, const double* solimp, double timestep, float KB[2]) {
+  double dmax = std::fmin(std::fmax(solimp[1], 1e-4), 0.9999);
+  if (solref[0] > 0) {
+    double tc = std::fmax(solref[0], 2 * timestep), dr = solref[1];
+    KB[0] = (float)(1.0 / (dmax * dmax * tc * tc * dr * dr));
+    KB[1] = (float)(2.0 / (dmax * tc));
+  } else {
+    KB[0] = (float)(-solref[0] / (dmax * dmax));
+    KB[1] = (float)(-solref[1] / dmax);
+  }
+}
+static void quat2mat_h(float R[9], const double* q) {
+  double w = q[0], x = q[1], y = q[2], z = q[3];
+  double n = std::sqrt(w * w + x * x + y * y + z * z);
+  w /= n, x /= n, y /= n, z /= n;
+  R[0] = 1 - 2 * (y * y + z * z), R[1] = 2 * (x * y - w * z), R[2] = 2 * (x * z + w * y);
+  R[3] = 2 * (x * y + w * z), R[4] = 1 - 2 * (x * x + z * z), R[5] = 2 * (y * z - w * x);
+  R[6] = 2 * (x * z - w * y), R[7] = 2 * (y * z + w * x), R[8] = 1 - 2 * (x * x + y * y);
+}
+
+static int validate_and_build(const sim_model_desc& d, sim_model* M) {
+  // topology: world, welded base, serial hinge chain, then free bodies under the world
+  if (d.nbody < 3 || d.nbody > SIM_MAXBODY) return fail(SIM_E_MODEL, "nbody out of range");
+  if (d.body_parentid[1] != 0 || d.body_jntnum[1] != 0)
+    return fail(SIM_E_MODEL, "body 1 must be a welded base under the world");
+  int na = 0;
+  int b = 2;
+  for (; b < d.nbody; b++) {
+    if (d.body_parentid[b] != b - 1) break;
+    if (d.body_jntnum[b] != 1 || d.jnt_type[d.body_jntadr[b]] != SIM_JNT_HINGE)
+      return fail(SIM_E_MODEL, "chain bodies must carry exactly one hinge");
+    int j = d.body_jntadr[b];
+    if (j != na || d.jnt_dofadr[j] != na || d.jnt_qposadr[j] != na)
+      return fail(SIM_E_MODEL, "chain hinge addresses must equal their chain index");
+    na++;
+  }
+  int nf = 0;
+  for (; b < d.nbody; b++) {
+    if (d.body_parentid[b] != 0 || d.body_jntnum[b] != 1 ||
+        d.jnt_type[d.body_jntadr[b]] != SIM_JNT_FREE)
+      return fail(SIM_E_MODEL, "bodies after the chain must be free bodies under the world");
+    int j = d.body_jntadr[b];
+    if (d.jnt_dofadr[j] != na + 6 * nf || d.jnt_qposadr[j] != na + 7 * nf)
+      return fail(SIM_E_MODEL, "free joint addresses out of order");
+    nf++;
+  }
+  if (na != 6 || nf > 1) return fail(SIM_E_MODEL, "kernels are compiled for a 6-hinge arm + <=1 free body");
+  if (d.nv != na + 6 * nf || d.nq != na + 7 * nf) return fail(SIM_E_MODEL, "nq/nv mismatch");
+  if (d.nu > na) return fail(SIM_E_MODEL, "more actuators than arm hinges");
+  for (int a = 0; a < d.nu; a++)
+    if (d.actuator_trnid[a] != a) return fail(SIM_E_MODEL, "actuator a must drive joint a");
+  for (int i = na; i < d.nv; i++)
+    if (d.dof_frictionloss[i] > 0) return fail(SIM_E_MODEL, "frictionloss on free dofs unsupported");
+  if (d.nact > na || d.obs_nq > na) return fail(SIM_E_MODEL, "obs/act larger than the arm");
+  for (int k = 0; k < d.obs_nq; k++)
+    if (d.obs_qadr[k] >= na) return fail(SIM_E_MODEL, "observed joints must be arm hinges");
+  for (int g = 0; g < d.ngeom; g++) {
+    int t = d.geom_type[g];
+    if (t != SIM_GEOM_PLANE && t != SIM_GEOM_BOX && t != SIM_GEOM_MESH)
+      return fail(SIM_E_MODEL, "geom type unsupported by the kernels");
+    if (d.geom_condim[g] != 3) return fail(SIM_E_MODEL, "only condim 3 contacts supported");
+  }
+  if (!d.disable_contact && d.ngeom > CON_MAXG) return fail(SIM_E_MODEL, "too many collidable geoms");
+  M->na = na;
+  M->nf = nf;
+
+  DModel& m = M->dm;
+  std::memset(&m, 0, sizeof(m));
+  m.nq = d.nq, m.nv = d.nv, m.nu = d.nu, m.ngeom = d.ngeom, m.npair = d.npair, m.nact = d.nact;
+  m.obs_site = d.obs_site, m.obs_nq = d.obs_nq;
+  for (int k = 0; k < SIM_MAXOBSQ; k++) m.obs_qadr[k] = d.obs_qadr[k];
+  m.iterations = d.iterations, m.disable_contact = d.disable_contact;
+  bool anyd = false;
+  for (int i = 0; i < d.nv; i++) anyd |= d.dof_damping[i] > 0;
+  m.eulerdamp = (!d.disable_eulerdamp && anyd) ? 1 : 0;
+  m.nhullvert = d.nhullvert;
+  m.timestep = (float)d.timestep, m.impratio = (float)d.impratio;
+  m.tolerance = (float)d.tolerance;
+  for (int k = 0; k < 3; k++) m.gravity[k] = (float)d.gravity[k];
+  for (int b2 = 0; b2 < d.nbody; b2++) {
+    for (int k = 0; k < 3; k++) {
+      m.body_pos[b2][k] = (float)d.body_pos[b2][k];
+      m.body_ipos[b2][k] = (float)d.body_ipos[b2][k];
+      m.body_inertia[b2][k] = (float)d.body_inertia[b2][k];
+    }
+    double qn = 0;
+    for (int k = 0; k < 4; k++) qn += d.body_quat[b2][k] * d.body_quat[b2][k];
+    for (int k = 0; k < 4; k++) m.body_quat[b2][k] = (float)(d.body_quat[b2][k] / std::sqrt(qn));
+    quat2mat_h(m.body_imat[b2], d.body_iquat[b2]);
+    m.body_mass[b2] = (float)d.body_mass[b2];
+    m.body_invweight0[b2][0] = (float)d.body_invweight0[b2][0];
+    m.body_invweight0[b2][1] = (float)d.body_invweight0[b2][1];
+  }
+  for (int j = 0; j < d.njnt; j++) {
+    for (int k = 0; k < 3; k++) {
+      m.jnt_pos[j][k] = (float)d.jnt_pos[j][k];
+      m.jnt_axis[j][k] = (float)d.jnt_axis[j][k];
+    }
+    m.jnt_range[j][0] = (float)d.jnt_range[j][0], m.jnt_range[j][1] = (float)d.jnt_range[j][1];
+    for (int k = 0; k < 5; k++) m.jnt_solimp[j][k] = (float)d.jnt_solimp[j][k];
+    host_KB(d.jnt_solref[j], d.jnt_solimp[j], d.timestep, m.jnt_KB[j]);
+    m.jnt_margin[j] = (float)d.jnt_margin[j];
+    m.jnt_limited[j] = d.jnt_limited[j] && d.jnt_type[j] == SIM_JNT_HINGE;
+  }
+  for (int i = 0; i < d.nq; i++) m.qpos0[i] = (float)d.qpos0[i];
+  for (int i = 0; i < d.nv; i++) {
+    m.dof_armature[i] = (float)d.dof_armature[i];
+    m.dof_damping[i] = (float)d.dof_damping[i];
+    m.dof_frictionloss[i] = (float)d.dof_frictionloss[i];
+    m.dof_invweight0[i] = (float)d.dof_invweight0[i];
+    double imp = host_impedance(d.dof_solimp[i], 0.0, 0.0);
+    m.dof_fricR[i] = (float)std::fmax(1e-15, (1 - imp) * d.dof_invweight0[i] / imp);
+    float KB[2];
+    host_KB(d.dof_solref[i], d.dof_solimp[i], d.timestep, KB);
+    m.dof_fricB[i] = KB[1];
+  }
+  for (int g = 0; g < d.ngeom; g++) {
+    m.geom_type[g] = d.geom_type[g], m.geom_bodyid[g] = d.geom_bodyid[g];
+    m.geom_hulladr[g] = d.geom_hulladr[g], m.geom_hullnum[g] = d.geom_hullnum[g];
+    for (int k = 0; k < 3; k++) {
+      m.geom_pos[g][k] = (float)d.geom_pos[g][k];
+      m.geom_size[g][k] = (float)d.geom_size[g][k];
+      m.geom_center[g][k] = (float)d.geom_aabb[g][k];
+      m.geom_half[g][k] = (float)d.geom_aabb[g][3 + k];
+    }
+    quat2mat_h(m.geom_mat[g], d.geom_quat[g]);
+    m.geom_rbound[g] = (float)d.geom_rbound[g];
+    m.geom_friction[g] = (float)d.geom_friction[g][0];
+  }
+  for (int p = 0; p < d.npair; p++) {
+    int g1 = d.pair_geom1[p], g2 = d.pair_geom2[p];
+    m.pair_geom1[p] = g1, m.pair_geom2[p] = g2;
+    double sr[2], si[5];
+    for (int k = 0; k < 2; k++) sr[k] = 0.5 * (d.geom_solref[g1][k] + d.geom_solref[g2][k]);
+    for (int k = 0; k < 5; k++) {
+      si[k] = 0.5 * (d.geom_solimp[g1][k] + d.geom_solimp[g2][k]);
+      m.pair_solimp[p][k] = (float)si[k];
+    }
+    host_KB(sr, si, d.timestep, m.pair_KB[p]);
+    m.pair_margin[p] = (float)std::fmax(d.geom_margin[g1], d.geom_margin[g2]);
+    m.pair_tran[p] = (float)(d.body_invweight0[d.geom_bodyid[g1]][0] + d.body_invweight0[d.geom_bodyid[g2]][0]);
+    m.pair_friction[p] = (float)std::fmax(d.geom_friction[g1][0], d.geom_friction[g2][0]);
+  }
+  for (int s = 0; s < d.nsite; s++) {
+    m.site_bodyid[s] = d.site_bodyid[s];
+    for (int k = 0; k < 3; k++) m.site_pos[s][k] = (float)d.site_pos[s][k];
+  }
+  for (int a = 0; a < d.nu; a++) {
+    m.act_ctrllimited[a] = d.actuator_ctrllimited[a];
+    m.act_forcelimited[a] = d.actuator_forcelimited[a];
+    m.act_gear[a] = (float)d.actuator_gear[a];
+    m.act_gain[a] = (float)d.actuator_gainprm[a];
+    for (int k = 0; k < 3; k++) m.act_bias[a][k] = (float)d.actuator_biasprm[a][k];
+    for (int k = 0; k < 2; k++) {
+      m.act_ctrlrange[a][k] = (float)d.actuator_ctrlrange[a][k];
+      m.act_forcerange[a][k] = (float)d.actuator_forcerange[a][k];
+    }
+  }
+  return SIM_OK;
+}
+
+// ============================================================== C ABI
+extern "C" {
+
+const char* sim_last_error(void) { return g_err.c_str(); }
+const char* sim_version(void) { return "soarm_sim 0.1.0 gfx950"; }
+
+int sim_model_create(const sim_model_desc* desc, const float* hull_vert, const int32_t* hull_adr,
+                     const int32_t* hull_adj, sim_model** out) {
+  if (!desc || !out) return fail(SIM_E_ARG, "null argument");
+  sim_model* M = new sim_model();
+  M->desc = *desc;
+  int rc = validate_and_build(*desc, M);
+  if (rc) {
+    delete M;
+    return rc;
+  }
+  M->hull_vert.resize(desc->nhullvert);
+  for (int i = 0; i < desc->nhullvert; i++)
+    M->hull_vert[i] = make_float4(hull_vert[3 * i], hull_vert[3 * i + 1], hull_vert[3 * i + 2], 0.f);
+  if (desc->nhullvert) {
+    if (!hull_adr || !hull_adj) {
+      delete M;
+      return fail(SIM_E_ARG, "hull graph missing");
+    }
+    M->hull_adr.assign(hull_adr, hull_adr + desc->nhullvert + 1);
+    M->hull_adj.assign(hull_adj, hull_adj + desc->nhulladj);
+  }
+  *out = M;
+  return SIM_OK;
+}
+
+void sim_model_free(sim_model* m) { delete m; }
+
+int sim_batch_create(const sim_model* m, int n_envs, int device, sim_batch** out) {
+  if (!m || !out || n_envs <= 0) return fail(SIM_E_ARG, "bad argument");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(SIM_E_NODEVICE, "no HIP device");
+  if (device < 0 || device >= ndev) return fail(SIM_E_ARG, "bad device ordinal");
+  HIPCHECK(hipSetDevice(device));
+  sim_batch* B = new sim_batch();
+  B->model = m;
+  B->n = n_envs;
+  B->device = device;
+  DModel dm = m->dm;
+  if (!m->hull_vert.empty()) {
+    HIPCHECK(hipMalloc(&B->d_hv, m->hull_vert.size() * sizeof(float4)));
+    HIPCHECK(hipMemcpy(B->d_hv, m->hull_vert.data(), m->hull_vert.size() * sizeof(float4), hipMemcpyHostToDevice));
+    HIPCHECK(hipMalloc(&B->d_hadr, m->hull_adr.size() * sizeof(int32_t)));
+    HIPCHECK(hipMemcpy(B->d_hadr, m->hull_adr.data(), m->hull_adr.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    HIPCHECK(hipMalloc(&B->d_hadj, m->hull_adj.size() * sizeof(int32_t)));
+    HIPCHECK(hipMemcpy(B->d_hadj, m->hull_adj.data(), m->hull_adj.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  }
+  dm.hull_vert = B->d_hv;
+  dm.hull_adr = B->d_hadr;
+  dm.hull_adj = B->d_hadj;
+  HIPCHECK(hipMalloc(&B->d_model, sizeof(DModel)));
+  HIPCHECK(hipMemcpy(B->d_model, &dm, sizeof(DModel), hipMemcpyHostToDevice));
+  if (!m->desc.disable_contact) {
+    const int nv = m->desc.nv;
+    B->scratch_floats = (size_t)4 * SIM_MAXCON * (2 * nv + 4) * n_envs;
+    HIPCHECK(hipMalloc(&B->d_scratch, B->scratch_floats * sizeof(float)));
+  }
+  *out = B;
+  return SIM_OK;
+}
+
+void sim_batch_free(sim_batch* b) {
+  if (!b) return;
+  (void)hipSetDevice(b->device);
+  (void)hipFree(b->d_model);
+  (void)hipFree(b->d_hv);
+  (void)hipFree(b->d_hadr);
+  (void)hipFree(b->d_hadj);
+  (void)hipFree(b->d_scratch);
+  delete b;
+}
+
+int sim_batch_set_params(sim_batch* b, const sim_params* p) {
+  if (!b) return fail(SIM_E_ARG, "null batch");
+  b->params = p ? *p : sim_params{nullptr, nullptr, nullptr};
+  return SIM_OK;
+}
+
+static int check_state(const sim_batch* b, const sim_state* s) {
+  if (!b || !s) return fail(SIM_E_ARG, "null argument");
+  if (!s->qpos || !s->qvel || !s->qacc_warmstart || !s->ctrl || !s->status)
+    return fail(SIM_E_ARG, "state buffers must all be set");
+  return SIM_OK;
+}
+
+int sim_reset(sim_batch* b, const sim_state* s, const float* init_qpos, const float* init_qvel,
+              const float* extra_qpos, uint64_t seed, int64_t env_offset, const uint8_t* mask,
+              float* obs, void* stream) {
+  if (int rc = check_state(b, s)) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  dispatch_nf(b->model->nf, [&](auto nfc) {
+    constexpr int NA = 6, NF = decltype(nfc)::value;
+    hipLaunchKernelGGL((k_reset<NA, NF>), grid_for(b->n), dim3(64), 0, st,
+                                             b->d_model, b->n, *s, init_qpos, init_qvel, extra_qpos,
+                                             (uint32_t)seed, (uint32_t)(seed >> 32), (long long)env_offset,
+                                             mask, obs);
+  });
+  HIPCHECK(hipGetLastError());
+  return SIM_OK;
+}
+
+int sim_step(sim_batch* b, const sim_state* s, const float* action, int frame_skip, float* obs,
+             void* stream) {
+  if (int rc = check_state(b, s)) return rc;
+  if (frame_skip < 1) return fail(SIM_E_ARG, "frame_skip must be >= 1");
+  hipStream_t st = (hipStream_t)stream;
+  const bool con = !b->model->desc.disable_contact;
+  if (con)
+    dispatch_nf(b->model->nf, [&](auto nfc) {
+    constexpr int NA = 6, NF = decltype(nfc)::value;
+    hipLaunchKernelGGL((k_step<NA, NF, true>), grid_for(b->n), dim3(64), 0, st,
+                                               b->d_model, b->n, frame_skip, *s, action, obs, b->params,
+                                               b->d_scratch);
+  });
+  else
+    dispatch_nf(b->model->nf, [&](auto nfc) {
+    constexpr int NA = 6, NF = decltype(nfc)::value;
+    hipLaunchKernelGGL((k_step<NA, NF, false>), grid_for(b->n), dim3(64), 0, st,
+                                               b->d_model, b->n, frame_skip, *s, action, obs, b->params,
+                                               b->d_scratch);
+  });
+  HIPCHECK(hipGetLastError());
+  return SIM_OK;
+}
+
+int sim_substeps(sim_batch* b, const sim_state* s, int nsub, void* stream) {
+  return sim_step(b, s, nullptr, nsub, nullptr, stream);
+}
+
+int sim_observe(sim_batch* b, const sim_state* s, float* obs, void* stream) {
+  if (int rc = check_state(b, s)) return rc;
+  if (!obs) return fail(SIM_E_ARG, "obs is null");
+  hipStream_t st = (hipStream_t)stream;
+  dispatch_nf(b->model->nf, [&](auto nfc) {
+    constexpr int NA = 6, NF = decltype(nfc)::value;
+    hipLaunchKernelGGL((k_observe<NA, NF>), grid_for(b->n), dim3(64), 0, st,
+                                             b->d_model, b->n, *s, obs);
+  });
+  HIPCHECK(hipGetLastError());
+  return SIM_OK;
+}
+
+int sim_ik_dls(sim_batch* b, const float* target, float* q, int32_t* ok, int32_t* iters,
+               const sim_ik_opts* opts, void* stream) {
+  if (!b || !target || !q || !opts) return fail(SIM_E_ARG, "null argument");
+  if (opts->ndof < 1 || opts->ndof > 6 || opts->max_steps < 0) return fail(SIM_E_ARG, "bad ik options");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL((k_ik<6>), grid_for(b->n), dim3(64), 0, st, b->d_model, b->n, target, q, ok,
+                     iters, *opts);
+  HIPCHECK(hipGetLastError());
+  return SIM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,145 @@
+"""Host-side batch simulator over the C ABI (``include/soarm_sim.h``).
+
+:class:`BatchSim` owns one ``sim_model`` + ``sim_batch`` and the env state as
+caller-owned torch tensors on the GPU (SoA ``[field][env]``).  It is the single
+object the reference-shaped APIs (``SOARM101Env``, ``SOARM101VecEnv``,
+``SOARM101DataGenerator``, ``CartesianTrajectoryGenerator``) drive.  Every call
+is asynchronous on torch's current stream; nothing here falls back to a CPU
+path — if the HIP library or the GPU is missing, construction raises.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import abi
+from .mjcf import SCENE_XML, compile_mjcf
+
+
+def _ptr(t):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+class BatchSim:
+    """`n_envs` SO-ARM101 environments stepped in lockstep on one GPU."""
+
+    def __init__(self, model=None, n_envs=1, device=0, **compile_kw):
+        import torch
+
+        if not torch.cuda.is_available():
+            raise RuntimeError("BatchSim needs a ROCm GPU (torch.cuda.is_available() is False)")
+        self.torch = torch
+        self.cm = model if model is not None else compile_mjcf(SCENE_XML, **compile_kw)
+        self.lib = abi.load_lib()
+        d = self.cm.desc
+        self.n = int(n_envs)
+        self.device = torch.device("cuda", device)
+        self.nq, self.nv, self.nu = d.nq, d.nv, d.nu
+        self.nact, self.obs_dim = d.nact, 3 + d.obs_nq
+        self.frame_skip = max(1, int(round(0.02 / d.timestep)))
+        self._hv = np.ascontiguousarray(self.cm.hull_vert, np.float32)
+        self._hadr = np.ascontiguousarray(self.cm.hull_adr, np.int32)
+        self._hadj = np.ascontiguousarray(self.cm.hull_adj, np.int32)
+        self._model = C.c_void_p()
+        abi.check(self.lib, self.lib.sim_model_create(
+            C.byref(d), self._hv.ctypes.data_as(C.c_void_p), self._hadr.ctypes.data_as(C.c_void_p),
+            self._hadj.ctypes.data_as(C.c_void_p), C.byref(self._model)))
+        self._batch = C.c_void_p()
+        abi.check(self.lib, self.lib.sim_batch_create(self._model, self.n, device, C.byref(self._batch)))
+        f32 = dict(dtype=torch.float32, device=self.device)
+        self.qpos = torch.zeros((self.nq, self.n), **f32)
+        self.qvel = torch.zeros((self.nv, self.n), **f32)
+        self.qacc_warmstart = torch.zeros((self.nv, self.n), **f32)
+        self.ctrl = torch.zeros((self.nu, self.n), **f32)
+        self.status = torch.zeros(self.n, dtype=torch.int32, device=self.device)
+        self.ncon = torch.zeros(self.n, **f32)
+        self.obs = torch.zeros((self.n, self.obs_dim), **f32)
+        self._state = abi.SimState(_ptr(self.qpos), _ptr(self.qvel), _ptr(self.qacc_warmstart),
+                                   _ptr(self.ctrl), _ptr(self.status), _ptr(self.ncon))
+        self._params = None
+
+    # ------------------------------------------------------------------ utils
+    def _stream(self):
+        return C.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _dev(self, x, shape=None):
+        if x is None:
+            return None
+        t = self.torch.as_tensor(x, dtype=self.torch.float32, device=self.device)
+        if shape is not None:
+            t = t.reshape(shape)
+        return t.contiguous()
+
+    def close(self):
+        if getattr(self, "_batch", None):
+            self.lib.sim_batch_free(self._batch)
+            self._batch = None
+        if getattr(self, "_model", None):
+            self.lib.sim_model_free(self._model)
+            self._model = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------- DR params
+    def set_params(self, mass_scale=None, friction=None, damping_scale=None):
+        """Per-env domain randomisation ([n] each, None = nominal)."""
+        self._pm = [self._dev(x, (self.n,)) for x in (mass_scale, friction, damping_scale)]
+        p = abi.SimParams(*[_ptr(x) for x in self._pm])
+        self._params = p
+        abi.check(self.lib, self.lib.sim_batch_set_params(self._batch, C.byref(p)))
+
+    # --------------------------------------------------------------- API calls
+    def reset(self, init_qpos=None, init_qvel=None, extra_qpos=None, seed=0, env_offset=0, mask=None):
+        """mj_resetData + init + mj_forward for masked envs; returns obs [n, obs_dim].
+
+        init_qpos / init_qvel: [n, obs_nq] (row per env) or None (U(-0.3,0.3) from
+        Philox keyed by (seed, env_offset + i); qvel 0).  extra_qpos: [n, nq]."""
+        d = self.cm.desc
+        iq = None if init_qpos is None else self._dev(init_qpos, (self.n, d.obs_nq)).T.contiguous()
+        iv = None if init_qvel is None else self._dev(init_qvel, (self.n, d.obs_nq)).T.contiguous()
+        ex = None if extra_qpos is None else self._dev(extra_qpos, (self.n, self.nq)).T.contiguous()
+        mk = None
+        if mask is not None:
+            mk = self.torch.as_tensor(mask, device=self.device).to(self.torch.uint8).contiguous()
+        self._keep = (iq, iv, ex, mk)
+        abi.check(self.lib, self.lib.sim_reset(self._batch, C.byref(self._state), _ptr(iq), _ptr(iv),
+                                               _ptr(ex), C.c_uint64(seed), C.c_int64(env_offset),
+                                               _ptr(mk), _ptr(self.obs), self._stream()))
+        return self.obs
+
+    def step(self, action, frame_skip=None):
+        """ctrl[:nact] = action ([n, nact]); frame_skip x mj_step; returns obs [n, obs_dim]."""
+        a = self._dev(action, (self.n, self.nact))
+        self._keep_a = a
+        abi.check(self.lib, self.lib.sim_step(self._batch, C.byref(self._state), _ptr(a),
+                                              int(frame_skip or self.frame_skip), _ptr(self.obs),
+                                              self._stream()))
+        return self.obs
+
+    def substeps(self, nsub):
+        abi.check(self.lib, self.lib.sim_substeps(self._batch, C.byref(self._state), int(nsub),
+                                                  self._stream()))
+
+    def observe(self):
+        abi.check(self.lib, self.lib.sim_observe(self._batch, C.byref(self._state), _ptr(self.obs),
+                                                 self._stream()))
+        return self.obs
+
+    def ik(self, target, q=None, tol=1e-6, regularization_threshold=0.1, regularization_strength=1e-2,
+           max_update_norm=2.0, progress_thresh=20.0, max_steps=100, ndof=5):
+        """Batched position-only DLS IK of the observed site.  target [n, 3];
+        q [nq, n] warm start (SoA, modified in place) or None (qpos0)."""
+        t = self._dev(target, (self.n, 3))
+        if q is None:
+            q = self.torch.zeros((self.nq, self.n), dtype=self.torch.float32, device=self.device)
+            q[:] = self._dev(self.cm.qpos0()).reshape(-1, 1)
+        ok = self.torch.zeros(self.n, dtype=self.torch.int32, device=self.device)
+        it = self.torch.zeros(self.n, dtype=self.torch.int32, device=self.device)
+        o = abi.IkOpts(tol, regularization_threshold, regularization_strength, max_update_norm,
+                       progress_thresh, int(max_steps), int(self.cm.desc.obs_site), int(ndof), 0)
+        abi.check(self.lib, self.lib.sim_ik_dls(self._batch, _ptr(t), _ptr(q), _ptr(ok), _ptr(it),
+                                                C.byref(o), self._stream()))
+        return q, ok, it
