@@ -1,0 +1,211 @@
+#!/usr/bin/env python3
+"""bench.py — SO-ARM101 batched simulation throughput on MI355X.
+
+Headline (BASELINE.json ``metric``): env-steps/sec (whole node) at 4096
+SO-ARM101 envs per GPU with contacts (config 3: the build-defined pick scene,
+table + cube, PGS, chirp actions).  One step = one ``SOARM101Env.step()`` for
+every env = 10 physics substeps of 2 ms (``SOARM101_Env.py:39-40,131-132``).
+
+    python bench.py [--gpus N --steps K --warmup W --config contact|nocontact|dr]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+One process per GPU; envs shard by global env id (rank r owns
+[r*n, (r+1)*n)), there is no per-step collective (``scaling: weak``); the
+timed region is bracketed by barrier + synchronize and the max over ranks is
+used.  Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "env-steps/sec (whole node), 4096 SO-ARM101 envs w/ contacts, 1/2/4/8 MI355X"
+PEAK_FP32_TFLOPS = 157.3   # MI355X FP32 vector (= FP32 MFMA) dense peak, MI355X_MICROARCH.md
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--envs", type=int, default=None, help="envs per GPU (default 4096; 8192 for dr)")
+    p.add_argument("--config", default="contact", choices=["contact", "nocontact", "dr"])
+    p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-profile", action="store_true")
+    return p.parse_args()
+
+
+def cpu_baseline(cfg_name, seconds, seed):
+    """The float64 oracle (C restatement of mj_step) on the host cores, bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    from oracle import Oracle
+    from lerobot_mujoco_sim2real_amd import workloads as W
+
+    cfg = W.CONFIGS[cfg_name]
+    cm = W.model(cfg_name)
+    orc = Oracle(cm)
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count()
+    cores = max(1, min(cores, 16))  # the GPU box's CPU share is 16
+    n, T = 256, 10
+    done, t0 = 0, time.perf_counter()
+    chunk = 0
+    while time.perf_counter() - t0 < seconds:
+        ids = np.arange(chunk * n, (chunk + 1) * n)
+        st = orc.new_state(n)
+        q = W.initial_qpos(cm, ids, seed)
+        orc.reset(st, init_qpos=q[:, :5], extra_qpos=q)
+        tab = W.chirp_tables(ids, seed)
+        prm = None
+        if cfg["dr"]:
+            p = W.dr_params(ids, seed)
+            prm = np.stack([p["mass_scale"], p["friction"], p["damping_scale"]], 1).astype(np.float64)
+        rng = np.random.default_rng(chunk)
+        for t in range(T):
+            a = W.chirp_action(tab, t) if cfg["action"] == "chirp" else rng.uniform(-0.5, 0.5, (n, 5))
+            orc.step(st, a, params=prm, nthreads=cores)
+            done += n
+        chunk += 1
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "env-steps/s", "cores": cores, "kind": "port",
+            "sample": f"{done} env-steps ({chunk} chunks of {n} envs x {T} steps, {cfg_name} workload) "
+                      f"of the float64 C oracle, OpenMP over envs, {dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import soarm_pkg  # noqa: F401
+    from lerobot_mujoco_sim2real_amd import build, workloads as W
+    from lerobot_mujoco_sim2real_amd.sim import BatchSim
+
+    build.build()
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://", device_id=dev)
+
+    name = args.config
+    cfg = W.CONFIGS[name]
+    n = args.envs or (8192 if name == "dr" else 4096)
+    ids = np.arange(rank * n, (rank + 1) * n)
+    cm = W.model(name)
+    sim = BatchSim(cm, n, local)
+    q0 = W.initial_qpos(cm, ids, args.seed)
+    sim.reset(init_qpos=q0[:, :5], extra_qpos=q0, seed=args.seed, env_offset=rank * n)
+    if cfg["dr"]:
+        sim.set_params(**W.dr_params(ids, args.seed))
+    tab = {k: (torch.as_tensor(v, dtype=torch.float32, device=dev) if isinstance(v, np.ndarray) else v)
+           for k, v in W.chirp_tables(ids, args.seed).items()}
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(args.seed * 1000003 + rank)
+    act = torch.empty((n, 5), dtype=torch.float32, device=dev)
+
+    def one_step(t):
+        if cfg["action"] == "chirp":
+            act.copy_(W.chirp_action(tab, float(t), lib=torch))
+        else:
+            torch.rand((n, 5), generator=gen, device=dev, out=act)
+            act.sub_(0.5)
+        sim.step(act)
+
+    t = 0
+    for _ in range(args.warmup):
+        one_step(t)
+        t += 1
+    sim.ncon.zero_()
+
+    def sync():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        one_step(t)
+        t += 1
+    sync()
+    dt = time.perf_counter() - t0
+    ncon = float(sim.ncon.sum().item())
+    if world > 1:
+        x = torch.tensor([dt, ncon], dtype=torch.float64, device=dev)
+        mx = x.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(x, op=dist.ReduceOp.SUM)
+        dt, ncon = float(mx[0]), float(x[1])
+    total_envs = n * world
+    value = total_envs * args.steps / dt
+    contacts = ncon / (total_envs * args.steps * 10)
+
+    # dominant kernel: HIP events around every launch of a profiled pass of the same workload
+    roof = None
+    cost = json.load(open(os.path.join(ROOT, "profiles", "algorithmic_cost.json")))[name]
+    if not args.no_profile:
+        kp = max(10, min(args.steps, 50))
+        sync()
+        sim.profile_begin()
+        for _ in range(kp):
+            one_step(t)
+            t += 1
+        prof = sim.profile_end()
+        kind, (ms, cnt) = max(prof.items(), key=lambda kv: kv[1][0])
+        avg_ms = ms / max(cnt, 1)
+        per_launch = {"step_fused": cost["flops_per_env_step"],
+                      "collide": cost["flops_per_env_substep_collision"],
+                      "substep": cost["flops_per_env_substep_dynamics"],
+                      "geom": 0.0}[kind] * n
+        achieved = per_launch / (avg_ms * 1e-3) / 1e12
+        traffic = None
+        tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(tpath):
+            traffic = json.load(open(tpath)).get(name, {}).get(kind)
+        roof = {"bound": "mfma", "achieved": achieved, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                "frac": achieved / PEAK_FP32_TFLOPS, "traffic": traffic,
+                "kernel": kind, "avg_launch_ms": avg_ms, "launches": cnt,
+                "flops_per_launch": per_launch,
+                "kernel_ms_per_step": {k: v[0] / kp for k, v in prof.items()},
+                "hbm_gbs_algorithmic": cost["hbm_bytes_per_env_step"] * n * world / (dt / args.steps) / 1e9,
+                "hbm_peak_gbs": PEAK_HBM_GBS,
+                "note": "FP32 VALU-bound per-env algebra (no MFMA); peak = FP32 vector = FP32 MFMA rate"}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(name, args.cpu_seconds, args.seed)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (Philox-keyed initial states / chirp inputs per global env id)",
+            "config": {"workload": cfg["desc"], "config": name, "envs_per_gpu": n, "global_envs": total_envs,
+                       "frame_skip": 10, "substeps_per_s": value * 10,
+                       "contacts_per_env_substep": contacts, "solver": "PGS (iterations 100, tol 1e-8)",
+                       "parallelism": f"env-sharded x{world} (no per-step collective)"},
+            "roofline": roof, "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -243,6 +243,19 @@ int sim_substeps(sim_batch* b, const sim_state* s, int nsub, void* stream);
 /* observation only (mj_kinematics + _get_state) */
 int sim_observe(sim_batch* b, const sim_state* s, float* obs, void* stream);
 
+/* replaces reading d.contact[:d.ncon] after mj_kinematics + mj_collision:
+   out [N][SIM_MAXCON][8] = (dist, pos[3], normal[3] geom1->geom2, pair id as
+   int32 bits), ncon [N].  Contact order = candidate-pair order (MuJoCo's). */
+int sim_contacts(sim_batch* b, const sim_state* s, float* out, int32_t* ncon, void* stream);
+
+/* kernel timing: between begin and end, sim_step brackets every kernel launch
+   with HIP events on its stream; end synchronises and returns the summed
+   milliseconds and launch counts per kernel kind
+   [0] fused step, [1] collide, [2] contact substep, [3] geom poses. */
+#define SIM_PROF_KINDS 4
+int sim_profile_begin(sim_batch* b);
+int sim_profile_end(sim_batch* b, double* ms, int32_t* launches);
+
 /* replaces dm_control qpos_from_site_pose, position-only (control/TrajectoryGenerator.py:96-107):
    target [N][3], q [nq][N] SoA in/out (warm start), ok [N] (1 = converged), iters [N] or NULL */
 int sim_ik_dls(sim_batch* b, const float* target, float* q, int32_t* ok, int32_t* iters,

@@ -1,0 +1,241 @@
+"""Batched SOARM101_DataCollection: the reference's rollout loop, on device.
+
+Reference: ``SOARM101/SOARM101_DataCollection.py``.  The reference steps one
+env per trajectory serially (``:108-134``); here all ``traj_num``
+trajectories are envs of one :class:`SOARM101VecEnv` stepped in lockstep on the
+GPU, with the action generators evaluated on device, so a whole dataset build
+is ``steps`` kernel launches.  The output layout is unchanged:
+``ndarray[traj, steps+1, 13]`` float64 with columns ``[u(5) | ee_xyz(3) | q(5)]``,
+row 0 = ``[u0, s0]`` and row i = ``[u_i, s_i]`` where ``s_i`` is the state
+after applying ``u_{i-1}`` (``:118-134``).
+
+Action sources (``input_type``):
+* ``random``: u ~ U[-0.5, 0.5)^5 each step (``:115,132``);
+* ``sin`` / ``chirp``: :class:`SineInputGenerator` (``:31-74``), tables
+  freq ~ U(0.0025, 0.05), amp ~ U(-0.5, 0.5), phase ~ U(0, 2pi) per
+  trajectory/dim (``:97-103``), chirp f += (f_end - f_start) t / 200;
+* ``ik_fig8`` / ``ik_circle`` (build-defined extension, SURVEY.md §8a note ii):
+  per env a Fig8/Circle Cartesian target stream (random phase), batched DLS-IK
+  gives q*, action = clip((q* - q) / dt, +-max_speed).
+"""
+import os
+
+import numpy as np
+
+from ..args import Args
+from .SOARM101_Env import SOARM101VecEnv
+
+
+class Collater:
+    """Splits a batch [B, T, 13] into x = [:, :, u:u+x] and u = [:, :, :u] (``:13-29``)."""
+
+    def __init__(self, x_dim: int, u_dim: int, device: str = "cuda"):
+        self.x_dim, self.u_dim, self.device = x_dim, u_dim, device
+
+    def __call__(self, batch_list):
+        import torch
+
+        batch = torch.stack(list(zip(*batch_list))[0], dim=0)
+        return dict(x=batch[:, :, self.u_dim:self.u_dim + self.x_dim].to(self.device),
+                    u=batch[:, :, :self.u_dim].to(self.device))
+
+    def split_device(self, rollout):
+        """Zero-copy views of a device rollout [T+1, N, 13] -> x [N, T+1, x], u [N, T+1, u]."""
+        r = rollout.transpose(0, 1)
+        return dict(x=r[:, :, self.u_dim:self.u_dim + self.x_dim], u=r[:, :, :self.u_dim])
+
+
+class SineInputGenerator:
+    """Per-trajectory sine / chirp inputs (reference ``:31-74``), vectorised over trajectories."""
+
+    def __init__(self, traj_num, udim=5, freq_range=(0.01, 0.05), amp_range=(0.05, 0.15),
+                 sine_mask=None, mode="sin", rng=None):
+        rng = rng if rng is not None else np.random
+        self.traj_num, self.udim, self.mode = traj_num, udim, mode
+        self.freq_start, self.freq_end = freq_range
+        self.freq_table = rng.uniform(freq_range[0], freq_range[1], size=(traj_num, udim))
+        self.amp_table = rng.uniform(amp_range[0], amp_range[1], size=(traj_num, udim))
+        self.phase_table = rng.uniform(0, 2 * np.pi, size=(traj_num, udim))
+        self.sine_mask = np.ones((traj_num, udim), bool) if sine_mask is None else sine_mask.astype(bool)
+
+    def freq(self, t, T_total=200):
+        if self.mode == "chirp":
+            return self.freq_table + (self.freq_end - self.freq_start) * (t / T_total)
+        return self.freq_table
+
+    def __call__(self, t, traj_i, T_total=200):
+        f = self.freq(t, T_total)[traj_i]
+        u = np.zeros(self.udim)
+        v = self.amp_table[traj_i] * np.sin(2 * np.pi * f * t + self.phase_table[traj_i])
+        m = self.sine_mask[traj_i]
+        u[m] = v[m]
+        return u
+
+    def batch(self, t, T_total=200):
+        """All trajectories at step t: [traj_num, udim] float64."""
+        v = self.amp_table * np.sin(2 * np.pi * self.freq(t, T_total) * t + self.phase_table)
+        return np.where(self.sine_mask, v, 0.0)
+
+
+class DeviceSine:
+    """The same generator evaluated on the GPU (tables resident, one fused torch expression per step)."""
+
+    def __init__(self, gen: SineInputGenerator, device):
+        import torch
+
+        self.g = gen
+        t = lambda a: torch.as_tensor(a, dtype=torch.float64, device=device)
+        self.f, self.a, self.p = t(gen.freq_table), t(gen.amp_table), t(gen.phase_table)
+        self.m = torch.as_tensor(gen.sine_mask, device=device)
+
+    def __call__(self, t, T_total=200):
+        import torch
+
+        f = self.f + (self.g.freq_end - self.g.freq_start) * (t / T_total) if self.g.mode == "chirp" else self.f
+        v = self.a * torch.sin(2 * np.pi * f * t + self.p)
+        return torch.where(self.m, v, torch.zeros_like(v)).float()
+
+
+def cartesian_targets(kind, t_param, idx=1, scale=0.5):
+    """Fig8 / Circle Cartesian paths of ``control/TrajectoryGenerator.py:138-166`` (numpy or torch)."""
+    lib = np if isinstance(t_param, np.ndarray) else __import__("torch")
+    one = lib.ones_like(t_param)
+    s, c = lib.sin(t_param), lib.cos(t_param)
+    if kind == "Fig8":
+        a = b = 0.2 * scale
+        if idx == 1:
+            x, y, z = 0.4 * one, b * c / (1 + s ** 2), 0.2 + 2 * a * s * c / (1 + s ** 2)
+        else:
+            x, y, z = 0.3 + 2 * a * s * c / (1 + s ** 2), b * c / (1 + s ** 2), 0.2 * one
+    elif kind == "Circle":
+        r = 0.1
+        if idx == 1:
+            x, y, z = 0.4 * one, r * c, 0.2 + r * s
+        else:
+            x, y, z = 0.3 + r * c, r * s, 0.2 * one
+    else:
+        raise ValueError(f"unknown trajectory {kind}")
+    return lib.stack([x, y, z], -1)
+
+
+class SOARM101DataGenerator:
+    """Reference ``SOARM101DataGenerator`` (``:77-205``) with a batched GPU rollout."""
+
+    def __init__(self, args: Args = None, device: int = 0, max_envs: int = 65536, model=None):
+        self.args = args if args is not None else Args()
+        self.udim, self.xdim = self.args.u_dim, self.args.x_dim
+        self.device_index = device
+        self.max_envs = max_envs
+        self.model = model
+        self.collate_fn = Collater(self.args.x_dim, self.args.u_dim, self.args.device)
+        self._envs = {}
+
+    def _env(self, n):
+        if n not in self._envs:
+            self._envs[n] = SOARM101VecEnv(num_envs=n, device=self.device_index, model=self.model,
+                                           seed=self.args.seed)
+            self.model = self._envs[n].model
+        return self._envs[n]
+
+    # ------------------------------------------------------------ device rollout
+    def rollout_device(self, n, steps, input_type="random", init_qpos=None, actions=None, seed=None,
+                       sine=None, env_offset=0):
+        """Rollout of `n` envs for `steps` env-steps; returns a device tensor [steps+1, n, 13] fp32.
+
+        actions: optional [steps+1, n, 5] (row i = u_i) to replay a fixed input sequence."""
+        import torch
+
+        env = self._env(n)
+        env._env_offset = env_offset
+        dev = env.sim.device
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(self.args.seed if seed is None else seed)
+        if input_type in ("sin", "chirp") and actions is None:
+            sine = sine or SineInputGenerator(n, self.udim, (0.0025, 0.05), (-0.5, 0.5), mode=input_type)
+            dsine = DeviceSine(sine, dev)
+        ik = input_type.startswith("ik_") and actions is None
+        if ik:
+            kind = "Fig8" if input_type == "ik_fig8" else "Circle"
+            phase = torch.rand(n, generator=gen, device=dev, dtype=torch.float64) * 2 * np.pi
+            qstar = None
+
+        def u_at(i, obs):
+            nonlocal qstar
+            if actions is not None:
+                return torch.as_tensor(actions[i], dtype=torch.float32, device=dev)
+            if input_type == "random":
+                return (torch.rand((n, self.udim), generator=gen, device=dev) - 0.5) * 2 * 0.5
+            if input_type in ("sin", "chirp"):
+                return dsine(i)
+            if ik:
+                t = 1.6 + 0.02 * (i + 1) + phase
+                tgt = cartesian_targets(kind, t).float()
+                qstar, ok, _ = env.sim.ik(tgt, q=qstar if qstar is not None else env.sim.qpos.clone())
+                q = obs[:, 3:8]
+                return torch.clamp((qstar[:5].T - q) / env.dt, -env.max_speed, env.max_speed)
+            raise ValueError(input_type)
+
+        out = torch.empty((steps + 1, n, self.udim + self.xdim), dtype=torch.float32, device=dev)
+        opts = None if init_qpos is None else {"initial_state": np.concatenate(
+            [np.asarray(init_qpos), np.zeros_like(init_qpos)], axis=1)}
+        s, _ = env.reset(seed=seed, options=opts)
+        u = u_at(0, s)
+        out[0, :, :self.udim] = u
+        out[0, :, self.udim:] = s
+        for i in range(1, steps + 1):
+            s, *_ = env.step(out[i - 1, :, :self.udim])
+            u = u_at(i, s)
+            out[i, :, :self.udim] = u
+            out[i, :, self.udim:] = s
+        return out
+
+    def generate_physics_based_data(self, traj_num, steps, input_type, **kw):
+        """Same contract as the reference (``:90-136``): ndarray[traj, steps+1, 13] float64."""
+        chunks = []
+        for s0 in range(0, traj_num, self.max_envs):
+            n = min(self.max_envs, traj_num - s0)
+            r = self.rollout_device(n, steps, input_type, env_offset=s0, **kw)
+            chunks.append(r.transpose(0, 1).double().cpu().numpy())
+        return np.concatenate(chunks, axis=0)
+
+    def generate_and_save_data(self):
+        """File cache / resume exactly as the reference (``:138-181``)."""
+        a = self.args
+        os.makedirs(a.data_dir_save, exist_ok=True)
+        if os.path.exists(a.data_dir_load_train):
+            self.train_data = np.load(a.data_dir_load_train)
+        else:
+            self.train_data = self.generate_physics_based_data(a.train_samples, a.train_steps, "random")
+            np.save(a.data_dir_load_train, self.train_data)
+        if os.path.exists(a.data_dir_load_val):
+            self.val_data = np.load(a.data_dir_load_val)
+        else:
+            self.val_data = self.generate_physics_based_data(a.test_samples, a.test_steps, "random")
+            np.save(a.data_dir_load_val, self.val_data)
+        self.test_data_dict = {}
+        for t in ["random", "sin", "chirp"]:
+            p = os.path.join(a.data_dir_save, f"test_data_{t}_{a.test_samples}_{a.test_steps}.npy")
+            if os.path.exists(p):
+                d = np.load(p)
+            else:
+                d = self.generate_physics_based_data(a.test_samples, a.test_steps, t)
+                np.save(p, d)
+            self.test_data_dict[t] = d
+
+    def get_train_loader(self):
+        import torch
+        from torch.utils.data import DataLoader, TensorDataset
+
+        tr = DataLoader(TensorDataset(torch.tensor(self.train_data, dtype=torch.float32)),
+                        batch_size=self.args.batch_size, collate_fn=self.collate_fn, shuffle=True)
+        va = DataLoader(TensorDataset(torch.tensor(self.val_data, dtype=torch.float32)),
+                        batch_size=self.args.eval_batch_size, collate_fn=self.collate_fn, shuffle=False)
+        return tr, va
+
+    def get_test_loader(self, test_type):
+        import torch
+        from torch.utils.data import DataLoader, TensorDataset
+
+        d = torch.tensor(self.test_data_dict[test_type], dtype=torch.float32)
+        return DataLoader(TensorDataset(d), batch_size=self.args.eval_batch_size,
+                          collate_fn=self.collate_fn, shuffle=False)

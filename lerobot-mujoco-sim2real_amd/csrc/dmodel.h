@@ -46,6 +46,9 @@ struct DModel {
   int pair_geom1[MAXP], pair_geom2[MAXP];
   float pair_solimp[MAXP][5], pair_KB[MAXP][2], pair_margin[MAXP], pair_tran[MAXP];
   float pair_friction[MAXP];
+  int pair_slot[MAXP];  // first contact slot of the pair in the collide output
+  int nslot;            // total contact slots (sum of per-pair capacities)
+  int free_diag;        // every free body has ipos = 0 and iquat = 1: its 6x6 M block is diagonal
 
   // sites
   int site_bodyid[SIM_MAXSITE];

@@ -10,9 +10,12 @@
 //     plane-box corners (<= 4), plane-hull deepest vertex;
 //   * hull support = steepest-ascent hill climbing on the hull vertex graph
 //     (L2-resident float4 vertices, CSR adjacency).
-// Geom world poses for the lane are staged once per substep in LDS laid out
-// [slot][lane] (consecutive lanes -> consecutive banks); contacts are appended
-// in pair order into the lane's LDS contact list.
+// Work decomposition: k_collide runs one lane per (env, pair) — one pair per
+// block so geom types and model lookups are wave-uniform, and 4096 envs x 86
+// pairs give ~5.5k waves to hide the hill-climbing load latency.  Each pair
+// writes <= 4 contacts into its own fixed slots; the dynamics kernel gathers
+// them by walking the pairs in order, which makes contact indexing identical
+// to the serial mj_collision order.
 #pragma once
 #include "soarm_step.h"
 
@@ -23,13 +26,7 @@ constexpr float FEPS = 1.1920929e-07f;
 constexpr float MPR_TOLF = 1e-6f;
 constexpr int MPR_ITERS = 50;
 
-// LDS views (per block of 64 lanes)
-struct GeomLds {
-  float (*a)[64];  // [CON_MAXG * 12][64]: pos(3), R(9)
-  int lane;
-  DEVI float& pos(int g, int k) const { return a[g * 12 + k][lane]; }
-  DEVI float& R(int g, int k) const { return a[g * 12 + 3 + k][lane]; }
-};
+// per-lane contact list of the dynamics kernel (LDS, [slot][lane])
 struct ConLds {
   float (*a)[64];  // [SIM_MAXCON * 8][64]: dist, pos(3), n(3), pair
   int lane;
@@ -44,12 +41,20 @@ struct GeomPose {
   float p[3], R[9];
 };
 
-DEVI void load_pose(const GeomLds& G, int g, GeomPose& o) {
+// geom world poses in global memory, SoA [geom*12 + k][env]
+DEVI void load_pose(const float* __restrict__ gpose, int n, int e, int g, GeomPose& o) {
 #pragma unroll
-  for (int k = 0; k < 3; k++) o.p[k] = G.pos(g, k);
+  for (int k = 0; k < 3; k++) o.p[k] = gpose[(size_t)(g * 12 + k) * n + e];
 #pragma unroll
-  for (int k = 0; k < 9; k++) o.R[k] = G.R(g, k);
+  for (int k = 0; k < 9; k++) o.R[k] = gpose[(size_t)(g * 12 + 3 + k) * n + e];
 }
+
+// contacts of one candidate pair (<= 4: box-box / plane-box corners; 1 otherwise)
+constexpr int PAIR_MAXCON = 4;
+struct PairOut {
+  int n;
+  float c[PAIR_MAXCON][7];  // dist, pos(3), normal(3) geom1 -> geom2
+};
 
 // hill-climbing support on a mesh hull; returns the local vertex
 DEVI float3 hull_support(const DModel& m, int g, const float l[3]) {
@@ -339,22 +344,19 @@ DEVI int mpr(const MPair& P, float& depth, float dir[3], float pos[3]) {
 }
 
 // ------------------------------------------------------------- primitives
-DEVI int emit(const ConLds& C, int& ncon, int& status, int pair, float dist, const float pos[3],
-              const float n[3]) {
-  if (ncon >= SIM_MAXCON) {
-    status |= SIM_ST_CONOVERFLOW;
-    return 0;
-  }
-  C.dist(ncon) = dist;
+// append one contact; slot indices are compile-time so PairOut stays in registers
+DEVI void emit(PairOut& o, float dist, const float pos[3], const float n[3]) {
 #pragma unroll
-  for (int k = 0; k < 3; k++) C.pos(ncon, k) = pos[k], C.n(ncon, k) = n[k];
-  C.set_pair(ncon, pair);
-  ncon++;
-  return 1;
+  for (int s = 0; s < PAIR_MAXCON; s++)
+    if (s == o.n) {
+      o.c[s][0] = dist;
+#pragma unroll
+      for (int k = 0; k < 3; k++) o.c[s][1 + k] = pos[k], o.c[s][4 + k] = n[k];
+    }
+  if (o.n < PAIR_MAXCON) o.n++;
 }
 
-DEVI void plane_box(const DModel& m, int gp, int gb, const GeomPose& Pp, const GeomPose& Pb,
-                    const ConLds& C, int& ncon, int& status, int pair) {
+DEVI void plane_box(const DModel& m, int gp, int gb, const GeomPose& Pp, const GeomPose& Pb, PairOut& o) {
   const float n[3] = {Pp.R[2], Pp.R[5], Pp.R[8]};
   int cnt = 0;
   for (int i = 0; i < 8 && cnt < 4; i++) {
@@ -367,14 +369,13 @@ DEVI void plane_box(const DModel& m, int gp, int gb, const GeomPose& Pp, const G
     const float dist = dot3(rel, n);
     if (dist < 0.f) {
       const float pos[3] = {p[0] - 0.5f * dist * n[0], p[1] - 0.5f * dist * n[1], p[2] - 0.5f * dist * n[2]};
-      emit(C, ncon, status, pair, dist, pos, n);
+      emit(o, dist, pos, n);
       cnt++;
     }
   }
 }
 
-DEVI void plane_convex(const DModel& m, int gp, int g, const GeomPose& Pp, const GeomPose& Pg,
-                       const ConLds& C, int& ncon, int& status, int pair) {
+DEVI void plane_convex(const DModel& m, int gp, int g, const GeomPose& Pp, const GeomPose& Pg, PairOut& o) {
   const float n[3] = {Pp.R[2], Pp.R[5], Pp.R[8]};
   const float nn[3] = {-n[0], -n[1], -n[2]};
   float p[3], rel[3];
@@ -383,7 +384,7 @@ DEVI void plane_convex(const DModel& m, int gp, int g, const GeomPose& Pp, const
   const float dist = dot3(rel, n);
   if (dist >= 0.f) return;
   const float pos[3] = {p[0] - 0.5f * dist * n[0], p[1] - 0.5f * dist * n[1], p[2] - 0.5f * dist * n[2]};
-  emit(C, ncon, status, pair, dist, pos, n);
+  emit(o, dist, pos, n);
 }
 
 DEVI int clip_poly(const float in[][3], int n, float out[][3], const float o[3], const float a[3], float lim) {
@@ -409,8 +410,7 @@ DEVI int clip_poly(const float in[][3], int n, float out[][3], const float o[3],
   return k;
 }
 
-DEVI void box_box(const DModel& m, int g1, int g2, const GeomPose& P1, const GeomPose& P2,
-                  const ConLds& C, int& ncon, int& status, int pair) {
+DEVI void box_box(const DModel& m, int g1, int g2, const GeomPose& P1, const GeomPose& P2, PairOut& o) {
   const float *h1 = m.geom_size[g1], *h2 = m.geom_size[g2];
   float A[3][3], B[3][3], t[3];
 #pragma unroll
@@ -477,6 +477,42 @@ DEVI void box_box(const DModel& m, int g1, int g2, const GeomPose& P1, const Geo
 #pragma unroll
       for (int k = 0; k < 3; k++)
         poly[q][k] = ci[k] + s * hi[ia] * Ai[ia][k] + su[q] * hi[u] * Ai[u][k] + sv[q] * hi[v] * Ai[v][k];
+    {
+      // fast path (cube resting on the table): the incident face lies inside the reference
+      // face's side slabs, so clipping is the identity; emit penetrating corners deepest first
+      // (the same stable order as the general path), all with compile-time indices.
+      const int ra = (fa + 1) % 3, rb = (fa + 2) % 3;
+      bool inside = true;
+      float dep[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        float rel[3];
+        sub(rel, poly[q], fc);
+        inside = inside && fabsf(dot3(rel, Ar[ra])) <= hr[ra] && fabsf(dot3(rel, Ar[rb])) <= hr[rb];
+        dep[q] = dot3(rel, nr);
+      }
+      if (inside) {
+        unsigned used = 0;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          int best = -1;
+          float bdep = 0.f;
+#pragma unroll
+          for (int q = 0; q < 4; q++)
+            if (!((used >> q) & 1u) && dep[q] < bdep) bdep = dep[q], best = q;
+          if (best < 0) break;
+          used |= 1u << best;
+          float pos[3] = {0, 0, 0};
+#pragma unroll
+          for (int q = 0; q < 4; q++)
+            if (q == best)
+#pragma unroll
+              for (int k = 0; k < 3; k++) pos[k] = poly[q][k] - 0.5f * bdep * nr[k];
+          emit(o, bdep, pos, bn);
+        }
+        return;
+      }
+    }
     int n = 4;
     const int ra = (fa + 1) % 3, rb = (fa + 2) % 3;
     float na[3];
@@ -505,7 +541,7 @@ DEVI void box_box(const DModel& m, int g1, int g2, const GeomPose& P1, const Geo
       const float* pp = poly[idx[q]];
       const float pos[3] = {pp[0] - 0.5f * dep[q] * nr[0], pp[1] - 0.5f * dep[q] * nr[1],
                             pp[2] - 0.5f * dep[q] * nr[2]};
-      emit(C, ncon, status, pair, dep[q], pos, bn);
+      emit(o, dep[q], pos, bn);
     }
     return;
   }
@@ -536,12 +572,12 @@ DEVI void box_box(const DModel& m, int g1, int g2, const GeomPose& P1, const Geo
   float pos[3];
 #pragma unroll
   for (int k = 0; k < 3; k++) pos[k] = 0.5f * (p1[k] + sp * A[ea][k] + p2[k] + tp * B[eb][k]);
-  emit(C, ncon, status, pair, -best / 1.05f, pos, bn);
+  emit(o, -best / 1.05f, pos, bn);
 }
 
-// mj_collision for one lane: stage geom poses, walk the pair list
+// world poses of every collidable geom of this env -> global SoA [geom*12+k][env]
 template <int NA, int NF>
-DEVI int collide(Sim<NA, NF>& S, const GeomLds& G, const ConLds& C) {
+DEVI void write_geom_poses(const Sim<NA, NF>& S, float* __restrict__ gpose, int n, int e) {
   const DModel& m = *S.mp;
   constexpr int NB = Sim<NA, NF>::NB;
   for (int g = 0; g < m.ngeom; g++) {
@@ -551,61 +587,59 @@ DEVI int collide(Sim<NA, NF>& S, const GeomLds& G, const ConLds& C) {
     for (int k = 1; k < NB; k++)
       if (k == b) {
 #pragma unroll
-        for (int e = 0; e < 3; e++) bp[e] = S.xpos[k][e];
+        for (int c = 0; c < 3; c++) bp[c] = S.xpos[k][c];
 #pragma unroll
-        for (int e = 0; e < 9; e++) bR[e] = S.xmat[k][e];
+        for (int c = 0; c < 9; c++) bR[c] = S.xmat[k][c];
       }
     const float gp[3] = {m.geom_pos[g][0], m.geom_pos[g][1], m.geom_pos[g][2]};
     float w[3], R[9];
     mv(w, bR, gp);
     mm(R, bR, m.geom_mat[g]);
 #pragma unroll
-    for (int e = 0; e < 3; e++) G.pos(g, e) = bp[e] + w[e];
+    for (int c = 0; c < 3; c++) gpose[(size_t)(g * 12 + c) * n + e] = bp[c] + w[c];
 #pragma unroll
-    for (int e = 0; e < 9; e++) G.R(g, e) = R[e];
+    for (int c = 0; c < 9; c++) gpose[(size_t)(g * 12 + 3 + c) * n + e] = R[c];
   }
-  int ncon = 0;
-  for (int p = 0; p < m.npair; p++) {
-    const int g1 = m.pair_geom1[p], g2 = m.pair_geom2[p];
-    const int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
-    GeomPose P1, P2;
-    load_pose(G, g1, P1);
-    load_pose(G, g2, P2);
-    if (m.geom_rbound[g1] > 0.f && m.geom_rbound[g2] > 0.f) {
-      float c1[3], c2[3], r[3];
-      geom_center(m, g1, P1, c1);
-      geom_center(m, g2, P2, c2);
-      sub(r, c1, c2);
-      const float mg = m.pair_margin[p];
-      const float rr = m.geom_rbound[g1] + m.geom_rbound[g2] + mg;
-      if (dot3(r, r) > rr * rr) continue;
-      bool sep = false;
+}
+
+// midphase + narrowphase of candidate pair p (geom types are wave-uniform)
+DEVI void collide_pair(const DModel& m, int p, const GeomPose& P1, const GeomPose& P2, PairOut& o) {
+  o.n = 0;
+  const int g1 = m.pair_geom1[p], g2 = m.pair_geom2[p];
+  const int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
+  if (m.geom_rbound[g1] > 0.f && m.geom_rbound[g2] > 0.f) {
+    float c1[3], c2[3], r[3];
+    geom_center(m, g1, P1, c1);
+    geom_center(m, g2, P2, c2);
+    sub(r, c1, c2);
+    const float mg = m.pair_margin[p];
+    const float rr = m.geom_rbound[g1] + m.geom_rbound[g2] + mg;
+    if (dot3(r, r) > rr * rr) return;
+    bool sep = false;
 #pragma unroll
-      for (int k = 0; k < 3; k++) {
-        const float e1 = fabsf(P1.R[3 * k]) * m.geom_half[g1][0] + fabsf(P1.R[3 * k + 1]) * m.geom_half[g1][1] +
-                         fabsf(P1.R[3 * k + 2]) * m.geom_half[g1][2];
-        const float e2 = fabsf(P2.R[3 * k]) * m.geom_half[g2][0] + fabsf(P2.R[3 * k + 1]) * m.geom_half[g2][1] +
-                         fabsf(P2.R[3 * k + 2]) * m.geom_half[g2][2];
-        sep |= fabsf(r[k]) > e1 + e2 + mg;
-      }
-      if (sep) continue;
+    for (int k = 0; k < 3; k++) {
+      const float e1 = fabsf(P1.R[3 * k]) * m.geom_half[g1][0] + fabsf(P1.R[3 * k + 1]) * m.geom_half[g1][1] +
+                       fabsf(P1.R[3 * k + 2]) * m.geom_half[g1][2];
+      const float e2 = fabsf(P2.R[3 * k]) * m.geom_half[g2][0] + fabsf(P2.R[3 * k + 1]) * m.geom_half[g2][1] +
+                       fabsf(P2.R[3 * k + 2]) * m.geom_half[g2][2];
+      sep |= fabsf(r[k]) > e1 + e2 + mg;
     }
-    if (t1 == SIM_GEOM_PLANE) {
-      if (t2 == SIM_GEOM_BOX)
-        plane_box(m, g1, g2, P1, P2, C, ncon, S.status, p);
-      else if (t2 == SIM_GEOM_MESH)
-        plane_convex(m, g1, g2, P1, P2, C, ncon, S.status, p);
-      continue;
-    }
-    if (t1 == SIM_GEOM_BOX && t2 == SIM_GEOM_BOX) {
-      box_box(m, g1, g2, P1, P2, C, ncon, S.status, p);
-      continue;
-    }
-    MPair mp{m, g1, g2, P1, P2};
-    float depth, dir[3], pos[3];
-    if (mpr(mp, depth, dir, pos)) emit(C, ncon, S.status, p, -depth, pos, dir);
+    if (sep) return;
   }
-  return ncon;
+  if (t1 == SIM_GEOM_PLANE) {
+    if (t2 == SIM_GEOM_BOX)
+      plane_box(m, g1, g2, P1, P2, o);
+    else if (t2 == SIM_GEOM_MESH)
+      plane_convex(m, g1, g2, P1, P2, o);
+    return;
+  }
+  if (t1 == SIM_GEOM_BOX && t2 == SIM_GEOM_BOX) {
+    box_box(m, g1, g2, P1, P2, o);
+    return;
+  }
+  MPair mp{m, g1, g2, P1, P2};
+  float depth, dir[3], pos[3];
+  if (mpr(mp, depth, dir, pos)) emit(o, -depth, pos, dir);
 }
 
 }  // namespace soarm

@@ -5,43 +5,131 @@
 // frictionloss row per arm dof (always active), joint-limit rows when a
 // hinge is past its range, and 4 pyramidal edges per contact.  Rows are
 // visited in MuJoCo's order (friction rows, then limits joint by joint
-// lower/upper, then contacts), so the sweep matches the oracle's.
+// lower/upper, then contacts in candidate-pair order), so the sweep matches
+// the oracle's.
 //
-// Fixed rows live in per-slot registers (J = +-e_i, so W = M^-1 J' is a
-// column of the arm block's inverse).  Contact edges keep J and W in a
-// per-lane scratch slab in global memory (L2-resident, [slot][env] SoA).
+// Where the rows live (one lane = one env, one wave per SIMD at 4096 envs, so
+// every sweep is a latency chain and nothing may come from global memory):
+//  * fixed rows: registers; J = +-e_i, W = M^-1 J' is a column of the arm
+//    block's explicit inverse;
+//  * contacts 0..LDS_CON-1: LDS, [field][lane] (conflict-free), one record per
+//    contact holding the 12-dof J_n, J_t1, J_t2; the 4 pyramid edges
+//    J_n +- mu J_tk are formed on the fly and W_e = M^-1 J_e comes from the
+//    block inverses in registers; arm / free-body halves are skipped by a
+//    per-contact flag (a cube-on-table contact touches only the 6 cube dofs);
+//  * contacts LDS_CON..SIM_MAXCON-1 (rare): per-edge J/W slab in global
+//    scratch, [row][env] SoA.
+// PGS on the resting cube's 16 redundant edges needs ~96 sweeps per substep
+// (measured on the oracle with MuJoCo's improvement criterion), so the sweep
+// body is the hot loop of the contact scene.
 #pragma once
 #include "soarm_collide.h"
 
 namespace soarm {
 
+constexpr int LDS_CON = 8;  // contacts whose rows stay in LDS
+constexpr int CF = 56;      // LDS floats per contact record
+// record fields: [0, 3*12) J_n | J_t1 | J_t2 (12 slots each), 36..39 aref_e,
+// 40..43 ARdiag_e, 44..47 force_e, 48..51 1/ARdiag_e, 52 mu, 53 R (pyramid), 54 flags
+enum { F_AREF = 36, F_ARD = 40, F_FRC = 44, F_IARD = 48, F_MU = 52, F_R = 53, F_FLAGS = 54 };
+enum { TOUCH_ARM = 1, TOUCH_FREE = 2 };
+
+struct RowLds {
+  float (*a)[64];  // [LDS_CON * CF][64]
+  int lane;
+  DEVI float& at(int c, int f) const { return a[c * CF + f][lane]; }
+};
+
 template <int NA, int NF>
 struct ContactRows {
   static constexpr int NV = NA + 6 * NF;
-  // scratch layout: for edge r (0..4*MAXCON-1): J[NV], W[NV] then scalars
+  // overflow rows (edge r of contact c >= LDS_CON): J[NV], W[NV], aref, R, ARdiag, force
   float* base;  // = scratch + e
   int stride;   // = n envs
   DEVI float& J(int r, int i) const { return base[((size_t)r * (2 * NV + 4) + i) * stride]; }
   DEVI float& W(int r, int i) const { return base[((size_t)r * (2 * NV + 4) + NV + i) * stride]; }
   DEVI float& S(int r, int k) const { return base[((size_t)r * (2 * NV + 4) + 2 * NV + k) * stride]; }
-  // S: 0 aref, 1 R, 2 ARdiag, 3 force
 };
 
+// explicit inverse of the block-diagonal M: arm block + one 6x6 per free body
+template <int NA, int NF>
+struct MInv {
+  static constexpr int NV = NA + 6 * NF;
+  float A[NA * (NA + 1) / 2];     // arm block inverse, packed lower triangle (symmetric)
+  float Fd[NF > 0 ? NF : 1][6];   // free bodies: diagonal mass block (host-validated) -> 1/M_ii
+  DEVI float a(int i, int k) const { return i >= k ? A[i * (i + 1) / 2 + k] : A[k * (k + 1) / 2 + i]; }
+  DEVI void build(const Sim<NA, NF>& S) {
+#pragma unroll
+    for (int i = 0; i < NA; i++) {
+      float ei[NA], col[NA];
+#pragma unroll
+      for (int k = 0; k < NA; k++) ei[k] = (k == i) ? 1.f : 0.f;
+      ldl_solve<NA>(S.LA, S.DAi, col, ei);
+#pragma unroll
+      for (int k = 0; k <= i; k++) A[i * (i + 1) / 2 + k] = col[k];
+    }
+#pragma unroll
+    for (int f = 0; f < NF; f++)
+#pragma unroll
+      for (int i = 0; i < 6; i++) Fd[f][i] = 1.f / S.MF[f][i * (i + 1) / 2 + i];
+  }
+  // y = M^-1 x, restricted to the halves x can be nonzero on
+  DEVI void mul(const float x[NV], float y[NV], bool arm, bool fr) const {
+#pragma unroll
+    for (int i = 0; i < NV; i++) y[i] = 0.f;
+    if (arm) {
+#pragma unroll
+      for (int i = 0; i < NA; i++) {
+        float s = 0.f;
+#pragma unroll
+        for (int k = 0; k < NA; k++) s += a(i, k) * x[k];
+        y[i] = s;
+      }
+    }
+    if (fr) {
+#pragma unroll
+      for (int f = 0; f < NF; f++)
+#pragma unroll
+        for (int i = 0; i < 6; i++) y[NA + 6 * f + i] = Fd[f][i] * x[NA + 6 * f + i];
+    }
+  }
+};
+
+template <int NA, int NF>
+DEVI float dotv(const float a[], const float b[], bool arm, bool fr) {
+  constexpr int NV = NA + 6 * NF;
+  float s0 = 0.f, s1 = 0.f;
+  if (arm) {
+#pragma unroll
+    for (int i = 0; i < NA; i++) s0 += a[i] * b[i];
+  }
+  if (fr) {
+#pragma unroll
+    for (int i = NA; i < NV; i++) s1 += a[i] * b[i];
+  }
+  return s0 + s1;
+}
+
+// pyramid edge e of a contact from its J_n, J_t1, J_t2:  J_n +- mu J_tk
+template <int NV>
+DEVI void edge_J(const float jn[NV], const float jt1[NV], const float jt2[NV], int e, float mu, float J[NV]) {
+  const float s = (e & 1) ? -mu : mu;
+  const float* jt = (e >> 1) ? jt2 : jt1;
+#pragma unroll
+  for (int i = 0; i < NV; i++) J[i] = jn[i] + s * jt[i];
+}
+
+// Builds every constraint row, solves the dual by PGS, sets S.qacc / S.fcon.
+// Contacts are read straight from the collide output (cbuf/ccount, pair order).
+// Returns the number of contacts used.
 template <int NA, int NF, bool CON>
-DEVI void solve_constraints(Sim<NA, NF>& S, const ConLds& C, int ncon, const ContactRows<NA, NF>& cr) {
+DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const int* __restrict__ ccount,
+                           int n, int e, const RowLds& L, const ContactRows<NA, NF>& cr) {
   constexpr int NV = Sim<NA, NF>::NV;
   const DModel& m = *S.mp;
   S.solve_m(S.qacc_s, S.fsmooth);
-
-  // inverse of the arm block, column by column
-  float Wa[NA][NA];
-#pragma unroll
-  for (int i = 0; i < NA; i++) {
-    float ei[NA];
-#pragma unroll
-    for (int k = 0; k < NA; k++) ei[k] = (k == i) ? 1.f : 0.f;
-    ldl_solve<NA>(S.LA, S.DAi, Wa[i], ei);
-  }
+  MInv<NA, NF> Mi;
+  Mi.build(S);
 
   // ---- fixed slots: [friction_i], then per joint [lower_i, upper_i]
   float f[3 * NA], aref[3 * NA], R[3 * NA], ARd[3 * NA];
@@ -51,7 +139,7 @@ DEVI void solve_constraints(Sim<NA, NF>& S, const ConLds& C, int ncon, const Con
     act[i] = m.dof_frictionloss[i] > 0.f;
     R[i] = m.dof_fricR[i];
     aref[i] = -m.dof_fricB[i] * S.qvel[i];
-    ARd[i] = Wa[i][i] + R[i];
+    ARd[i] = Mi.a(i, i) + R[i];
 #pragma unroll
     for (int side = 0; side < 2; side++) {
       const int s = NA + 2 * i + side;
@@ -61,105 +149,130 @@ DEVI void solve_constraints(Sim<NA, NF>& S, const ConLds& C, int ncon, const Con
       R[s] = fmaxf(MINVALF, (1.f - imp) * m.dof_invweight0[i] / imp);
       const float vel = side == 0 ? S.qvel[i] : -S.qvel[i];
       aref[s] = -m.jnt_KB[i][1] * vel - m.jnt_KB[i][0] * imp * (dist - m.jnt_margin[i]);
-      ARd[s] = Wa[i][i] + R[s];
+      ARd[s] = Mi.a(i, i) + R[s];
     }
   }
   auto slot_dof = [](int s) { return s < NA ? s : (s - NA) >> 1; };
   auto slot_sgn = [](int s) { return (s < NA || ((s - NA) & 1) == 0) ? 1.f : -1.f; };
+  float iARd[3 * NA];
+#pragma unroll
+  for (int s = 0; s < 3 * NA; s++) iARd[s] = 1.f / ARd[s];
 
-  // ---- contact edges -> scratch (J, W, aref, R, ARd)
-  int ne = 0;
+  // ---- contact rows, straight from the collide output in pair order
+  int ncon = 0;
   if constexpr (CON) {
-    ne = 4 * ncon;
-    for (int c = 0; c < ncon; c++) {
-      const int p = C.pair(c);
-      const float cpos[3] = {C.pos(c, 0), C.pos(c, 1), C.pos(c, 2)};
-      const float cdist = C.dist(c);
-      const int b1 = m.geom_bodyid[m.pair_geom1[p]], b2 = m.geom_bodyid[m.pair_geom2[p]];
-      // frame (mju_makeFrame)
-      float fr[9] = {C.n(c, 0), C.n(c, 1), C.n(c, 2), 0, 0, 0, 0, 0, 0};
-      {
-        float y[3];
-        if (fabsf(fr[1]) < 0.5f)
-          y[0] = 0, y[1] = 1, y[2] = 0;
-        else
-          y[0] = 0, y[1] = 0, y[2] = 1;
-        const float dd = dot3(fr, y);
-        y[0] -= dd * fr[0], y[1] -= dd * fr[1], y[2] -= dd * fr[2];
-        const float inv = rsqrtf(dot3(y, y));
-        fr[3] = y[0] * inv, fr[4] = y[1] * inv, fr[5] = y[2] * inv;
-        cross(fr + 6, fr, fr + 3);
-      }
-      // relative translational Jacobian (body2 - body1) at the contact point, in the contact frame
-      float jd[3][NV];
-#pragma unroll
-      for (int i = 0; i < NV; i++) jd[0][i] = jd[1][i] = jd[2][i] = 0.f;
-#pragma unroll
-      for (int side = 0; side < 2; side++) {
-        const int b = side ? b2 : b1;
-        const float sg = side ? 1.f : -1.f;
-        // arm dofs: dof i moves bodies >= i+2 of the chain
-#pragma unroll
-        for (int i = 0; i < NA; i++) {
-          if (b >= i + 2 && b < 2 + NA) {
-            float l[3];
-            cross(l, S.cdof[i], cpos);
-            const float jp[3] = {S.cdof[i][3] + l[0], S.cdof[i][4] + l[1], S.cdof[i][5] + l[2]};
-#pragma unroll
-            for (int k = 0; k < 3; k++) jd[k][i] += sg * dot3(fr + 3 * k, jp);
-          }
+    if (ccount != nullptr)
+    for (int p = 0; p < m.npair; p++) {
+      const int cnt = ccount[(size_t)p * n + e];
+      const int s0 = m.pair_slot[p];
+      for (int k = 0; k < cnt; k++) {
+        if (ncon >= SIM_MAXCON) {
+          S.status |= SIM_ST_CONOVERFLOW;
+          break;
         }
+        const size_t base = (size_t)(s0 + k) * 7;
+        const float cdist = cbuf[base * n + e];
+        const float cpos[3] = {cbuf[(base + 1) * n + e], cbuf[(base + 2) * n + e], cbuf[(base + 3) * n + e]};
+        float fr[9] = {cbuf[(base + 4) * n + e], cbuf[(base + 5) * n + e], cbuf[(base + 6) * n + e], 0, 0, 0, 0, 0, 0};
+        {  // contact frame (mju_makeFrame)
+          float y[3];
+          if (fabsf(fr[1]) < 0.5f)
+            y[0] = 0, y[1] = 1, y[2] = 0;
+          else
+            y[0] = 0, y[1] = 0, y[2] = 1;
+          const float dd = dot3(fr, y);
+          y[0] -= dd * fr[0], y[1] -= dd * fr[1], y[2] -= dd * fr[2];
+          const float inv = rsqrtf(dot3(y, y));
+          fr[3] = y[0] * inv, fr[4] = y[1] * inv, fr[5] = y[2] * inv;
+          cross(fr + 6, fr, fr + 3);
+        }
+        const int b1 = m.geom_bodyid[m.pair_geom1[p]], b2 = m.geom_bodyid[m.pair_geom2[p]];
+        // relative translational Jacobian (body2 - body1) at the contact point, contact frame
+        float jd[3][NV];
 #pragma unroll
-        for (int ff = 0; ff < NF; ff++) {
-          const int fb = 2 + NA + ff, d0 = NA + 6 * ff;
-          if (b == fb) {
-            const float off[3] = {cpos[0] - S.xpos[fb][0], cpos[1] - S.xpos[fb][1],
-                                  cpos[2] - S.xpos[fb][2]};
+        for (int i = 0; i < NV; i++) jd[0][i] = jd[1][i] = jd[2][i] = 0.f;
+        int flags = 0;
 #pragma unroll
-            for (int i = 0; i < 6; i++) {
+        for (int side = 0; side < 2; side++) {
+          const int b = side ? b2 : b1;
+          const float sg = side ? 1.f : -1.f;
+          if (b >= 2 && b < 2 + NA) flags |= TOUCH_ARM;
+#pragma unroll
+          for (int i = 0; i < NA; i++) {
+            if (b >= i + 2 && b < 2 + NA) {  // hinge i moves chain bodies i+2.. (reference point: origin)
               float l[3];
-              cross(l, S.cdof[d0 + i], off);
-              const float jp[3] = {S.cdof[d0 + i][3] + l[0], S.cdof[d0 + i][4] + l[1],
-                                   S.cdof[d0 + i][5] + l[2]};
+              cross(l, S.cdof[i], cpos);
+              const float jp[3] = {S.cdof[i][3] + l[0], S.cdof[i][4] + l[1], S.cdof[i][5] + l[2]};
 #pragma unroll
-              for (int k = 0; k < 3; k++) jd[k][d0 + i] += sg * dot3(fr + 3 * k, jp);
+              for (int q = 0; q < 3; q++) jd[q][i] += sg * dot3(fr + 3 * q, jp);
+            }
+          }
+#pragma unroll
+          for (int ff = 0; ff < NF; ff++) {
+            const int fb = 2 + NA + ff, d0 = NA + 6 * ff;
+            if (b == fb) {
+              flags |= TOUCH_FREE;
+              const float off[3] = {cpos[0] - S.xpos[fb][0], cpos[1] - S.xpos[fb][1], cpos[2] - S.xpos[fb][2]};
+#pragma unroll
+              for (int i = 0; i < 6; i++) {
+                float l[3];
+                cross(l, S.cdof[d0 + i], off);
+                const float jp[3] = {S.cdof[d0 + i][3] + l[0], S.cdof[d0 + i][4] + l[1], S.cdof[d0 + i][5] + l[2]};
+#pragma unroll
+                for (int q = 0; q < 3; q++) jd[q][d0 + i] += sg * dot3(fr + 3 * q, jp);
+              }
             }
           }
         }
-      }
-      const float mu = S.fric >= 0.f ? S.fric : m.pair_friction[p];
-      const float tran = m.pair_tran[p];
-      const float margin = m.pair_margin[p];
-      const float imp = impedance(m.pair_solimp[p], cdist, margin);
-      const float diag = tran + mu * mu * tran;
-      const float R0 = fmaxf(MINVALF, (1.f - imp) * diag / imp);
-      const float Rpy = 2.f * mu * mu * R0 / m.impratio;
+        const bool ta = flags & TOUCH_ARM, tf = flags & TOUCH_FREE;
+        const float mu = S.fric >= 0.f ? S.fric : m.pair_friction[p];
+        const float tran = m.pair_tran[p];
+        const float margin = m.pair_margin[p];
+        const float imp = impedance(m.pair_solimp[p], cdist, margin);
+        const float diag = tran + mu * mu * tran;
+        const float R0 = fmaxf(MINVALF, (1.f - imp) * diag / imp);
+        const float Rpy = 2.f * mu * mu * R0 / m.impratio;
+        const bool lds = ncon < LDS_CON;
+        if (lds) {
 #pragma unroll
-      for (int ed = 0; ed < 4; ed++) {
-        const int r = 4 * c + ed;
-        const int k = 1 + (ed >> 1);
-        const float sg = (ed & 1) ? -1.f : 1.f;
-        float J[NV], W[NV];
-        float vel = 0.f;
+          for (int q = 0; q < 3; q++)
 #pragma unroll
-        for (int i = 0; i < NV; i++) {
-          J[i] = jd[0][i] + sg * mu * jd[k][i];
-          vel += J[i] * S.qvel[i];
+            for (int i = 0; i < NV; i++) L.at(ncon, 12 * q + i) = jd[q][i];
+          L.at(ncon, F_MU) = mu;
+          L.at(ncon, F_R) = Rpy;
+          L.at(ncon, F_FLAGS) = (float)flags;
         }
-        S.solve_m(W, J);
-        float jw = 0.f;
 #pragma unroll
-        for (int i = 0; i < NV; i++) {
-          jw += J[i] * W[i];
-          cr.J(r, i) = J[i];
-          cr.W(r, i) = W[i];
+        for (int ed = 0; ed < 4; ed++) {
+          float J[NV], W[NV];
+          edge_J<NV>(jd[0], jd[1], jd[2], ed, mu, J);
+          float vel = 0.f;
+#pragma unroll
+          for (int i = 0; i < NV; i++) vel += J[i] * S.qvel[i];
+          Mi.mul(J, W, ta, tf);
+          const float ard = dotv<NA, NF>(J, W, ta, tf) + Rpy;
+          const float ar = -m.pair_KB[p][1] * vel - m.pair_KB[p][0] * imp * (cdist - margin);
+          if (lds) {
+            L.at(ncon, F_AREF + ed) = ar;
+            L.at(ncon, F_ARD + ed) = ard;
+            L.at(ncon, F_IARD + ed) = 1.f / ard;
+          } else {
+            const int r = 4 * ncon + ed;
+#pragma unroll
+            for (int i = 0; i < NV; i++) {
+              cr.J(r, i) = J[i];
+              cr.W(r, i) = W[i];
+            }
+            cr.S(r, 0) = ar;
+            cr.S(r, 1) = Rpy;
+            cr.S(r, 2) = ard;
+          }
         }
-        cr.S(r, 0) = -m.pair_KB[p][1] * vel - m.pair_KB[p][0] * imp * (cdist - margin);
-        cr.S(r, 1) = Rpy;
-        cr.S(r, 2) = jw + Rpy;
+        ncon++;
       }
     }
   }
+  const int nl = ncon < LDS_CON ? ncon : LDS_CON;
 
   // ---- warm start from qacc_warmstart (forces implied by the primal), keep if it beats f = 0
   float v[NV];
@@ -179,26 +292,69 @@ DEVI void solve_constraints(Sim<NA, NF>& S, const ConLds& C, int ncon, const Con
     }
     f[s] = act[s] ? fs : 0.f;
 #pragma unroll
-    for (int k = 0; k < NA; k++) v[k] += Wa[i][k] * sg * f[s];
+    for (int k = 0; k < NA; k++) v[k] += Mi.a(i, k) * sg * f[s];
   }
-  for (int r = 0; r < ne; r++) {
-    float jar = -cr.S(r, 0);
+  float cost = 0.f;
+  for (int c = 0; c < nl; c++) {
+    const int fl = (int)L.at(c, F_FLAGS);
+    const bool ta = fl & TOUCH_ARM, tf = fl & TOUCH_FREE;
+    float jn[NV], jt1[NV], jt2[NV];
 #pragma unroll
-    for (int i = 0; i < NV; i++) jar += cr.J(r, i) * S.warm[i];
-    const float fs = jar < 0.f ? -jar / cr.S(r, 1) : 0.f;
-    cr.S(r, 3) = fs;
+    for (int i = 0; i < NV; i++) jn[i] = L.at(c, i), jt1[i] = L.at(c, 12 + i), jt2[i] = L.at(c, 24 + i);
+    const float mu = L.at(c, F_MU), Rp = L.at(c, F_R);
 #pragma unroll
-    for (int i = 0; i < NV; i++) v[i] += cr.W(r, i) * fs;
-  }
-  {
-    float cost = 0.f;
+    for (int ed = 0; ed < 4; ed++) {
+      float J[NV], W[NV];
+      edge_J<NV>(jn, jt1, jt2, ed, mu, J);
+      const float jar = dotv<NA, NF>(J, S.warm, ta, tf) - L.at(c, F_AREF + ed);
+      const float fs = jar < 0.f ? -jar / Rp : 0.f;
+      L.at(c, F_FRC + ed) = fs;
+      if (fs != 0.f) {
+        Mi.mul(J, W, ta, tf);
 #pragma unroll
-    for (int s = 0; s < 3 * NA; s++) {
-      const int i = slot_dof(s);
-      const float sg = slot_sgn(s);
-      cost += 0.5f * f[s] * (sg * v[i] - aref[s] + R[s] * f[s]) + 0.5f * f[s] * (sg * S.qacc_s[i] - aref[s]);
+        for (int i = 0; i < NV; i++) v[i] += W[i] * fs;
+      }
     }
-    for (int r = 0; r < ne; r++) {
+  }
+  for (int c = nl; c < ncon; c++)
+    for (int ed = 0; ed < 4; ed++) {
+      const int r = 4 * c + ed;
+      float jar = -cr.S(r, 0);
+#pragma unroll
+      for (int i = 0; i < NV; i++) jar += cr.J(r, i) * S.warm[i];
+      const float fs = jar < 0.f ? -jar / cr.S(r, 1) : 0.f;
+      cr.S(r, 3) = fs;
+#pragma unroll
+      for (int i = 0; i < NV; i++) v[i] += cr.W(r, i) * fs;
+    }
+  // dual cost of the warm start: sum_r 0.5 f_r (J_r v - aref_r + R_r f_r) + 0.5 f_r (J_r qacc_smooth - aref_r)
+#pragma unroll
+  for (int s = 0; s < 3 * NA; s++) {
+    const int i = slot_dof(s);
+    const float sg = slot_sgn(s);
+    cost += 0.5f * f[s] * (sg * v[i] - aref[s] + R[s] * f[s]) + 0.5f * f[s] * (sg * S.qacc_s[i] - aref[s]);
+  }
+  for (int c = 0; c < nl; c++) {
+    const int fl = (int)L.at(c, F_FLAGS);
+    const bool ta = fl & TOUCH_ARM, tf = fl & TOUCH_FREE;
+    float jn[NV], jt1[NV], jt2[NV];
+#pragma unroll
+    for (int i = 0; i < NV; i++) jn[i] = L.at(c, i), jt1[i] = L.at(c, 12 + i), jt2[i] = L.at(c, 24 + i);
+    const float mu = L.at(c, F_MU), Rp = L.at(c, F_R);
+#pragma unroll
+    for (int ed = 0; ed < 4; ed++) {
+      const float fr = L.at(c, F_FRC + ed);
+      if (fr == 0.f) continue;
+      float J[NV];
+      edge_J<NV>(jn, jt1, jt2, ed, mu, J);
+      const float ar = L.at(c, F_AREF + ed);
+      cost += 0.5f * fr * (dotv<NA, NF>(J, v, ta, tf) - ar + Rp * fr) +
+              0.5f * fr * (dotv<NA, NF>(J, S.qacc_s, ta, tf) - ar);
+    }
+  }
+  for (int c = nl; c < ncon; c++)
+    for (int ed = 0; ed < 4; ed++) {
+      const int r = 4 * c + ed;
       float jv = 0.f, jq = 0.f;
 #pragma unroll
       for (int i = 0; i < NV; i++) {
@@ -208,16 +364,18 @@ DEVI void solve_constraints(Sim<NA, NF>& S, const ConLds& C, int ncon, const Con
       const float fr = cr.S(r, 3), ar = cr.S(r, 0);
       cost += 0.5f * fr * (jv - ar + cr.S(r, 1) * fr) + 0.5f * fr * (jq - ar);
     }
-    if (cost > 0.f) {
+  if (cost > 0.f) {
 #pragma unroll
-      for (int s = 0; s < 3 * NA; s++) f[s] = 0.f;
-      for (int r = 0; r < ne; r++) cr.S(r, 3) = 0.f;
+    for (int s = 0; s < 3 * NA; s++) f[s] = 0.f;
+    for (int c = 0; c < nl; c++)
 #pragma unroll
-      for (int i = 0; i < NV; i++) v[i] = S.qacc_s[i];
-    }
+      for (int ed = 0; ed < 4; ed++) L.at(c, F_FRC + ed) = 0.f;
+    for (int r = 4 * nl; r < 4 * ncon; r++) cr.S(r, 3) = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; i++) v[i] = S.qacc_s[i];
   }
 
-  // ---- projected Gauss-Seidel sweeps
+  // ---- projected Gauss-Seidel sweeps (MuJoCo improvement criterion, scaled by 1/trace(M))
   float tr = 0.f;
 #pragma unroll
   for (int i = 0; i < NA; i++) tr += S.MA[i * (i + 1) / 2 + i];
@@ -234,7 +392,7 @@ DEVI void solve_constraints(Sim<NA, NF>& S, const ConLds& C, int ncon, const Con
       const int i = slot_dof(s);
       const float sg = slot_sgn(s);
       const float res = sg * v[i] - aref[s] + R[s] * f[s];
-      float fn = f[s] - res / ARd[s];
+      float fn = f[s] - res * iARd[s];
       if (s < NA) {
         const float fl = m.dof_frictionloss[i];
         fn = fminf(fmaxf(fn, -fl), fl);
@@ -243,27 +401,61 @@ DEVI void solve_constraints(Sim<NA, NF>& S, const ConLds& C, int ncon, const Con
       }
       const float df = fn - f[s];
 #pragma unroll
-      for (int k = 0; k < NA; k++) v[k] += Wa[i][k] * sg * df;
+      for (int k = 0; k < NA; k++) v[k] += Mi.a(i, k) * sg * df;
       f[s] = fn;
       improvement -= df * res + 0.5f * ARd[s] * df * df;
     }
-    for (int r = 0; r < ne; r++) {
+    for (int c = 0; c < nl; c++) {
+      const int fl = (int)L.at(c, F_FLAGS);
+      const bool ta = fl & TOUCH_ARM, tf = fl & TOUCH_FREE;
+      float jn[NV], jt1[NV], jt2[NV];
+#pragma unroll
+      for (int i = 0; i < NV; i++) jn[i] = jt1[i] = jt2[i] = 0.f;
+      if (ta) {
+#pragma unroll
+        for (int i = 0; i < NA; i++) jn[i] = L.at(c, i), jt1[i] = L.at(c, 12 + i), jt2[i] = L.at(c, 24 + i);
+      }
+      if (tf) {
+#pragma unroll
+        for (int i = NA; i < NV; i++) jn[i] = L.at(c, i), jt1[i] = L.at(c, 12 + i), jt2[i] = L.at(c, 24 + i);
+      }
+      const float mu = L.at(c, F_MU), Rp = L.at(c, F_R);
+#pragma unroll
+      for (int ed = 0; ed < 4; ed++) {
+        float J[NV];
+        edge_J<NV>(jn, jt1, jt2, ed, mu, J);
+        const float fo = L.at(c, F_FRC + ed), ard = L.at(c, F_ARD + ed);
+        const float res = dotv<NA, NF>(J, v, ta, tf) - L.at(c, F_AREF + ed) + Rp * fo;
+        const float fnew = fmaxf(fo - res * L.at(c, F_IARD + ed), 0.f);
+        const float df = fnew - fo;
+        if (df != 0.f) {
+          float W[NV];
+          Mi.mul(J, W, ta, tf);
+#pragma unroll
+          for (int i = 0; i < NV; i++) v[i] += W[i] * df;
+          L.at(c, F_FRC + ed) = fnew;
+          improvement -= df * res + 0.5f * ard * df * df;
+        }
+      }
+    }
+    for (int r = 4 * nl; r < 4 * ncon; r++) {
       float res = -cr.S(r, 0) + cr.S(r, 1) * cr.S(r, 3);
 #pragma unroll
       for (int i = 0; i < NV; i++) res += cr.J(r, i) * v[i];
       const float fo = cr.S(r, 3);
-      const float fn = fmaxf(fo - res / cr.S(r, 2), 0.f);
-      const float df = fn - fo;
+      const float fnew = fmaxf(fo - res / cr.S(r, 2), 0.f);
+      const float df = fnew - fo;
       if (df != 0.f) {
 #pragma unroll
         for (int i = 0; i < NV; i++) v[i] += cr.W(r, i) * df;
-        cr.S(r, 3) = fn;
+        cr.S(r, 3) = fnew;
         improvement -= df * res + 0.5f * cr.S(r, 2) * df * df;
       }
     }
     if (improvement * scale < m.tolerance) break;
   }
 
+  // ---- qacc and qfrc_constraint = J' f
 #pragma unroll
   for (int i = 0; i < NV; i++) {
     S.qacc[i] = v[i];
@@ -271,11 +463,26 @@ DEVI void solve_constraints(Sim<NA, NF>& S, const ConLds& C, int ncon, const Con
   }
 #pragma unroll
   for (int s = 0; s < 3 * NA; s++) S.fcon[slot_dof(s)] += slot_sgn(s) * f[s];
-  for (int r = 0; r < ne; r++) {
+  for (int c = 0; c < nl; c++) {
+    float jn[NV], jt1[NV], jt2[NV];
+#pragma unroll
+    for (int i = 0; i < NV; i++) jn[i] = L.at(c, i), jt1[i] = L.at(c, 12 + i), jt2[i] = L.at(c, 24 + i);
+    const float mu = L.at(c, F_MU);
+#pragma unroll
+    for (int ed = 0; ed < 4; ed++) {
+      float J[NV];
+      edge_J<NV>(jn, jt1, jt2, ed, mu, J);
+      const float fr = L.at(c, F_FRC + ed);
+#pragma unroll
+      for (int i = 0; i < NV; i++) S.fcon[i] += J[i] * fr;
+    }
+  }
+  for (int r = 4 * nl; r < 4 * ncon; r++) {
     const float fr = cr.S(r, 3);
 #pragma unroll
     for (int i = 0; i < NV; i++) S.fcon[i] += cr.J(r, i) * fr;
   }
+  return ncon;
 }
 
 }  // namespace soarm

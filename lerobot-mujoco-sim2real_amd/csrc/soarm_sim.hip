@@ -48,6 +48,14 @@ struct sim_batch {
   int32_t *d_hadr = nullptr, *d_hadj = nullptr;
   float* d_scratch = nullptr;  // contact rows, [slot][env]
   size_t scratch_floats = 0;
+  float* d_gpose = nullptr;    // geom world poses [geom*12+k][env]
+  float* d_cbuf = nullptr;     // collide output [slot*7+f][env]
+  int* d_ccount = nullptr;     // contacts per pair [pair][env]
+  // profiling (sim_profile_begin/end)
+  bool prof = false;
+  std::vector<hipEvent_t> ev_pool;
+  size_t ev_used = 0;
+  std::vector<std::pair<int, size_t>> ev_marks;  // (kind, index of start event)
   sim_params params{nullptr, nullptr, nullptr};
 };
 
@@ -67,6 +75,13 @@ __host__ __device__ inline u4 philox(u4 c, uint32_t k0, uint32_t k1) {
   return c;
 }
 __host__ __device__ inline float u01(uint32_t x) { return (float)(x >> 8) * (1.0f / 16777216.0f); }
+// lo + (hi - lo) u with two roundings (no FMA contraction): the host mirror
+// (sim.reset_qpos_draw / workloads.philox_uniform) reproduces it bit for bit
+__host__ __device__ inline float uniform_range(float lo, float width, float u) {
+#pragma clang fp contract(off)
+  const float t = width * u;
+  return lo + t;
+}
 
 // -------------------------------------------------------------------- kernels
 template <int NA, int NF>
@@ -114,24 +129,23 @@ DEVI void write_obs(const Sim<NA, NF>& S, float* obs, int e) {
   }
 }
 
-// one mj_forward (position + velocity + acceleration stages)
+// one mj_forward (position + velocity + acceleration stages); the contacts
+// (cbuf/ccount, may be null) were produced by k_collide from this substep's positions
 template <int NA, int NF, bool CON>
-DEVI int forward(Sim<NA, NF>& S, const GeomLds& G, const ConLds& C, const ContactRows<NA, NF>& cr) {
+DEVI int forward(Sim<NA, NF>& S, const float* cbuf, const int* ccount, int n, int e, const RowLds& L,
+                 const ContactRows<NA, NF>& cr) {
   S.kinematics();
   S.com_crb();
   S.factor();
-  int ncon = 0;
-  if constexpr (CON) ncon = collide<NA, NF>(S, G, C);
   S.smooth_forces();
-  solve_constraints<NA, NF, CON>(S, C, ncon, cr);
-  return ncon;
+  return solve_constraints<NA, NF, CON>(S, cbuf, ccount, n, e, L, cr);
 }
 
-template <int NA, int NF, bool CON>
+// contact-free scenes (mjDSBL_CONTACT): all frame_skip substeps fused in one launch
+template <int NA, int NF>
 __global__ __launch_bounds__(64) void k_step(const DModel* __restrict__ dm, int n, int nsub,
                                              sim_state st, const float* __restrict__ action,
-                                             float* __restrict__ obs, sim_params pp,
-                                             float* __restrict__ scratch) {
+                                             float* __restrict__ obs, sim_params pp) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
   const DModel& m = *dm;
@@ -143,25 +157,141 @@ __global__ __launch_bounds__(64) void k_step(const DModel* __restrict__ dm, int 
     for (int k = 0; k < NA; k++)
       if (k < m.nact) S.ctrl[k] = action[(size_t)e * m.nact + k];
   }
-  __shared__ float s_geom[CON ? CON_MAXG * 12 : 1][64];
-  __shared__ float s_con[CON ? SIM_MAXCON * 8 : 1][64];
-  const GeomLds G{s_geom, (int)threadIdx.x};
-  const ConLds C{s_con, (int)threadIdx.x};
-  ContactRows<NA, NF> cr{scratch + e, n};
-  float ncon_acc = 0.f;
+  const RowLds L{nullptr, 0};
+  const ContactRows<NA, NF> cr{nullptr, n};
   for (int s = 0; s < nsub; s++) {
     S.relaunder();
     S.check_state();
-    ncon_acc += forward<NA, NF, CON>(S, G, C, cr);
+    forward<NA, NF, false>(S, nullptr, nullptr, n, e, L, cr);
     if (S.acc_bad()) {
       S.soft_reset(SIM_ST_BADQACC);
-      forward<NA, NF, CON>(S, G, C, cr);
+      forward<NA, NF, false>(S, nullptr, nullptr, n, e, L, cr);
     }
     S.integrate();
   }
   store_state(S, st, n, e);
-  if (st.ncon) st.ncon[e] += ncon_acc;
   if (obs) write_obs(S, obs, e);
+}
+
+// geom world poses from the current qpos (collision input)
+template <int NA, int NF>
+__global__ __launch_bounds__(64) void k_geom(const DModel* __restrict__ dm, int n, sim_state st,
+                                             float* __restrict__ gpose) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  Sim<NA, NF> S(dm, 1.f, -1.f, 1.f);
+  load_state(S, st, n, e);
+  S.kinematics();
+  write_geom_poses(S, gpose, n, e);
+}
+
+// mj_collision, one lane per (env, candidate pair); blockIdx.y = pair
+__global__ __launch_bounds__(256) void k_collide(const DModel* __restrict__ dm, int n,
+                                                 const float* __restrict__ gpose,
+                                                 float* __restrict__ cbuf, int* __restrict__ ccount) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const int p = blockIdx.y;
+  if (e >= n) return;
+  const DModel& m = *dm;
+  GeomPose P1, P2;
+  load_pose(gpose, n, e, m.pair_geom1[p], P1);
+  load_pose(gpose, n, e, m.pair_geom2[p], P2);
+  PairOut o;
+  collide_pair(m, p, P1, P2, o);
+  ccount[(size_t)p * n + e] = o.n;
+  const int s0 = m.pair_slot[p];
+#pragma unroll
+  for (int k = 0; k < PAIR_MAXCON; k++)
+    if (k < o.n)
+#pragma unroll
+      for (int f = 0; f < 7; f++) cbuf[((size_t)(s0 + k) * 7 + f) * n + e] = o.c[k][f];
+}
+
+// walk the pairs in order and append their contacts (deterministic indexing)
+DEVI int gather_contacts(const DModel& m, int n, int e, const float* __restrict__ cbuf,
+                         const int* __restrict__ ccount, const ConLds& C, int& status) {
+  int ncon = 0;
+  for (int p = 0; p < m.npair; p++) {
+    const int c = ccount[(size_t)p * n + e];
+    const int s0 = m.pair_slot[p];
+    for (int k = 0; k < c; k++) {
+      if (ncon >= SIM_MAXCON) {
+        status |= SIM_ST_CONOVERFLOW;
+        break;
+      }
+      C.dist(ncon) = cbuf[((size_t)(s0 + k) * 7) * n + e];
+#pragma unroll
+      for (int f = 0; f < 3; f++) {
+        C.pos(ncon, f) = cbuf[((size_t)(s0 + k) * 7 + 1 + f) * n + e];
+        C.n(ncon, f) = cbuf[((size_t)(s0 + k) * 7 + 4 + f) * n + e];
+      }
+      C.set_pair(ncon, p);
+      ncon++;
+    }
+  }
+  return ncon;
+}
+
+// one substep with contacts: gather -> forward -> Euler -> next substep's geom poses
+template <int NA, int NF>
+__global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, int n, sim_state st,
+                                                const float* __restrict__ action,
+                                                float* __restrict__ obs, sim_params pp,
+                                                float* __restrict__ scratch,
+                                                const float* __restrict__ cbuf,
+                                                const int* __restrict__ ccount,
+                                                float* __restrict__ gpose) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const DModel& m = *dm;
+  Sim<NA, NF> S(dm, pp.mass_scale ? pp.mass_scale[e] : 1.f, pp.friction ? pp.friction[e] : -1.f,
+                pp.damping_scale ? pp.damping_scale[e] : 1.f);
+  load_state(S, st, n, e);
+  if (action) {
+#pragma unroll
+    for (int k = 0; k < NA; k++)
+      if (k < m.nact) S.ctrl[k] = action[(size_t)e * m.nact + k];
+  }
+  __shared__ float s_rows[LDS_CON * CF][64];
+  const RowLds L{s_rows, (int)threadIdx.x};
+  const ContactRows<NA, NF> cr{scratch + e, n};
+  const int st0 = S.status;
+  S.check_state();
+  // a soft reset moved the env: the collide output no longer applies
+  const bool use = S.status == st0 && ccount != nullptr;
+  int ncon = forward<NA, NF, true>(S, use ? cbuf : nullptr, use ? ccount : nullptr, n, e, L, cr);
+  if (S.acc_bad()) {
+    S.soft_reset(SIM_ST_BADQACC);
+    ncon = forward<NA, NF, true>(S, nullptr, nullptr, n, e, L, cr);
+  }
+  const float ee[3] = {S.ee[0], S.ee[1], S.ee[2]};
+  S.integrate();
+  store_state(S, st, n, e);
+  if (st.ncon) st.ncon[e] += (float)ncon;
+  if (obs) {
+    S.ee[0] = ee[0], S.ee[1] = ee[1], S.ee[2] = ee[2];
+    write_obs(S, obs, e);
+  }
+  if (gpose) {
+    S.kinematics();
+    write_geom_poses(S, gpose, n, e);
+  }
+}
+
+// diagnostic: compacted contact list [N][SIM_MAXCON][8] (dist, pos, normal, pair) + count
+__global__ __launch_bounds__(64) void k_gather(const DModel* __restrict__ dm, int n,
+                                               const float* __restrict__ cbuf,
+                                               const int* __restrict__ ccount, float* __restrict__ out,
+                                               int* __restrict__ nout) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  __shared__ float s_con[SIM_MAXCON * 8][64];
+  const ConLds C{s_con, (int)threadIdx.x};
+  int status = 0;
+  const int nc = gather_contacts(*dm, n, e, cbuf, ccount, C, status);
+  for (int c = 0; c < nc; c++)
+    for (int f = 0; f < 8; f++) out[((size_t)e * SIM_MAXCON + c) * 8 + f] = s_con[c * 8 + f][threadIdx.x];
+  nout[e] = nc;
 }
 
 template <int NA, int NF>
@@ -192,7 +322,7 @@ __global__ __launch_bounds__(64) void k_reset(const DModel* __restrict__ dm, int
   const uint32_t rr[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
   for (int k = 0; k < m.obs_nq; k++) {
     const int a = m.obs_qadr[k];  // arm joint: qpos address == dof address
-    const float qv = init_qpos ? init_qpos[(size_t)k * n + e] : -0.3f + 0.6f * u01(rr[k & 7]);
+    const float qv = init_qpos ? init_qpos[(size_t)k * n + e] : uniform_range(-0.3f, 0.6f, u01(rr[k & 7]));
     const float vv = init_qvel ? init_qvel[(size_t)k * n + e] : 0.f;
 #pragma unroll
     for (int i = 0; i < NQ; i++)
@@ -308,6 +438,18 @@ static void dispatch_nf(int nf, F&& f) {
 }
 
 static inline dim3 grid_for(int n) { return dim3((n + 63) / 64); }
+
+// profiling: kind >= 0 records a start event for that kernel kind, -1 the matching stop
+static void prof_mark(sim_batch* b, int kind, hipStream_t st) {
+  if (!b->prof) return;
+  if (b->ev_used == b->ev_pool.size()) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return;
+    b->ev_pool.push_back(e);
+  }
+  if (kind >= 0) b->ev_marks.emplace_back(kind, b->ev_used);
+  (void)hipEventRecord(b->ev_pool[b->ev_used++], st);
+}
 
 // ------------------------------------------------------------------ model
 static float host_impedance(const double* si, double pos, double margin) {
@@ -463,6 +605,20 @@ static int validate_and_build(const sim_model_desc& d, sim_model* M) {
     m.pair_margin[p] = (float)std::fmax(d.geom_margin[g1], d.geom_margin[g2]);
     m.pair_tran[p] = (float)(d.body_invweight0[d.geom_bodyid[g1]][0] + d.body_invweight0[d.geom_bodyid[g2]][0]);
     m.pair_friction[p] = (float)std::fmax(d.geom_friction[g1][0], d.geom_friction[g2][0]);
+    // slot capacity: box-box and plane-box can return up to 4 contacts, the rest 1
+    const int t1 = d.geom_type[g1], t2 = d.geom_type[g2];
+    const int cap = (t2 == SIM_GEOM_BOX && (t1 == SIM_GEOM_BOX || t1 == SIM_GEOM_PLANE)) ? 4 : 1;
+    m.pair_slot[p] = m.nslot;
+    m.nslot += cap;
+  }
+  // free bodies: the kernels use a diagonal 6x6 mass block, which needs the inertia frame at
+  // the body frame (ipos = 0, iquat = identity) — true for the build-defined cube
+  m.free_diag = 1;
+  for (int b2 = 2 + na; b2 < d.nbody; b2++) {
+    const double* ip = d.body_ipos[b2];
+    const double* iq = d.body_iquat[b2];
+    if (ip[0] != 0 || ip[1] != 0 || ip[2] != 0 || iq[0] != 1 || iq[1] != 0 || iq[2] != 0 || iq[3] != 0)
+      return fail(SIM_E_MODEL, "free bodies need ipos = 0 and an inertia frame equal to the body frame");
   }
   for (int s = 0; s < d.nsite; s++) {
     m.site_bodyid[s] = d.site_bodyid[s];
@@ -543,6 +699,9 @@ int sim_batch_create(const sim_model* m, int n_envs, int device, sim_batch** out
     const int nv = m->desc.nv;
     B->scratch_floats = (size_t)4 * SIM_MAXCON * (2 * nv + 4) * n_envs;
     HIPCHECK(hipMalloc(&B->d_scratch, B->scratch_floats * sizeof(float)));
+    HIPCHECK(hipMalloc(&B->d_gpose, (size_t)m->desc.ngeom * 12 * n_envs * sizeof(float)));
+    HIPCHECK(hipMalloc(&B->d_cbuf, (size_t)(m->dm.nslot > 0 ? m->dm.nslot : 1) * 7 * n_envs * sizeof(float)));
+    HIPCHECK(hipMalloc(&B->d_ccount, (size_t)(m->desc.npair > 0 ? m->desc.npair : 1) * n_envs * sizeof(int)));
   }
   *out = B;
   return SIM_OK;
@@ -556,6 +715,10 @@ void sim_batch_free(sim_batch* b) {
   (void)hipFree(b->d_hadr);
   (void)hipFree(b->d_hadj);
   (void)hipFree(b->d_scratch);
+  (void)hipFree(b->d_gpose);
+  (void)hipFree(b->d_cbuf);
+  (void)hipFree(b->d_ccount);
+  for (auto e : b->ev_pool) (void)hipEventDestroy(e);
   delete b;
 }
 
@@ -594,20 +757,84 @@ int sim_step(sim_batch* b, const sim_state* s, const float* action, int frame_sk
   if (frame_skip < 1) return fail(SIM_E_ARG, "frame_skip must be >= 1");
   hipStream_t st = (hipStream_t)stream;
   const bool con = !b->model->desc.disable_contact;
-  if (con)
+  if (!con) {
     dispatch_nf(b->model->nf, [&](auto nfc) {
+      constexpr int NA = 6, NF = decltype(nfc)::value;
+      prof_mark(b, 0, st);
+      hipLaunchKernelGGL((k_step<NA, NF>), grid_for(b->n), dim3(64), 0, st, b->d_model, b->n,
+                         frame_skip, *s, action, obs, b->params);
+      prof_mark(b, -1, st);
+    });
+    HIPCHECK(hipGetLastError());
+    return SIM_OK;
+  }
+  // contacts: geom poses, then per substep (env, pair)-parallel collide + per-env dynamics
+  const int np = b->model->desc.npair;
+  dispatch_nf(b->model->nf, [&](auto nfc) {
     constexpr int NA = 6, NF = decltype(nfc)::value;
-    hipLaunchKernelGGL((k_step<NA, NF, true>), grid_for(b->n), dim3(64), 0, st,
-                                               b->d_model, b->n, frame_skip, *s, action, obs, b->params,
-                                               b->d_scratch);
+    prof_mark(b, 3, st);
+    hipLaunchKernelGGL((k_geom<NA, NF>), grid_for(b->n), dim3(64), 0, st, b->d_model, b->n, *s,
+                       b->d_gpose);
+    prof_mark(b, -1, st);
+    for (int sub = 0; sub < frame_skip; sub++) {
+      if (np > 0) {
+        prof_mark(b, 1, st);
+        hipLaunchKernelGGL(k_collide, dim3((b->n + 255) / 256, np), dim3(256), 0, st, b->d_model, b->n,
+                           b->d_gpose, b->d_cbuf, b->d_ccount);
+        prof_mark(b, -1, st);
+      }
+      const bool last = sub == frame_skip - 1;
+      prof_mark(b, 2, st);
+      hipLaunchKernelGGL((k_substep<NA, NF>), grid_for(b->n), dim3(64), 0, st, b->d_model, b->n, *s,
+                         sub == 0 ? action : nullptr, last ? obs : nullptr, b->params, b->d_scratch,
+                         b->d_cbuf, np > 0 ? b->d_ccount : nullptr, last ? nullptr : b->d_gpose);
+      prof_mark(b, -1, st);
+    }
   });
-  else
-    dispatch_nf(b->model->nf, [&](auto nfc) {
+  HIPCHECK(hipGetLastError());
+  return SIM_OK;
+}
+
+int sim_profile_begin(sim_batch* b) {
+  if (!b) return fail(SIM_E_ARG, "null batch");
+  b->prof = true;
+  b->ev_used = 0;
+  b->ev_marks.clear();
+  return SIM_OK;
+}
+
+int sim_profile_end(sim_batch* b, double* ms, int32_t* launches) {
+  if (!b || !ms || !launches) return fail(SIM_E_ARG, "null argument");
+  b->prof = false;
+  for (int k = 0; k < SIM_PROF_KINDS; k++) ms[k] = 0, launches[k] = 0;
+  for (auto& mk : b->ev_marks) {
+    HIPCHECK(hipEventSynchronize(b->ev_pool[mk.second + 1]));
+    float t = 0.f;
+    HIPCHECK(hipEventElapsedTime(&t, b->ev_pool[mk.second], b->ev_pool[mk.second + 1]));
+    ms[mk.first] += t;
+    launches[mk.first] += 1;
+  }
+  b->ev_marks.clear();
+  b->ev_used = 0;
+  return SIM_OK;
+}
+
+int sim_contacts(sim_batch* b, const sim_state* s, float* out, int32_t* ncon, void* stream) {
+  if (int rc = check_state(b, s)) return rc;
+  if (!out || !ncon) return fail(SIM_E_ARG, "null output");
+  if (b->model->desc.disable_contact) return fail(SIM_E_ARG, "model compiled with contacts disabled");
+  hipStream_t st = (hipStream_t)stream;
+  const int np = b->model->desc.npair;
+  dispatch_nf(b->model->nf, [&](auto nfc) {
     constexpr int NA = 6, NF = decltype(nfc)::value;
-    hipLaunchKernelGGL((k_step<NA, NF, false>), grid_for(b->n), dim3(64), 0, st,
-                                               b->d_model, b->n, frame_skip, *s, action, obs, b->params,
-                                               b->d_scratch);
+    hipLaunchKernelGGL((k_geom<NA, NF>), grid_for(b->n), dim3(64), 0, st, b->d_model, b->n, *s,
+                       b->d_gpose);
   });
+  if (np > 0)
+    hipLaunchKernelGGL(k_collide, dim3((b->n + 255) / 256, np), dim3(256), 0, st, b->d_model, b->n,
+                       b->d_gpose, b->d_cbuf, b->d_ccount);
+  hipLaunchKernelGGL(k_gather, grid_for(b->n), dim3(64), 0, st, b->d_model, b->n, b->d_cbuf, b->d_ccount,
+                     out, ncon);
   HIPCHECK(hipGetLastError());
   return SIM_OK;
 }

@@ -19,6 +19,35 @@ def _ptr(t):
     return None if t is None else C.c_void_p(t.data_ptr())
 
 
+def philox4x32(ctr, key):
+    """Philox4x32-10 on uint32 arrays ctr [n, 4], key (k0, k1) -> [n, 4] (mirror of the device RNG)."""
+    c = np.array(ctr, dtype=np.uint64) & 0xFFFFFFFF
+    k0, k1 = np.uint64(key[0]), np.uint64(key[1])
+    m = np.uint64(0xFFFFFFFF)
+    for _ in range(10):
+        p0 = np.uint64(0xD2511F53) * c[:, 0]
+        p1 = np.uint64(0xCD9E8D57) * c[:, 2]
+        hi0, lo0 = p0 >> np.uint64(32), p0 & m
+        hi1, lo1 = p1 >> np.uint64(32), p1 & m
+        c = np.stack([hi1 ^ c[:, 1] ^ k0, lo1, hi0 ^ c[:, 3] ^ k1, lo0], 1)
+        k0 = (k0 + np.uint64(0x9E3779B9)) & m
+        k1 = (k1 + np.uint64(0xBB67AE85)) & m
+    return c.astype(np.uint32)
+
+
+def reset_qpos_draw(seed, env_ids, nobs=5):
+    """The U(-0.3, 0.3) initial joint angles sim_reset draws on device for env ids (float32)."""
+    ids = np.asarray(env_ids, dtype=np.uint64)
+    k = (int(seed) & 0xFFFFFFFF, (int(seed) >> 32) & 0xFFFFFFFF)
+    out = []
+    for blk in range(2):
+        ctr = np.stack([ids & 0xFFFFFFFF, ids >> np.uint64(32), np.full_like(ids, blk), np.zeros_like(ids)], 1)
+        out.append(philox4x32(ctr, k))
+    r = np.concatenate(out, 1)[:, :nobs]
+    u = (r >> 8).astype(np.float32) * np.float32(1.0 / 16777216.0)
+    return np.float32(-0.3) + np.float32(0.6) * u
+
+
 class BatchSim:
     """`n_envs` SO-ARM101 environments stepped in lockstep on one GPU."""
 
@@ -127,6 +156,25 @@ class BatchSim:
         abi.check(self.lib, self.lib.sim_observe(self._batch, C.byref(self._state), _ptr(self.obs),
                                                  self._stream()))
         return self.obs
+
+    def profile_begin(self):
+        abi.check(self.lib, self.lib.sim_profile_begin(self._batch))
+
+    def profile_end(self):
+        """{kind: (total_ms, launches)} for the launches since profile_begin (synchronises)."""
+        ms = (C.c_double * 4)()
+        cnt = (C.c_int32 * 4)()
+        abi.check(self.lib, self.lib.sim_profile_end(self._batch, C.cast(ms, C.c_void_p), C.cast(cnt, C.c_void_p)))
+        return {k: (ms[i], cnt[i]) for i, k in enumerate(abi.PROF_KINDS)}
+
+    def contacts(self):
+        """Contacts at the current positions: (list [n][MAXCON][8], ncon [n]).
+        Fields: dist, pos(3), normal(3) geom1->geom2, pair id (int32 bits)."""
+        out = self.torch.zeros((self.n, abi.MAXCON, 8), dtype=self.torch.float32, device=self.device)
+        nc = self.torch.zeros(self.n, dtype=self.torch.int32, device=self.device)
+        abi.check(self.lib, self.lib.sim_contacts(self._batch, C.byref(self._state), _ptr(out), _ptr(nc),
+                                                  self._stream()))
+        return out, nc
 
     def ik(self, target, q=None, tol=1e-6, regularization_threshold=0.1, regularization_strength=1e-2,
            max_update_norm=2.0, progress_thresh=20.0, max_steps=100, ndof=5):

@@ -1,0 +1,79 @@
+"""Synthetic workloads of BASELINE.json ``configs``.
+
+Every random draw is Philox4x32-10 keyed by (seed, global env id), so the
+same env gets the same initial state, inputs and DR parameters whether the
+batch runs on 1 or 8 GPUs.
+
+* ``nocontact`` (config 2): arm on the table, collision disabled (frictionloss
+  and joint limits on), qpos ~ U(-0.3, 0.3)^5, random actions U[-0.5, 0.5)^5
+  every env-step (``SOARM101_DataCollection.py:132``).
+* ``contact`` (config 3, the headline): build-defined pick scene — the cube
+  (half-size 0.015 m, 0.03 kg) rests on the table at (0.25 +- 0.05, +-0.05);
+  arm starts U(-0.3, 0.3)^5; chirp actions (``SineInputGenerator`` mode
+  "chirp", tables drawn per env, ``:31-74``); contacts via PGS.
+* ``dr`` (config 4): ``contact`` + per-env domain randomisation: body mass
+  x U(0.8, 1.2) (inertia scaled alike), sliding friction U(0.5, 1.5), dof
+  damping x U(0.8, 1.2).
+"""
+import numpy as np
+
+from .mjcf import CUBE_SCENE_XML, SCENE_XML, compile_mjcf
+from .sim import philox4x32
+
+CONFIGS = {
+    "nocontact": dict(xml=SCENE_XML, disable_contact=True, action="random", dr=False,
+                      desc="4096 SO-ARM101 envs, contact-free arm dynamics (config 2)"),
+    "contact": dict(xml=CUBE_SCENE_XML, disable_contact=False, action="chirp", dr=False,
+                    desc="4096 SO-ARM101 envs, tabletop+cube contacts, PGS (config 3, pick scene)"),
+    "dr": dict(xml=CUBE_SCENE_XML, disable_contact=False, action="chirp", dr=True,
+               desc="SO-ARM101 pick scene with per-env mass/friction/damping DR (config 4)"),
+}
+
+
+def philox_uniform(seed, ids, k):
+    """[n, k] float32 uniforms in [0, 1) keyed by (seed, env id)."""
+    ids = np.asarray(ids, dtype=np.uint64)
+    key = (int(seed) & 0xFFFFFFFF, (int(seed) >> 32) & 0xFFFFFFFF)
+    blocks = []
+    for b in range((k + 3) // 4):
+        ctr = np.stack([ids & 0xFFFFFFFF, ids >> np.uint64(32), np.full_like(ids, b), np.zeros_like(ids)], 1)
+        blocks.append(philox4x32(ctr, key))
+    r = np.concatenate(blocks, 1)[:, :k]
+    return (r >> 8).astype(np.float32) * np.float32(1.0 / 16777216.0)
+
+
+def model(name, **kw):
+    c = CONFIGS[name]
+    return compile_mjcf(c["xml"], disable_contact=c["disable_contact"], **kw)
+
+
+def initial_qpos(cm, ids, seed=0):
+    """Full qpos [n, nq] float32: arm U(-0.3, 0.3)^5 (gripper 0), cube resting on the table."""
+    n = len(ids)
+    q = np.tile(cm.qpos0().astype(np.float32), (n, 1))
+    q[:, :5] = -0.3 + 0.6 * philox_uniform(seed, ids, 5)
+    if cm.nq > 6:
+        u = philox_uniform(seed + 1, ids, 2)
+        q[:, 6] = 0.25 + 0.1 * (u[:, 0] - 0.5)
+        q[:, 7] = 0.1 * (u[:, 1] - 0.5)
+        q[:, 8] = -0.0009 + 0.015
+    return q
+
+
+def chirp_tables(ids, seed=0, udim=5, freq_range=(0.0025, 0.05), amp_range=(-0.5, 0.5)):
+    u = philox_uniform(seed + 2, ids, 3 * udim).astype(np.float64)
+    f = freq_range[0] + (freq_range[1] - freq_range[0]) * u[:, :udim]
+    a = amp_range[0] + (amp_range[1] - amp_range[0]) * u[:, udim:2 * udim]
+    p = 2 * np.pi * u[:, 2 * udim:]
+    return dict(freq=f, amp=a, phase=p, freq_start=freq_range[0], freq_end=freq_range[1])
+
+
+def chirp_action(tab, t, lib=np, T_total=200):
+    """u = amp sin(2 pi (f + (f_end - f_start) t / T) t + phase)  (SineInputGenerator 'chirp')."""
+    f = tab["freq"] + (tab["freq_end"] - tab["freq_start"]) * (t / T_total)
+    return tab["amp"] * lib.sin(2 * np.pi * f * t + tab["phase"])
+
+
+def dr_params(ids, seed=0):
+    u = philox_uniform(seed + 3, ids, 3)
+    return dict(mass_scale=0.8 + 0.4 * u[:, 0], friction=0.5 + 1.0 * u[:, 1], damping_scale=0.8 + 0.4 * u[:, 2])

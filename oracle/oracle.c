@@ -584,6 +584,15 @@ void orc_make_constraint(const orc_model* om, orc_data* d) {
   d->flops += 30.0 * r;
 }
 
+/* solver statistics (single-threaded use): calls, sweeps, rows */
+static double orc_stats[3];
+void orc_solver_stats(double* out, int reset) {
+  for (int k = 0; k < 3; k++) {
+    out[k] = orc_stats[k];
+    if (reset) orc_stats[k] = 0;
+  }
+}
+
 /* ------------------------------------------------ PGS dual solver [ext mj_solPGS] */
 static double project(int type, double f, double fl) {
   if (type == ORC_EFC_FRICTION) return f < -fl ? -fl : (f > fl ? fl : f);
@@ -663,6 +672,9 @@ void orc_solve_pgs(const orc_model* om, orc_data* d) {
     }
   }
   d->solver_iter = it;
+  orc_stats[0] += 1;
+  orc_stats[1] += it;
+  orc_stats[2] += ne;
   memcpy(d->qacc, v, nv * sizeof(double));
   memcpy(d->efc_force, f, ne * sizeof(double));
   for (int i = 0; i < nv; i++) {
@@ -704,10 +716,11 @@ static int bad(double x) { return !(x == x) || fabs(x) > MAXVAL; }
 
 static void soft_reset(const orc_model* om, orc_data* d, int bit) {
   int st = d->status | bit;
-  double fl = d->flops;
+  double fl = d->flops, cf = d->cflops;
   orc_reset_data(om, d);
   d->status = st;
   d->flops = fl;
+  d->cflops = cf;
 }
 
 /* integrate positions: hinge/slide q += h v; free: pos += h v, quat *= exp(h w_local / 2) */
@@ -835,10 +848,10 @@ void orc_batch_step(const sim_model_desc* m, const float* hv, const int32_t* had
                     const int32_t* hadj, int n, double* qpos, double* qvel, double* warm,
                     double* ctrl, const double* action, int nsub, double* obs, int32_t* status,
                     double* ncon_sum, const double* params, int nthreads, double* flops) {
-  double fl_total = 0;
+  double fl_total = 0, cf_total = 0;
 #ifdef _OPENMP
   if (nthreads <= 0) nthreads = omp_get_max_threads();
-#pragma omp parallel for num_threads(nthreads) schedule(dynamic, 1) reduction(+ : fl_total)
+#pragma omp parallel for num_threads(nthreads) schedule(dynamic, 1) reduction(+ : fl_total, cf_total)
 #endif
   for (int e = 0; e < n; e++) {
     orc_model om;
@@ -869,9 +882,13 @@ void orc_batch_step(const sim_model_desc* m, const float* hv, const int32_t* had
     if (ncon_sum) ncon_sum[e] += nc;
     if (obs) write_obs(m, &d, obs + e * (3 + m->obs_nq));
     fl_total += d.flops;
+    cf_total += d.cflops;
   }
   (void)nthreads;
-  if (flops) *flops = fl_total;
+  if (flops) {
+    flops[0] = fl_total; /* total */
+    flops[1] = cf_total; /* of which collision */
+  }
 }
 
 int orc_debug_forward(const sim_model_desc* m, const float* hv, const int32_t* hadr,
@@ -917,4 +934,116 @@ int orc_debug_forward(const sim_model_desc* m, const float* hv, const int32_t* h
     for (int r = 0; r < d.nefc; r++) efc_force[r] = d.efc_force[r];
   if (nefc) *nefc = d.nefc;
   return d.ncon;
+}
+
+/* ---------------------------------------------------------------------------
+ * dm_control utils.inverse_kinematics.qpos_from_site_pose, position only
+ * [ext; restated from its published algorithm], as called at
+ * control/TrajectoryGenerator.py:96-107 (tol 1e-6, regularization_strength 1e-2,
+ * regularization_threshold 0.1, max_update_norm 2, progress_thresh 20,
+ * max_steps 100; joints = the first `ndof` hinges):
+ *   err = target - site_xpos; success if |err| < tol
+ *   J = mj_jacSite translational columns of the joints
+ *   reg = strength if |err| > threshold else 0
+ *   dq = solve(J'J + reg I, J'err)   (reg > 0)
+ *   dq = lstsq(J'J, J'err)           (reg = 0: minimum-norm, = J'(JJ')^-1 err)
+ *   halt if |err|/|dq| > progress_thresh; clip |dq| <= max_update_norm
+ *   mj_integratePos(q, dq, 1); joint limits are NOT enforced.
+ * q is [n][nq] row-major in/out.
+ * ------------------------------------------------------------------------- */
+static int chol_solve(int n, double A[8][8], double* x, const double* b) {
+  double L[8][8] = {{0}};
+  for (int i = 0; i < n; i++)
+    for (int j = 0; j <= i; j++) {
+      double s = A[i][j];
+      for (int k = 0; k < j; k++) s -= L[i][k] * L[j][k];
+      if (i == j) {
+        if (s <= 0) return -1;
+        L[i][i] = sqrt(s);
+      } else {
+        L[i][j] = s / L[j][j];
+      }
+    }
+  double y[8];
+  for (int i = 0; i < n; i++) {
+    double s = b[i];
+    for (int k = 0; k < i; k++) s -= L[i][k] * y[k];
+    y[i] = s / L[i][i];
+  }
+  for (int i = n - 1; i >= 0; i--) {
+    double s = y[i];
+    for (int k = i + 1; k < n; k++) s -= L[k][i] * x[k];
+    x[i] = s / L[i][i];
+  }
+  return 0;
+}
+
+void orc_ik_dls(const sim_model_desc* m, int n, const double* target, double* q, int32_t* ok,
+                int32_t* iters, double tol, double reg_thresh, double reg_strength,
+                double max_update, double progress_thresh, int max_steps, int site, int ndof) {
+  orc_model om;
+  make_om(&om, m, NULL, NULL, NULL, NULL);
+  for (int e = 0; e < n; e++) {
+    orc_data d;
+    orc_reset_data(&om, &d);
+    for (int i = 0; i < m->nq; i++) d.qpos[i] = q[e * m->nq + i];
+    const double* tg = target + 3 * e;
+    int success = 0, it;
+    for (it = 0; it < max_steps; it++) {
+      orc_kinematics(&om, &d);
+      double err[3];
+      for (int k = 0; k < 3; k++) err[k] = tg[k] - d.site_xpos[site][k];
+      double en = sqrt(err[0] * err[0] + err[1] * err[1] + err[2] * err[2]);
+      if (en < tol) {
+        success = 1;
+        break;
+      }
+      /* site Jacobian columns of the hinges that are ancestors of the site body */
+      double J[3][8] = {{0}};
+      int sb = m->site_bodyid[site];
+      for (int j = 0; j < ndof; j++) {
+        int b = m->jnt_bodyid[j], anc = 0;
+        for (int x = sb; x > 0; x = m->body_parentid[x])
+          if (x == b) anc = 1;
+        if (!anc) continue;
+        double r[3] = {d.site_xpos[site][0] - d.xanchor[j][0], d.site_xpos[site][1] - d.xanchor[j][1],
+                       d.site_xpos[site][2] - d.xanchor[j][2]};
+        double c[3] = {d.xaxis[j][1] * r[2] - d.xaxis[j][2] * r[1],
+                       d.xaxis[j][2] * r[0] - d.xaxis[j][0] * r[2],
+                       d.xaxis[j][0] * r[1] - d.xaxis[j][1] * r[0]};
+        for (int k = 0; k < 3; k++) J[k][j] = c[k];
+      }
+      double reg = en > reg_thresh ? reg_strength : 0.0;
+      double dq[8] = {0};
+      if (reg > 0) {
+        double H[8][8], g[8];
+        for (int a = 0; a < ndof; a++) {
+          g[a] = J[0][a] * err[0] + J[1][a] * err[1] + J[2][a] * err[2];
+          for (int b = 0; b < ndof; b++)
+            H[a][b] = J[0][a] * J[0][b] + J[1][a] * J[1][b] + J[2][a] * J[2][b] + (a == b ? reg : 0);
+        }
+        chol_solve(ndof, H, dq, g);
+      } else {
+        double A[8][8], y[3];
+        for (int a = 0; a < 3; a++)
+          for (int b = 0; b < 3; b++) {
+            double s = 0;
+            for (int k = 0; k < ndof; k++) s += J[a][k] * J[b][k];
+            A[a][b] = s;
+          }
+        if (chol_solve(3, A, y, err) != 0) break;
+        for (int k = 0; k < ndof; k++) dq[k] = J[0][k] * y[0] + J[1][k] * y[1] + J[2][k] * y[2];
+      }
+      double dn = 0;
+      for (int k = 0; k < ndof; k++) dn += dq[k] * dq[k];
+      dn = sqrt(dn);
+      if (en / dn > progress_thresh) break;
+      if (dn > max_update)
+        for (int k = 0; k < ndof; k++) dq[k] *= max_update / dn;
+      for (int k = 0; k < ndof; k++) d.qpos[m->jnt_qposadr[k]] += dq[k];
+    }
+    for (int i = 0; i < m->nq; i++) q[e * m->nq + i] = d.qpos[i];
+    if (ok) ok[e] = success;
+    if (iters) iters[e] = it;
+  }
 }

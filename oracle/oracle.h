@@ -78,6 +78,7 @@ typedef struct orc_data {
   int solver_iter;
   /* flop counter (SURVEY.md §8d binding procedure) */
   double flops;
+  double cflops; /* the collision share of flops */
 } orc_data;
 
 enum { ORC_EFC_FRICTION = 0, ORC_EFC_LIMIT = 1, ORC_EFC_CONTACT = 2 };
@@ -131,6 +132,9 @@ int orc_debug_forward(const sim_model_desc* m, const float* hv, const int32_t* h
 int orc_collide_geoms(const sim_model_desc* m, const float* hv, const int32_t* hadr,
                       const int32_t* hadj, const double* qpos, int g1, int g2, double* out,
                       int maxout);
+void orc_ik_dls(const sim_model_desc* m, int n, const double* target, double* q, int32_t* ok,
+                int32_t* iters, double tol, double reg_thresh, double reg_strength,
+                double max_update, double progress_thresh, int max_steps, int site, int ndof);
 #ifdef __cplusplus
 }
 #endif

@@ -21,8 +21,8 @@ _fp = np.ctypeslib.ndpointer(dtype=np.float32, flags="C_CONTIGUOUS")
 
 
 def build(force=False):
-    if force or not os.path.exists(LIB):
-        subprocess.check_call(["make", "-s", "-C", HERE])
+    """make is a no-op when liboracle.so is newer than its sources."""
+    subprocess.check_call(["make", "-s", "-C", HERE] + (["-B"] if force else []))
     return LIB
 
 
@@ -44,6 +44,10 @@ def lib():
         L.orc_debug_forward.restype = C.c_int
         L.orc_collide_geoms.argtypes = [vp] * 5 + [C.c_int, C.c_int, vp, C.c_int]
         L.orc_collide_geoms.restype = C.c_int
+        L.orc_ik_dls.argtypes = [vp, C.c_int, vp, vp, vp, vp] + [C.c_double] * 5 + [C.c_int] * 3
+        L.orc_ik_dls.restype = None
+        L.orc_hull_support_flat.argtypes = [vp] * 4 + [C.c_int, vp, C.c_int, C.c_int, vp]
+        L.orc_hull_support_flat.restype = C.c_int
         _lib = L
     return _lib
 
@@ -88,12 +92,13 @@ class Oracle:
         obs = np.zeros((n, 3 + d.obs_nq))
         a = None if action is None else np.ascontiguousarray(action, np.float64)
         pr = None if params is None else np.ascontiguousarray(params, np.float64)
-        fl = np.zeros(1)
+        fl = np.zeros(2)
         lib().orc_batch_step(self._desc_p, _p(self.hv), _p(self.hadr), _p(self.hadj), n,
                              _p(st["qpos"]), _p(st["qvel"]), _p(st["warm"]), _p(st["ctrl"]), _p(a),
                              nsub, _p(obs), _p(st["status"]), _p(st["ncon"]), _p(pr), nthreads,
                              _p(fl))
         self.last_flops = float(fl[0])
+        self.last_collision_flops = float(fl[1])
         return obs
 
     def forward(self, qpos, qvel=None, ctrl=None, warm=None):
@@ -114,6 +119,25 @@ class Oracle:
         return dict(M=M.reshape(nv, nv), bias=bias, qacc=qacc, ncon=ncon,
                     contacts=con.reshape(16, 9)[:ncon], site_xpos=site.reshape(-1, 3)[: d.nsite],
                     geom_xpos=gx.reshape(-1, 3)[: d.ngeom], efc_force=efc[: nefc.value])
+
+    def ik(self, target, q, tol=1e-6, regularization_threshold=0.1, regularization_strength=1e-2,
+           max_update_norm=2.0, progress_thresh=20.0, max_steps=100, ndof=5):
+        """dm_control qpos_from_site_pose restated; target [n,3], q [n,nq] (copied)."""
+        t = np.ascontiguousarray(target, np.float64).reshape(-1, 3)
+        q = np.array(q, dtype=np.float64, order="C").reshape(len(t), -1)
+        ok = np.zeros(len(t), np.int32)
+        it = np.zeros(len(t), np.int32)
+        lib().orc_ik_dls(self._desc_p, len(t), _p(t), _p(q), _p(ok), _p(it), tol,
+                         regularization_threshold, regularization_strength, max_update_norm,
+                         progress_thresh, max_steps, int(self.desc.obs_site), ndof)
+        return q, ok.astype(bool), it
+
+    def hull_support(self, g, dirs, use_graph=True):
+        d = np.ascontiguousarray(dirs, np.float64).reshape(-1, 3)
+        out = np.zeros(len(d), np.int32)
+        lib().orc_hull_support_flat(self._desc_p, _p(self.hv), _p(self.hadr), _p(self.hadj), g,
+                                    _p(d), len(d), int(use_graph), _p(out))
+        return out
 
     def collide(self, qpos, g1, g2, maxout=8):
         out = np.zeros(7 * 8)

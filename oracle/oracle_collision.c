@@ -26,6 +26,9 @@
 #define MPR_TOL 1e-6
 #define MPR_ITER 50
 
+/* algorithmic flop counter for collision work (SURVEY.md §8d binding procedure) */
+static __thread double g_cflops;
+
 static double dot3(const double a[3], const double b[3]) {
   return a[0] * b[0] + a[1] * b[1] + a[2] * b[2];
 }
@@ -92,9 +95,11 @@ int orc_hull_support_ex(const orc_model* om, int g, const double l[3], int use_g
   const int32_t* adr = om->hull_adr + m->geom_hulladr[g];
   int cur = 0;
   double cd = l[0] * v[0] + l[1] * v[1] + l[2] * v[2];
+  g_cflops += 5;
   for (int guard = 0; guard < nvert; guard++) {
     int nxt = cur;
     double nd = cd;
+    g_cflops += 5.0 * (adr[cur + 1] - adr[cur]);
     for (int a = adr[cur]; a < adr[cur + 1]; a++) {
       int u = om->hull_adj[a];
       double s = l[0] * v[3 * u] + l[1] * v[3 * u + 1] + l[2] * v[3 * u + 2];
@@ -157,6 +162,7 @@ typedef struct {
 
 static void msupport(const mpair* P, const double dir[3], msup* s) {
   double nd[3] = {-dir[0], -dir[1], -dir[2]};
+  g_cflops += 2 * 36.0 + 3 + 40; /* two frame transforms, difference, portal bookkeeping */
   support(P->om, P->d, P->g1, dir, s->v1);
   support(P->om, P->d, P->g2, nd, s->v2);
   sub3(s->v, s->v1, s->v2);
@@ -633,12 +639,17 @@ int orc_collide_pair(const orc_model* om, const orc_data* d, int g1, int g2, orc
       if (fabs(r[k]) > e1 + e2 + mg) return 0;
     }
   }
+  g_cflops += 60; /* midphase sphere + AABB */
   if (t1 == SIM_GEOM_PLANE) {
+    g_cflops += 150;
     if (t2 == SIM_GEOM_BOX) return plane_box(om, d, g1, g2, out, maxout);
     if (t2 == SIM_GEOM_MESH) return plane_convex(om, d, g1, g2, out);
     return 0;
   }
-  if (t1 == SIM_GEOM_BOX && t2 == SIM_GEOM_BOX) return box_box(om, d, g1, g2, out, maxout);
+  if (t1 == SIM_GEOM_BOX && t2 == SIM_GEOM_BOX) {
+    g_cflops += 700; /* 15-axis SAT + face clipping */
+    return box_box(om, d, g1, g2, out, maxout);
+  }
   mpair P = {om, d, g1, g2};
   double depth, dir[3], pos[3];
   if (!mpr_penetration(&P, &depth, dir, pos)) return 0;
@@ -652,6 +663,7 @@ int orc_collide_pair(const orc_model* om, const orc_data* d, int g1, int g2, orc
 void orc_collision(const orc_model* om, orc_data* d) {
   const sim_model_desc* m = om->m;
   d->ncon = 0;
+  g_cflops = 0;
   for (int p = 0; p < m->npair; p++) {
     int g1 = m->pair_geom1[p], g2 = m->pair_geom2[p];
     orc_contact tmp[8];
@@ -677,8 +689,9 @@ void orc_collision(const orc_model* om, orc_data* d) {
       }
       c->mu = c->friction[0];
     }
-    d->flops += 40;
   }
+  d->flops += g_cflops;
+  d->cflops += g_cflops;
 }
 
 int orc_collide_geoms(const sim_model_desc* m, const float* hv, const int32_t* hadr,

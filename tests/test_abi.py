@@ -1,0 +1,69 @@
+"""C-ABI boundary: the HIP library loads and exports exactly what include/soarm_sim.h declares.
+
+No compute calls here (no GPU in the CPU suite)."""
+import ctypes as C
+import os
+import re
+
+from lerobot_mujoco_sim2real_amd import abi, build
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, "include", "soarm_sim.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(sim_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_header_matches_python_exports():
+    assert header_functions() == sorted(abi.EXPORTS)
+
+
+def test_library_loads_and_exports_everything():
+    build.build()
+    lib = abi.load_lib()
+    for name in header_functions():
+        assert hasattr(lib, name), name
+    assert lib.sim_version().decode().startswith("soarm_sim")
+
+
+def test_no_device_fails_loudly():
+    """Without a GPU, batch creation returns an error code (never a CPU fallback)."""
+    import torch
+    if torch.cuda.is_available():
+        return
+    import soarm_pkg  # noqa: F401
+    from lerobot_mujoco_sim2real_amd import mjcf
+    cm = mjcf.compile_mjcf(mjcf.SCENE_XML)
+    lib = abi.load_lib()
+    import numpy as np
+    hv = np.ascontiguousarray(cm.hull_vert)
+    ha = np.ascontiguousarray(cm.hull_adr)
+    hj = np.ascontiguousarray(cm.hull_adj)
+    model = C.c_void_p()
+    assert lib.sim_model_create(C.byref(cm.desc), hv.ctypes.data_as(C.c_void_p), ha.ctypes.data_as(C.c_void_p),
+                                hj.ctypes.data_as(C.c_void_p), C.byref(model)) == 0
+    batch = C.c_void_p()
+    rc = lib.sim_batch_create(model, 4, 0, C.byref(batch))
+    assert rc == -4 and b"no HIP device" in lib.sim_last_error()
+    lib.sim_model_free(model)
+
+
+def test_model_validation_rejects_unsupported():
+    import soarm_pkg  # noqa: F401
+    from lerobot_mujoco_sim2real_amd import mjcf
+    cm = mjcf.compile_mjcf(mjcf.SCENE_XML)
+    cm.desc.geom_condim[0] = 6
+    lib = abi.load_lib()
+    model = C.c_void_p()
+    rc = lib.sim_model_create(C.byref(cm.desc), None, None, None, C.byref(model))
+    assert rc == -2 and b"condim" in lib.sim_last_error()
+
+
+def test_philox_mirror_known_answer():
+    """Philox4x32-10 known-answer vector (Random123 kat_vectors: ctr=0, key=0)."""
+    import numpy as np
+    from lerobot_mujoco_sim2real_amd.sim import philox4x32
+    out = philox4x32(np.zeros((1, 4), np.uint32), (0, 0))[0]
+    assert [hex(x) for x in out] == ["0x6627e8d5", "0xe169c58d", "0xbc57ac4c", "0x9b00dbd8"]

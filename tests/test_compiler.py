@@ -1,0 +1,97 @@
+"""MJCF compiler: the model facts of SURVEY.md §8 and the survey's FK anchors."""
+import numpy as np
+
+from lerobot_mujoco_sim2real_amd import abi, mjcf
+
+
+def test_sizes_arm(arm_model):
+    d = arm_model.desc
+    assert (d.nbody, d.njnt, d.nq, d.nv, d.nu) == (8, 6, 6, 6, 6)
+    assert d.ngeom == 15                # 13 collision hulls + floor + table
+    assert d.npair == 71                # 45 self + 26 arm x {table, floor}
+    assert d.nhullvert == 28592
+    assert arm_model.body_names[1:] == ["base", "shoulder", "upper_arm", "lower_arm", "wrist", "gripper",
+                                        "moving_jaw_so101_v1"]
+
+
+def test_sizes_cube(cube_model):
+    d = cube_model.desc
+    assert (d.nbody, d.nq, d.nv) == (9, 13, 12)
+    assert d.npair == 86                # +15: cube x 13 arm geoms, table, floor
+    assert d.jnt_type[6] == abi.JNT_FREE
+    assert abs(d.body_mass[8] - 0.03) < 1e-12
+    np.testing.assert_allclose(d.body_inertia[8][:], [4.5e-6] * 3, rtol=1e-9)
+
+
+def test_joint_and_actuator_defaults(arm_model):
+    d = arm_model.desc
+    # class sts3215 (so101_new_calib_v.xml:22) and velocity actuators (:160-165)
+    for i in range(6):
+        assert d.dof_damping[i] == 0.60 and d.dof_frictionloss[i] == 0.052 and d.dof_armature[i] == 0.028
+        assert d.jnt_limited[i] == 1
+        assert d.actuator_gainprm[i] == 50.0 and list(d.actuator_biasprm[i]) == [0, 0, -50.0]
+        assert d.actuator_ctrllimited[i] and d.actuator_forcelimited[i]
+        assert list(d.actuator_forcerange[i]) == [-3.5, 3.5] and list(d.actuator_ctrlrange[i]) == [-2, 2]
+    np.testing.assert_allclose(d.jnt_range[2][:], [-1.69, 1.69])
+    assert abs(d.timestep - 0.002) < 1e-15 and list(d.gravity) == [0, 0, -9.81]
+
+
+def test_kv_switch():
+    cm = mjcf.compile_mjcf(mjcf.SCENE_XML, kv=1.0)
+    assert cm.desc.actuator_gainprm[0] == 1.0 and cm.desc.actuator_biasprm[0][2] == -1.0
+
+
+def test_fk_anchors(arm_model):
+    """q=0 EE ~ (0.391, 0, 0.227); home EE ~ (0.224, 0.008, 0.051)."""
+    kin = mjcf.NumpyKinematics(arm_model).forward_position(np.zeros(6))
+    ee = kin.site_xpos(arm_model.desc.obs_site)
+    np.testing.assert_allclose(ee, [0.391, 0.0, 0.227], atol=1e-3)
+    q = arm_model.keyframes["home"]["qpos"]
+    ee = mjcf.NumpyKinematics(arm_model).forward_position(q).site_xpos(arm_model.desc.obs_site)
+    np.testing.assert_allclose(ee, [0.224, 0.008, 0.051], atol=1e-3)
+
+
+def test_lowest_point_q0(arm_model):
+    """Lowest arm hull point at q=0 is z ~ 0.016 (SURVEY.md §8 model facts)."""
+    d = arm_model.desc
+    kin = mjcf.NumpyKinematics(arm_model).forward_position(np.zeros(6))
+    zmin = 1.0
+    for g in range(d.ngeom):
+        if d.geom_type[g] != abi.GEOM_MESH:
+            continue
+        p, R = kin.geom_pose(g)
+        v = arm_model.hull_vert[d.geom_hulladr[g]: d.geom_hulladr[g] + d.geom_hullnum[g]]
+        zmin = min(zmin, (p + v.astype(np.float64) @ R.T)[:, 2].min())
+    assert abs(zmin - 0.0162) < 1e-3
+
+
+def test_pair_order_deterministic(arm_model):
+    d = arm_model.desc
+    prs = [(d.geom_bodyid[d.pair_geom1[k]], d.geom_bodyid[d.pair_geom2[k]]) for k in range(d.npair)]
+    key = [tuple(sorted(p)) for p in prs]
+    assert key == sorted(key)
+    for k in range(d.npair):  # collision table is upper-triangular in geom type
+        assert d.geom_type[d.pair_geom1[k]] <= d.geom_type[d.pair_geom2[k]]
+    # no parent/child or same-body pairs
+    for b1, b2 in prs:
+        assert b1 != b2 and d.body_parentid[max(b1, b2)] != min(b1, b2) or min(b1, b2) == 0
+
+
+def test_invweight0_positive(arm_model):
+    d = arm_model.desc
+    assert all(d.dof_invweight0[i] > 0 for i in range(6))
+    assert d.body_invweight0[1][0] == 0          # welded base
+    assert all(d.body_invweight0[b][0] > 0 for b in range(2, 8))
+
+
+def test_hull_graph_consistency(arm_model):
+    cm = arm_model
+    d = cm.desc
+    for g in range(d.ngeom):
+        if d.geom_type[g] != abi.GEOM_MESH:
+            continue
+        a0, n = d.geom_hulladr[g], d.geom_hullnum[g]
+        adr = cm.hull_adr[a0: a0 + n + 1]
+        nb = cm.hull_adj[adr[0]: adr[-1]]
+        assert nb.min() >= 0 and nb.max() < n
+        assert np.all(np.diff(adr) >= 3)  # every hull vertex has >= 3 neighbours

@@ -1,0 +1,301 @@
+"""HIP path vs the float64 oracle (tests marked gpu run on the MI355X box).
+
+Tolerances (fp32 kernel vs fp64 oracle):
+* reset / kinematics / contacts / one substep: absolute, stated per test;
+* whole trajectories: the SO-ARM101 velocity servo (kv = 50, force clamp
+  3.5 N m, h kv / M ~ 3) chatters chaotically, so two fp64 runs that start
+  1e-7 apart separate just like fp32 vs fp64 does.  Trajectory parity is
+  therefore a shadowing bound: the GPU-vs-oracle divergence must stay within
+  a small factor of the oracle-vs-perturbed-oracle divergence.
+"""
+import numpy as np
+import pytest
+
+from conftest import cube_qpos
+from oracle import Oracle
+
+pytestmark = pytest.mark.gpu
+
+RNG = np.random.default_rng(7)
+
+
+def make_sim(cm, n):
+    from lerobot_mujoco_sim2real_amd.sim import BatchSim
+    return BatchSim(cm, n)
+
+
+def to_np(t):
+    return t.detach().cpu().numpy().astype(np.float64)
+
+
+def load_state(S, st):
+    import torch
+    dev = S.device
+    S.qpos.copy_(torch.as_tensor(st["qpos"].T, dtype=torch.float32, device=dev))
+    S.qvel.copy_(torch.as_tensor(st["qvel"].T, dtype=torch.float32, device=dev))
+    S.qacc_warmstart.copy_(torch.as_tensor(st["warm"].T, dtype=torch.float32, device=dev))
+    S.ctrl.copy_(torch.as_tensor(st["ctrl"].T, dtype=torch.float32, device=dev))
+    S.status.zero_()
+
+
+def f32(st):
+    """Round an oracle state to float32 so both sides start bit-identical."""
+    return {k: (v.astype(np.float32).astype(np.float64) if v.dtype == np.float64 else v) for k, v in st.items()}
+
+
+def random_states(cm, orc, n, steps=3, lo=-1.0, hi=1.0):
+    """Mid-trajectory states (qvel, warm start and ctrl populated) from the oracle."""
+    st = orc.new_state(n)
+    orc.reset(st, init_qpos=RNG.uniform(lo, hi, (n, 5)))
+    for _ in range(steps):
+        orc.step(st, RNG.uniform(-0.5, 0.5, (n, 5)))
+    return f32(st)
+
+
+def test_reset_obs(gpu_lib, arm_model, cube_model):
+    for cm in (arm_model, cube_model):
+        n = 512
+        S, orc = make_sim(cm, n), Oracle(cm)
+        iq = RNG.uniform(-1.5, 1.5, (n, 5)).astype(np.float32)
+        ex = cube_qpos(cm, n, RNG).astype(np.float32) if cm.nq > 6 else None
+        og = to_np(S.reset(init_qpos=iq, extra_qpos=ex))
+        st = orc.new_state(n)
+        oc = orc.reset(st, init_qpos=iq.astype(np.float64), extra_qpos=ex)
+        np.testing.assert_allclose(og, oc, atol=2e-6)
+        np.testing.assert_allclose(to_np(S.qpos).T, st["qpos"], atol=1e-7)
+
+
+def test_reset_device_rng(gpu_lib, arm_model):
+    from lerobot_mujoco_sim2real_amd.sim import reset_qpos_draw
+    n = 1000
+    S = make_sim(arm_model, n)
+    S.reset(seed=123456789, env_offset=5000)
+    q = to_np(S.qpos)[:5].T
+    np.testing.assert_array_equal(q.astype(np.float32), reset_qpos_draw(123456789, np.arange(5000, 5000 + n)))
+    assert q.min() >= -0.3 and q.max() < 0.3
+
+
+def test_one_substep_no_contact(gpu_lib, arm_model_nocontact):
+    cm = arm_model_nocontact
+    n = 1024
+    S, orc = make_sim(cm, n), Oracle(cm)
+    st = random_states(cm, orc, n)
+    load_state(S, st)
+    S.substeps(1)
+    orc.step(st, None, nsub=1)
+    np.testing.assert_allclose(to_np(S.qpos).T, st["qpos"], atol=2e-6)
+    np.testing.assert_allclose(to_np(S.qvel).T, st["qvel"], atol=5e-4)
+    assert (to_np(S.status) == st["status"]).all()
+
+
+def test_one_env_step_obs(gpu_lib, arm_model_nocontact):
+    cm = arm_model_nocontact
+    n = 1024
+    S, orc = make_sim(cm, n), Oracle(cm)
+    st = random_states(cm, orc, n)
+    load_state(S, st)
+    a = RNG.uniform(-0.5, 0.5, (n, 5)).astype(np.float32)
+    og = to_np(S.step(a))
+    oc = orc.step(st, a.astype(np.float64))
+    err = np.abs(og - oc)
+    assert np.median(err) < 1e-6 and err.max() < 5e-4
+
+
+def _divergence(cm, n, T, perturb):
+    orc = Oracle(cm)
+    iq = RNG.uniform(-0.3, 0.3, (n, 5))
+    acts = RNG.uniform(-0.5, 0.5, (T, n, 5)).astype(np.float32).astype(np.float64)
+    a, b = orc.new_state(n), orc.new_state(n)
+    orc.reset(a, init_qpos=iq)
+    orc.reset(b, init_qpos=iq * (1 + perturb))
+    dev = []
+    for t in range(T):
+        dev.append(np.abs(orc.step(a, acts[t]) - orc.step(b, acts[t])))
+    return iq, acts, np.stack(dev)
+
+
+def test_trajectory_shadowing(gpu_lib, arm_model_nocontact):
+    """GPU fp32 vs oracle fp64 over 20 env-steps stays within 4x the oracle's own 1e-7 envelope."""
+    cm = arm_model_nocontact
+    n, T = 512, 20
+    iq, acts, envelope = _divergence(cm, n, T, 1e-7)
+    S, orc = make_sim(cm, n), Oracle(cm)
+    st = orc.new_state(n)
+    S.reset(init_qpos=iq.astype(np.float32))
+    orc.reset(st, init_qpos=iq.astype(np.float32).astype(np.float64))
+    for t in range(T):
+        e = np.abs(to_np(S.step(acts[t].astype(np.float32))) - orc.step(st, acts[t]))
+        env = envelope[t]
+        # floor: fp32 re-rounds the state every substep, the envelope perturbs it once
+        assert np.median(e) <= 4 * np.median(env) + 1e-5, (t, np.median(e), np.median(env))
+        assert np.quantile(e, 0.9) <= 4 * np.quantile(env, 0.9) + 1e-4
+
+
+def _contact_poses(cm, n):
+    """Poses that drive the gripper into the table / fold the arm (self contacts)."""
+    q = np.zeros((n, 6))
+    q[:, 0] = RNG.uniform(-1.0, 1.0, n)
+    q[:, 1] = RNG.uniform(0.6, 1.6, n)
+    q[:, 2] = RNG.uniform(-0.5, 1.0, n)
+    q[:, 3] = RNG.uniform(0.3, 1.6, n)
+    q[:, 4] = RNG.uniform(-2.0, 2.0, n)
+    q[:, 5] = RNG.uniform(0.0, 1.5, n)
+    half = n // 2
+    q[half:, 1] = RNG.uniform(-1.7, -1.3, n - half)    # home-like fold: shoulder servo vs lower arm
+    q[half:, 2] = RNG.uniform(1.3, 1.69, n - half)
+    return q.astype(np.float32).astype(np.float64)
+
+
+def test_contacts_match_oracle(gpu_lib, arm_model, cube_model):
+    """Same contact pairs in the same order (bit-exact indexing); geometry within fp32 tolerance."""
+    import torch
+    for cm in (arm_model, cube_model):
+        n = 512
+        S, orc = make_sim(cm, n), Oracle(cm)
+        q = _contact_poses(cm, n)
+        full = cube_qpos(cm, n, RNG, q) if cm.nq > 6 else q
+        full = full.astype(np.float32).astype(np.float64)
+        S.qpos.copy_(torch.as_tensor(full.T, dtype=torch.float32, device=S.device))
+        out, nc = S.contacts()
+        out, nc = to_np(out), to_np(nc).astype(int)
+        pair_ids = out.astype(np.float32).view(np.int32)[..., 7]
+        d = cm.desc
+        checked = total = 0
+        for e in range(n):
+            ref = orc.forward(full[e])
+            rc = ref["contacts"]
+            if len(rc) and np.min(np.abs(rc[:, 0])) < 2e-5:
+                continue  # grazing contact: existence is decided below fp32 resolution
+            total += len(rc)
+            assert nc[e] == len(rc), (e, nc[e], len(rc))
+            for k in range(nc[e]):
+                p = pair_ids[e, k]
+                assert (d.pair_geom1[p], d.pair_geom2[p]) == (int(rc[k, 7]), int(rc[k, 8]))
+                # deep (unphysical) penetrations make MPR's answer ill-conditioned: relative bound
+                deep = abs(rc[k, 0]) > 5e-3
+                np.testing.assert_allclose(out[e, k, 0], rc[k, 0], atol=5e-5, rtol=1e-2 if deep else 0)
+                np.testing.assert_allclose(out[e, k, 1:4], rc[k, 1:4], atol=2e-2 if deep else 2e-3)
+                np.testing.assert_allclose(out[e, k, 4:7], rc[k, 4:7], atol=1e-1 if deep else 2e-2)
+            checked += 1
+        assert checked > 0.9 * n and total > n // 4
+
+
+def test_one_substep_with_contacts(gpu_lib, cube_model):
+    cm = cube_model
+    n = 512
+    S, orc = make_sim(cm, n), Oracle(cm)
+    st = orc.new_state(n)
+    ex = cube_qpos(cm, n, RNG)
+    orc.reset(st, init_qpos=RNG.uniform(-0.3, 0.3, (n, 5)), extra_qpos=ex)
+    for _ in range(5):  # settle the cube onto the table (4 resting contacts each)
+        orc.step(st, RNG.uniform(-0.5, 0.5, (n, 5)))
+    st = f32(st)
+    st["ncon"][:] = 0
+    load_state(S, st)
+    S.substeps(1)
+    orc.step(st, None, nsub=1)
+    np.testing.assert_allclose(to_np(S.qpos).T, st["qpos"], atol=5e-6)
+    np.testing.assert_allclose(to_np(S.qvel).T[:, 6:], st["qvel"][:, 6:], atol=5e-3)
+    np.testing.assert_allclose(to_np(S.qvel).T[:, :6], st["qvel"][:, :6], atol=5e-3)
+    assert to_np(S.ncon).sum() == st["ncon"].sum()
+
+
+def test_cube_rests_gpu(gpu_lib, cube_model):
+    cm = cube_model
+    n = 256
+    S = make_sim(cm, n)
+    S.reset(extra_qpos=cube_qpos(cm, n, RNG).astype(np.float32))
+    for _ in range(50):
+        S.step(np.zeros((n, 5), np.float32))
+    q = to_np(S.qpos).T
+    v = to_np(S.qvel).T
+    assert np.abs(q[:, 8] - (-0.0009 + 0.015)).max() < 2e-3   # resting height
+    assert np.abs(v[:, 6:]).max() < 1e-2
+    assert (to_np(S.ncon) > 0).all()
+
+
+def test_ik_matches_oracle(gpu_lib, arm_model):
+    from lerobot_mujoco_sim2real_amd.SOARM101.SOARM101_DataCollection import cartesian_targets
+    n = 600
+    tp = 1.6 + 0.02 * RNG.uniform(0, 300, n)
+    tgt = np.concatenate([cartesian_targets("Fig8", tp[:300]), cartesian_targets("Circle", tp[300:], idx=0)])
+    tgt = tgt.astype(np.float32)
+    S, orc = make_sim(arm_model, n), Oracle(arm_model)
+    q0 = np.zeros((n, 6), np.float32)
+    q0[:, :5] = RNG.uniform(-0.3, 0.3, (n, 5))
+    import torch
+    qg, okg, itg = S.ik(tgt, q=torch.as_tensor(q0.T.copy(), device=S.device))
+    qg, okg = to_np(qg).T, to_np(okg).astype(bool)
+    qc, okc, itc = orc.ik(tgt.astype(np.float64), q0.astype(np.float64))
+    assert okc.mean() > 0.95
+    assert (okg == okc).mean() > 0.98
+    both = okg & okc
+    np.testing.assert_allclose(qg[both][:, :5], qc[both][:, :5], atol=2e-3)
+    from lerobot_mujoco_sim2real_amd import mjcf
+    for e in np.nonzero(both)[0][:50]:
+        ee = mjcf.NumpyKinematics(arm_model).forward_position(qg[e]).site_xpos(arm_model.desc.obs_site)
+        assert np.linalg.norm(ee - tgt[e]) < 1e-5
+
+
+def test_bad_state_soft_reset(gpu_lib, arm_model_nocontact):
+    import torch
+    from lerobot_mujoco_sim2real_amd import abi
+    cm = arm_model_nocontact
+    S = make_sim(cm, 64)
+    S.reset()
+    S.qvel[2, 5] = float("nan")
+    S.qpos[1, 7] = 1e12
+    S.step(torch.zeros((64, 5), device=S.device))
+    st = to_np(S.status).astype(int)
+    assert st[5] & abi.ST_BADQVEL and st[7] & abi.ST_BADQPOS
+    assert np.isfinite(to_np(S.qpos)).all() and (st[[0, 1, 2, 3]] == 0).all()
+
+
+def test_golden_fixture_gpu(gpu_lib, arm_model_nocontact):
+    import os
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "oracle_arm_random.npz"))
+    S = make_sim(arm_model_nocontact, z["init_qpos"].shape[0])
+    obs = [to_np(S.reset(init_qpos=z["init_qpos"].astype(np.float32)))]
+    for a in z["actions"]:
+        obs.append(to_np(S.step(a.astype(np.float32))))
+    obs = np.stack(obs)
+    np.testing.assert_allclose(obs[:2], z["obs"][:2], atol=1e-4)
+    np.testing.assert_allclose(obs, z["obs"], atol=3e-2)
+
+
+def test_datacollection_layout_and_replay(gpu_lib, arm_model_nocontact):
+    """[traj, steps+1, 13] layout, row i = [u_i, s_i]; replaying the same inputs through the oracle."""
+    from lerobot_mujoco_sim2real_amd.args import Args
+    from lerobot_mujoco_sim2real_amd.SOARM101.SOARM101_DataCollection import SOARM101DataGenerator
+    gen = SOARM101DataGenerator(Args([]), model=arm_model_nocontact)
+    for kind in ("random", "sin", "chirp"):
+        d = gen.generate_physics_based_data(64, 6, kind)
+        assert d.shape == (64, 7, 13) and d.dtype == np.float64
+        assert np.abs(d[:, :, :5]).max() <= 0.5
+    n, T = 128, 3
+    iq = RNG.uniform(-0.3, 0.3, (n, 5))
+    acts = RNG.uniform(-0.5, 0.5, (T + 1, n, 5)).astype(np.float32)
+    r = to_np(gen.rollout_device(n, T, "random", init_qpos=iq, actions=acts))
+    orc = Oracle(arm_model_nocontact)
+    st = orc.new_state(n)
+    s0 = orc.reset(st, init_qpos=iq.astype(np.float32).astype(np.float64))
+    np.testing.assert_allclose(r[0, :, 5:], s0, atol=2e-6)
+    np.testing.assert_allclose(r[:, :, :5], acts, atol=0)
+    s1 = orc.step(st, acts[0].astype(np.float64))
+    np.testing.assert_allclose(r[1, :, 5:], s1, atol=5e-4)
+
+
+def test_vecenv_api(gpu_lib):
+    from lerobot_mujoco_sim2real_amd.SOARM101 import SOARM101Env, SOARM101VecEnv
+    env = SOARM101Env()
+    assert env.frame_skip == 10 and abs(env.dt - 0.02) < 1e-12 and env.joint_ids == [0, 1, 2, 3, 4]
+    obs, info = env.reset(seed=0)
+    assert obs.shape == (8,) and obs.dtype == np.float32 and info == {}
+    assert np.all(np.abs(obs[3:]) <= 0.3)
+    obs2, r, term, trunc, info = env.step(np.zeros(5, np.float32))
+    assert obs2.shape == (8,) and r == 0.0 and term is False and trunc is False
+    obs, _ = env.reset(options={"initial_state": np.r_[np.full(5, 0.1), np.zeros(5)]})
+    np.testing.assert_allclose(obs[3:], 0.1, atol=1e-7)
+    venv = SOARM101VecEnv(num_envs=32)
+    o, _ = venv.reset(seed=3)
+    assert tuple(o.shape) == (32, 8)

@@ -1,0 +1,196 @@
+"""The float64 CPU oracle pinned by analytic known answers.
+
+MuJoCo is absent and the reference may not be run, so the
+oracle's parity with mj_step is unpinned; these tests pin its physics by
+independent constructions instead.
+"""
+import numpy as np
+import pytest
+
+from lerobot_mujoco_sim2real_amd import abi, mjcf
+from conftest import cube_qpos
+from oracle import Oracle
+
+RNG = np.random.default_rng(1234)
+
+
+def _poses(n, lo=-1.0, hi=1.0):
+    q = np.zeros((n, 6))
+    q[:, :5] = RNG.uniform(lo, hi, (n, 5))
+    return q
+
+
+def test_mass_matrix_vs_jacobian_sum(arm_model_nocontact):
+    """CRBA M == sum_b (m J_p'J_p + J_r' I J_r) + armature, SPD."""
+    orc = Oracle(arm_model_nocontact)
+    for q in _poses(8):
+        M = orc.forward(q)["M"]
+        Mn = mjcf.NumpyKinematics(arm_model_nocontact).forward_position(q).mass_matrix()
+        np.testing.assert_allclose(M, Mn, atol=1e-14)
+        assert np.all(np.linalg.eigvalsh(M) > 0.028 - 1e-9)
+
+
+def test_gravity_is_potential_gradient(arm_model_nocontact):
+    cm = arm_model_nocontact
+    orc = Oracle(cm)
+
+    def V(q):
+        k = mjcf.NumpyKinematics(cm).forward_position(q)
+        return sum(cm.desc.body_mass[b] * 9.81 * k.xipos[b][2] for b in range(cm.desc.nbody))
+
+    for q in _poses(4):
+        g = np.array([(V(q + 1e-6 * e) - V(q - 1e-6 * e)) / 2e-6 for e in np.eye(6)])
+        np.testing.assert_allclose(orc.forward(q, np.zeros(6))["bias"], g, atol=1e-8)
+
+
+def test_coriolis_is_lagrangian(arm_model_nocontact):
+    """bias(q, v) - g(q) == dM/dt v - 1/2 d(v'Mv)/dq  (Euler-Lagrange)."""
+    cm = arm_model_nocontact
+    orc = Oracle(cm)
+    Mq = lambda q: mjcf.NumpyKinematics(cm).forward_position(q).mass_matrix()
+    for q in _poses(3):
+        v = RNG.normal(size=6)
+        dM = [(Mq(q + 1e-6 * e) - Mq(q - 1e-6 * e)) / 2e-6 for e in np.eye(6)]
+        cor = sum(dM[i] * v[i] for i in range(6)) @ v - 0.5 * np.array([v @ dM[i] @ v for i in range(6)])
+        b = orc.forward(q, v)["bias"] - orc.forward(q, np.zeros(6))["bias"]
+        np.testing.assert_allclose(b, cor, atol=1e-8)
+
+
+def test_passive_energy_decreases():
+    """kv = 0 (no servo): damping + frictionloss only dissipate (ctrl irrelevant)."""
+    cm = mjcf.compile_mjcf(mjcf.SCENE_XML, kv=0.0, disable_contact=True)
+    orc = Oracle(cm)
+    n = 8
+    st = orc.new_state(n)
+    orc.reset(st, init_qpos=RNG.uniform(-0.5, 0.5, (n, 5)), init_qvel=RNG.uniform(-2, 2, (n, 5)))
+
+    def energy(i):
+        q, v = st["qpos"][i], st["qvel"][i]
+        k = mjcf.NumpyKinematics(cm).forward_position(q)
+        V = sum(cm.desc.body_mass[b] * 9.81 * k.xipos[b][2] for b in range(cm.desc.nbody))
+        return 0.5 * v @ k.mass_matrix() @ v + V
+
+    E0 = np.array([energy(i) for i in range(n)])
+    for _ in range(5):
+        orc.step(st, None, nsub=10)
+        E1 = np.array([energy(i) for i in range(n)])
+        assert np.all(E1 < E0 + 1e-6)
+        E0 = E1
+
+
+def test_frictionloss_rows_bounded(arm_model_nocontact):
+    orc = Oracle(arm_model_nocontact)
+    for q in _poses(6):
+        out = orc.forward(q, RNG.normal(size=6), ctrl=RNG.uniform(-2, 2, 6))
+        f = out["efc_force"][:6]
+        assert np.all(np.abs(f) <= 0.052 + 1e-12)
+
+
+def test_stiction_holds_small_torque():
+    """Zero gravity, kv = 0, at rest: a 0.03 N m applied-by-bias torque is below
+    frictionloss 0.052 -> the soft friction row cancels most of it."""
+    cm = mjcf.compile_mjcf(mjcf.SCENE_XML, kv=0.0, disable_contact=True)
+    cm.desc.gravity[:] = [0, 0, 0]
+    for a in range(6):  # motor-like: force = gain * ctrl
+        cm.desc.actuator_gainprm[a] = 1.0
+        cm.desc.actuator_biasprm[a][:] = [0, 0, 0]
+    orc = Oracle(cm)
+    q = np.zeros(6)
+    free = orc.forward(q, np.zeros(6), ctrl=np.r_[0, 0, 0, 0, 0.03, 0])
+    cm.desc.dof_frictionloss[4] = 0.0
+    nofric = Oracle(cm).forward(q, np.zeros(6), ctrl=np.r_[0, 0, 0, 0, 0.03, 0])
+    cm.desc.dof_frictionloss[4] = 0.052
+    assert abs(free["qacc"][4]) < 0.15 * abs(nofric["qacc"][4])
+    assert abs(free["efc_force"][4]) < 0.052  # not saturated
+
+
+def test_hill_climb_equals_brute_force(arm_model):
+    orc = Oracle(arm_model)
+    d = arm_model.desc
+    dirs = RNG.normal(size=(400, 3))
+    for g in range(d.ngeom):
+        if d.geom_type[g] != abi.GEOM_MESH:
+            continue
+        a = orc.hull_support(g, dirs, True)
+        b = orc.hull_support(g, dirs, False)
+        v = arm_model.hull_vert[d.geom_hulladr[g]: d.geom_hulladr[g] + d.geom_hullnum[g]].astype(np.float64)
+        np.testing.assert_allclose((v[a] * dirs).sum(1), (v[b] * dirs).sum(1), atol=1e-12)
+
+
+def test_cube_rests_on_table(cube_model):
+    """Cube settles on the table: 4 box-box contacts, sum of normal forces = m g."""
+    cm = cube_model
+    orc = Oracle(cm)
+    n = 1
+    st = orc.new_state(n)
+    ex = cube_qpos(cm, n, np.random.default_rng(0))
+    orc.reset(st, extra_qpos=ex)
+    for _ in range(30):
+        orc.step(st, np.zeros((n, 5)))
+    out = orc.forward(st["qpos"][0], st["qvel"][0], st["ctrl"][0], st["warm"][0])
+    cube_g = cm.geom("cube")
+    con = [c for c in out["contacts"] if int(c[8]) == cube_g or int(c[7]) == cube_g]
+    assert len(con) == 4
+    for c in con:
+        np.testing.assert_allclose(c[4:7], [0, 0, 1], atol=1e-6)
+        assert -2e-3 < c[0] < 0
+    nf = len(out["efc_force"]) - 4 * out["ncon"]
+    fn = out["efc_force"][nf:].sum()  # every pyramid edge carries its force along the normal
+    assert abs(fn - 0.03 * 9.81) < 0.02 * 0.03 * 9.81
+    assert np.abs(st["qvel"][0][6:]).max() < 1e-3
+
+
+def test_table_penetration_depth(arm_model):
+    """Gripper pushed into the table: MPR depth == table top - lowest hull point, normal +z."""
+    cm = arm_model
+    orc = Oracle(cm)
+    d = cm.desc
+    table = cm.geom("table")
+    # fold the arm down until a gripper hull dips into the table top (z = -0.0009)
+    q = np.array([0.0, 1.2, 0.2, 1.2, 0.0, 0.0])
+    kin = mjcf.NumpyKinematics(cm).forward_position(q)
+    found = 0
+    for k in range(d.npair):
+        if d.pair_geom1[k] != table:
+            continue
+        g = d.pair_geom2[k]
+        p, R = kin.geom_pose(g)
+        v = cm.hull_vert[d.geom_hulladr[g]: d.geom_hulladr[g] + d.geom_hullnum[g]].astype(np.float64)
+        zmin = (p + v @ R.T)[:, 2].min()
+        depth = -0.0009 - zmin
+        con = orc.collide(q, table, g)
+        if depth > 1e-4:
+            assert len(con) == 1
+            found += 1
+            np.testing.assert_allclose(-con[0][0], depth, rtol=2e-2, atol=1e-5)
+            np.testing.assert_allclose(con[0][4:7], [0, 0, 1], atol=3e-2)
+        elif depth < -1e-4:
+            assert len(con) == 0
+    assert found >= 1
+
+
+def test_ik_converges_on_fig8(arm_model):
+    from lerobot_mujoco_sim2real_amd.SOARM101.SOARM101_DataCollection import cartesian_targets
+    orc = Oracle(arm_model)
+    tp = 1.6 + 0.02 * np.linspace(0, 300, 300)
+    xyz = cartesian_targets("Fig8", tp)
+    q = np.zeros(6)
+    for p in xyz[:40]:
+        qn, ok, it = orc.ik(p[None], q[None])
+        assert ok[0]
+        q = qn[0]
+        kin = mjcf.NumpyKinematics(arm_model).forward_position(q)
+        assert np.linalg.norm(kin.site_xpos(arm_model.desc.obs_site) - p) < 1e-6
+
+
+def test_golden_regression(arm_model_nocontact):
+    """Committed fixtures (tests/golden/make_golden.py) — the oracle must keep reproducing them."""
+    import os
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "oracle_arm_random.npz"))
+    orc = Oracle(arm_model_nocontact)
+    n = z["init_qpos"].shape[0]
+    st = orc.new_state(n)
+    obs = [orc.reset(st, init_qpos=z["init_qpos"])]
+    for a in z["actions"]:
+        obs.append(orc.step(st, a))
+    np.testing.assert_allclose(np.stack(obs), z["obs"], atol=1e-9)

@@ -1,0 +1,69 @@
+"""Freeze the algorithmic cost per env-step (SURVEY.md §8d binding procedure).
+
+Runs the instrumented float64 oracle on a sample of each bench workload and
+writes profiles/algorithmic_cost.json: flops per env-step (total, collision
+share, dynamics share) and the algorithmic HBM bytes per env-step.  bench.py
+computes every roofline fraction from this frozen file.
+"""
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import soarm_pkg  # noqa: E402,F401
+from lerobot_mujoco_sim2real_amd import workloads as W  # noqa: E402
+from oracle import Oracle  # noqa: E402
+
+N, T = 256, 60  # envs x env-steps sampled per workload
+
+
+def state_bytes(cm, dr):
+    # read qpos, qvel, warmstart, ctrl(nu) + action(5); write qpos, qvel, warmstart, ctrl, obs(8); fp32
+    b = 4 * (2 * cm.nq + 4 * cm.nv + 2 * cm.nu + 5 + 8 + 1)
+    return b + (4 * 3 if dr else 0)
+
+
+def main():
+    out = {}
+    for name, c in W.CONFIGS.items():
+        cm = W.model(name)
+        orc = Oracle(cm)
+        ids = np.arange(N)
+        st = orc.new_state(N)
+        q = W.initial_qpos(cm, ids)
+        orc.reset(st, init_qpos=q[:, :5], extra_qpos=q)
+        tab = W.chirp_tables(ids)
+        prm = None
+        if c["dr"]:
+            p = W.dr_params(ids)
+            prm = np.stack([p["mass_scale"], p["friction"], p["damping_scale"]], 1).astype(np.float64)
+        rng = np.random.default_rng(0)
+        tot = col = 0.0
+        for t in range(T):
+            a = W.chirp_action(tab, t) if c["action"] == "chirp" else rng.uniform(-0.5, 0.5, (N, 5))
+            orc.step(st, a, params=prm, nthreads=8)
+            tot += orc.last_flops
+            col += orc.last_collision_flops
+        fs = 10
+        out[name] = dict(
+            flops_per_env_step=tot / (N * T),
+            collision_flops_per_env_step=col / (N * T),
+            dynamics_flops_per_env_step=(tot - col) / (N * T),
+            flops_per_env_substep_collision=col / (N * T * fs),
+            flops_per_env_substep_dynamics=(tot - col) / (N * T * fs),
+            contacts_per_env_substep=float(st["ncon"].sum() / (N * T * fs)),
+            hbm_bytes_per_env_step=state_bytes(cm, c["dr"]),
+            sample=f"{N} envs x {T} env-steps, oracle float64, seed 0",
+        )
+        print(name, json.dumps(out[name]))
+    path = os.path.join(ROOT, "profiles", "algorithmic_cost.json")
+    json.dump(out, open(path, "w"), indent=1)
+    print("wrote", path)
+
+
+if __name__ == "__main__":
+    main()
