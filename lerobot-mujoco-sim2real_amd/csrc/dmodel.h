@@ -63,6 +63,18 @@ struct DModel {
   const float4* hull_vert;  // xyz, w unused
   const int32_t* hull_adr;  // CSR offsets per global vertex (+1)
   const int32_t* hull_adj;  // local neighbour ids
+  const int32_t* hull_seed; // per mesh geom: HULL_NSEED local start vertices for hill climbing
 };
+
+// Hill-climbing seeds: the argmax vertex of each hull for HULL_NSEED directions
+// on a Fibonacci sphere.  Climbing starts at the best seed for the query
+// direction, so a support query walks a few edges instead of crossing the hull.
+constexpr int HULL_NSEED = 32;
+inline void fibonacci_dir(int k, double d[3]) {
+  const double z = 1.0 - (2.0 * k + 1.0) / HULL_NSEED;
+  const double r = __builtin_sqrt(1.0 - z * z);
+  const double phi = k * 2.399963229728653;  // pi * (3 - sqrt 5)
+  d[0] = r * __builtin_cos(phi), d[1] = r * __builtin_sin(phi), d[2] = z;
+}
 
 }  // namespace soarm

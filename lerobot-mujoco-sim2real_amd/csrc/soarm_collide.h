@@ -61,9 +61,18 @@ DEVI float3 hull_support(const DModel& m, int g, const float l[3]) {
   const float4* v = m.hull_vert + m.geom_hulladr[g];
   const int32_t* adr = m.hull_adr + m.geom_hulladr[g];
   const int nvert = m.geom_hullnum[g];
-  int cur = 0;
-  float4 cv = v[0];
+  // best seed (the seed vertices are shared by every lane of the wave: cache-line broadcast)
+  const int32_t* seed = m.hull_seed + g * HULL_NSEED;
+  int cur = seed[0];
+  float4 cv = v[cur];
   float cd = l[0] * cv.x + l[1] * cv.y + l[2] * cv.z;
+#pragma unroll 8
+  for (int k = 1; k < HULL_NSEED; k++) {
+    const int s = seed[k];
+    const float4 w = v[s];
+    const float d = l[0] * w.x + l[1] * w.y + l[2] * w.z;
+    if (d > cd) cd = d, cur = s;
+  }
   for (int guard = 0; guard < nvert; guard++) {
     int nxt = cur;
     float nd = cd;

@@ -95,6 +95,9 @@ struct MInv {
   }
 };
 
+// diagonal inverse mass of the (single) free body, dof i of its 6
+#define S_FD(Mi, i) ((Mi).Fd[0][(i)])
+
 template <int NA, int NF>
 DEVI float dotv(const float a[], const float b[], bool arm, bool fr) {
   constexpr int NV = NA + 6 * NF;
@@ -408,6 +411,44 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
     for (int c = 0; c < nl; c++) {
       const int fl = (int)L.at(c, F_FLAGS);
       const bool ta = fl & TOUCH_ARM, tf = fl & TOUCH_FREE;
+      if constexpr (NF == 1) {
+        // Fast path, wave-uniform: no active lane's contact c touches the arm (cube on the
+        // table).  6-dof math on the free body only, every LDS load of the record issued up
+        // front, forces read once / written once.  Same arithmetic as the general path.
+        if (__all(!ta)) {
+          float jn[6], jt1[6], jt2[6], fo[4], ar[4], ia[4], ad[4];
+#pragma unroll
+          for (int i = 0; i < 6; i++)
+            jn[i] = L.at(c, NA + i), jt1[i] = L.at(c, 12 + NA + i), jt2[i] = L.at(c, 24 + NA + i);
+#pragma unroll
+          for (int ed = 0; ed < 4; ed++)
+            fo[ed] = L.at(c, F_FRC + ed), ar[ed] = L.at(c, F_AREF + ed), ia[ed] = L.at(c, F_IARD + ed),
+            ad[ed] = L.at(c, F_ARD + ed);
+          const float mu = L.at(c, F_MU), Rp = L.at(c, F_R);
+#pragma unroll
+          for (int ed = 0; ed < 4; ed++) {
+            const float s = (ed & 1) ? -mu : mu;
+            float J6[6], W6[6];
+#pragma unroll
+            for (int i = 0; i < 6; i++) {
+              J6[i] = jn[i] + s * ((ed >> 1) ? jt2[i] : jt1[i]);
+              W6[i] = S_FD(Mi, i) * J6[i];
+            }
+            const float d0 = J6[0] * v[NA] + J6[1] * v[NA + 1] + J6[2] * v[NA + 2];
+            const float d1 = J6[3] * v[NA + 3] + J6[4] * v[NA + 4] + J6[5] * v[NA + 5];
+            const float res = (d0 + d1) - ar[ed] + Rp * fo[ed];
+            const float fnew = fmaxf(fo[ed] - res * ia[ed], 0.f);
+            const float df = fnew - fo[ed];
+#pragma unroll
+            for (int i = 0; i < 6; i++) v[NA + i] += W6[i] * df;
+            improvement -= df * res + 0.5f * ad[ed] * df * df;
+            fo[ed] = fnew;
+          }
+#pragma unroll
+          for (int ed = 0; ed < 4; ed++) L.at(c, F_FRC + ed) = fo[ed];
+          continue;
+        }
+      }
       float jn[NV], jt1[NV], jt2[NV];
 #pragma unroll
       for (int i = 0; i < NV; i++) jn[i] = jt1[i] = jt2[i] = 0.f;

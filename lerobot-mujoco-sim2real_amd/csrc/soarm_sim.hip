@@ -36,7 +36,7 @@ struct sim_model {
   sim_model_desc desc;
   DModel dm;  // host copy; hull pointers filled per batch
   std::vector<float4> hull_vert;
-  std::vector<int32_t> hull_adr, hull_adj;
+  std::vector<int32_t> hull_adr, hull_adj, hull_seed;
   int na = 0, nf = 0;
 };
 
@@ -45,7 +45,7 @@ struct sim_batch {
   int n = 0, device = 0;
   DModel* d_model = nullptr;
   float4* d_hv = nullptr;
-  int32_t *d_hadr = nullptr, *d_hadj = nullptr;
+  int32_t *d_hadr = nullptr, *d_hadj = nullptr, *d_hseed = nullptr;
   float* d_scratch = nullptr;  // contact rows, [slot][env]
   size_t scratch_floats = 0;
   float* d_gpose = nullptr;    // geom world poses [geom*12+k][env]
@@ -665,6 +665,23 @@ int sim_model_create(const sim_model_desc* desc, const float* hull_vert, const i
     M->hull_adr.assign(hull_adr, hull_adr + desc->nhullvert + 1);
     M->hull_adj.assign(hull_adj, hull_adj + desc->nhulladj);
   }
+  // hill-climbing seeds: per mesh geom, the argmax vertex for each Fibonacci direction
+  M->hull_seed.assign((size_t)std::max(desc->ngeom, 1) * HULL_NSEED, 0);
+  for (int g = 0; g < desc->ngeom; g++) {
+    if (desc->geom_type[g] != SIM_GEOM_MESH) continue;
+    const float* hv = hull_vert + 3 * (size_t)desc->geom_hulladr[g];
+    for (int k = 0; k < HULL_NSEED; k++) {
+      double d[3];
+      fibonacci_dir(k, d);
+      int best = 0;
+      double bd = -1e300;
+      for (int i = 0; i < desc->geom_hullnum[g]; i++) {
+        const double s = d[0] * hv[3 * i] + d[1] * hv[3 * i + 1] + d[2] * hv[3 * i + 2];
+        if (s > bd) bd = s, best = i;
+      }
+      M->hull_seed[(size_t)g * HULL_NSEED + k] = best;
+    }
+  }
   *out = M;
   return SIM_OK;
 }
@@ -693,6 +710,9 @@ int sim_batch_create(const sim_model* m, int n_envs, int device, sim_batch** out
   dm.hull_vert = B->d_hv;
   dm.hull_adr = B->d_hadr;
   dm.hull_adj = B->d_hadj;
+  HIPCHECK(hipMalloc(&B->d_hseed, m->hull_seed.size() * sizeof(int32_t)));
+  HIPCHECK(hipMemcpy(B->d_hseed, m->hull_seed.data(), m->hull_seed.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  dm.hull_seed = B->d_hseed;
   HIPCHECK(hipMalloc(&B->d_model, sizeof(DModel)));
   HIPCHECK(hipMemcpy(B->d_model, &dm, sizeof(DModel), hipMemcpyHostToDevice));
   if (!m->desc.disable_contact) {
@@ -714,6 +734,7 @@ void sim_batch_free(sim_batch* b) {
   (void)hipFree(b->d_hv);
   (void)hipFree(b->d_hadr);
   (void)hipFree(b->d_hadj);
+  (void)hipFree(b->d_hseed);
   (void)hipFree(b->d_scratch);
   (void)hipFree(b->d_gpose);
   (void)hipFree(b->d_cbuf);

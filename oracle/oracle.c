@@ -796,6 +796,7 @@ static void make_om(orc_model* om, const sim_model_desc* m, const float* hv, con
   om->hull_vert = hv;
   om->hull_adr = hadr;
   om->hull_adj = hadj;
+  om->hull_seed = NULL; /* callers with hulls set the seeds they computed once per call */
   om->mass_scale = params ? params[0] : 1.0;
   om->friction = params ? params[1] : -1.0;
   om->damping_scale = params ? params[2] : 1.0;
@@ -849,6 +850,8 @@ void orc_batch_step(const sim_model_desc* m, const float* hv, const int32_t* had
                     double* ctrl, const double* action, int nsub, double* obs, int32_t* status,
                     double* ncon_sum, const double* params, int nthreads, double* flops) {
   double fl_total = 0, cf_total = 0;
+  int32_t seeds[SIM_MAXGEOM * ORC_NSEED];
+  if (hv) orc_hull_seeds(m, hv, seeds);
 #ifdef _OPENMP
   if (nthreads <= 0) nthreads = omp_get_max_threads();
 #pragma omp parallel for num_threads(nthreads) schedule(dynamic, 1) reduction(+ : fl_total, cf_total)
@@ -856,6 +859,7 @@ void orc_batch_step(const sim_model_desc* m, const float* hv, const int32_t* had
   for (int e = 0; e < n; e++) {
     orc_model om;
     make_om(&om, m, hv, hadr, hadj, params ? params + 3 * e : NULL);
+    om.hull_seed = hv ? seeds : NULL;
     orc_data d;
     memset(&d, 0, sizeof(d));
     for (int i = 0; i < m->nq; i++) d.qpos[i] = qpos[e * m->nq + i];
@@ -896,8 +900,11 @@ int orc_debug_forward(const sim_model_desc* m, const float* hv, const int32_t* h
                       const double* ctrl, const double* warm, double* M, double* bias,
                       double* qacc, double* contacts, double* site_xpos, double* geom_xpos,
                       double* efc_force, int* nefc) {
+  int32_t seeds[SIM_MAXGEOM * ORC_NSEED];
+  if (hv) orc_hull_seeds(m, hv, seeds);
   orc_model om;
   make_om(&om, m, hv, hadr, hadj, NULL);
+  om.hull_seed = hv ? seeds : NULL;
   orc_data d;
   orc_reset_data(&om, &d);
   for (int i = 0; i < m->nq; i++) d.qpos[i] = qpos[i];

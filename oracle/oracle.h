@@ -24,12 +24,14 @@
 #include "../include/soarm_sim.h"
 
 #define ORC_MAXEFC (2 * SIM_MAXDOF + 4 * SIM_MAXCON)
+#define ORC_NSEED 32 /* hill-climbing seeds per hull: argmax vertex of 32 Fibonacci directions */
 
 typedef struct orc_model {
   const sim_model_desc* m;
   const float* hull_vert;
   const int32_t* hull_adr;
   const int32_t* hull_adj;
+  const int32_t* hull_seed; /* [ngeom][ORC_NSEED] hill-climb start candidates, or NULL */
   /* per-env domain randomisation (1,0/neg,1 = nominal) */
   double mass_scale;
   double friction; /* <0: use geom_friction */
@@ -105,6 +107,7 @@ void orc_jac(const orc_model* om, const orc_data* d, const double p[3], int body
              double* jacr);
 
 /* collision primitives (oracle_collision.c) */
+void orc_hull_seeds(const sim_model_desc* m, const float* hv, int32_t* seeds /*[ngeom][ORC_NSEED]*/);
 int orc_hull_support(const orc_model* om, int g, const double l[3]);
 int orc_hull_support_ex(const orc_model* om, int g, const double l[3], int use_graph);
 int orc_hull_support_flat(const sim_model_desc* m, const float* hv, const int32_t* hadr,

@@ -96,6 +96,20 @@ int orc_hull_support_ex(const orc_model* om, int g, const double l[3], int use_g
   int cur = 0;
   double cd = l[0] * v[0] + l[1] * v[1] + l[2] * v[2];
   g_cflops += 5;
+  if (om->hull_seed) { /* start from the best seed (the same exact argmax is reached) */
+    const int32_t* sd = om->hull_seed + g * ORC_NSEED;
+    cur = sd[0];
+    cd = l[0] * v[3 * cur] + l[1] * v[3 * cur + 1] + l[2] * v[3 * cur + 2];
+    for (int k = 1; k < ORC_NSEED; k++) {
+      int s = sd[k];
+      double t = l[0] * v[3 * s] + l[1] * v[3 * s + 1] + l[2] * v[3 * s + 2];
+      if (t > cd) {
+        cd = t;
+        cur = s;
+      }
+    }
+    g_cflops += 5.0 * ORC_NSEED;
+  }
   for (int guard = 0; guard < nvert; guard++) {
     int nxt = cur;
     double nd = cd;
@@ -116,6 +130,29 @@ int orc_hull_support_ex(const orc_model* om, int g, const double l[3], int use_g
 }
 int orc_hull_support(const orc_model* om, int g, const double l[3]) {
   return orc_hull_support_ex(om, g, l, 1);
+}
+
+/* seeds: for each of ORC_NSEED Fibonacci-sphere directions the brute-force
+   argmax hull vertex (ties -> lowest index) */
+void orc_hull_seeds(const sim_model_desc* m, const float* hv, int32_t* seeds) {
+  for (int g = 0; g < m->ngeom; g++) {
+    for (int k = 0; k < ORC_NSEED; k++) seeds[g * ORC_NSEED + k] = 0;
+    if (m->geom_type[g] != SIM_GEOM_MESH) continue;
+    const float* v = hv + 3 * (size_t)m->geom_hulladr[g];
+    for (int k = 0; k < ORC_NSEED; k++) {
+      double z = 1.0 - (2.0 * k + 1.0) / ORC_NSEED, r = sqrt(1.0 - z * z), ph = k * 2.399963229728653;
+      double d[3] = {r * cos(ph), r * sin(ph), z}, bd = -1e300;
+      int best = 0;
+      for (int i = 0; i < m->geom_hullnum[g]; i++) {
+        double s = d[0] * v[3 * i] + d[1] * v[3 * i + 1] + d[2] * v[3 * i + 2];
+        if (s > bd) {
+          bd = s;
+          best = i;
+        }
+      }
+      seeds[g * ORC_NSEED + k] = best;
+    }
+  }
 }
 
 /* world-frame support point of geom g in direction dir */
@@ -697,7 +734,9 @@ void orc_collision(const orc_model* om, orc_data* d) {
 int orc_collide_geoms(const sim_model_desc* m, const float* hv, const int32_t* hadr,
                       const int32_t* hadj, const double* qpos, int g1, int g2, double* out,
                       int maxout) {
-  orc_model om = {m, hv, hadr, hadj, 1.0, -1.0, 1.0};
+  int32_t seeds[SIM_MAXGEOM * ORC_NSEED];
+  if (hv) orc_hull_seeds(m, hv, seeds);
+  orc_model om = {m, hv, hadr, hadj, hv ? seeds : NULL, 1.0, -1.0, 1.0};
   static __thread orc_data d;
   orc_reset_data(&om, &d);
   for (int i = 0; i < m->nq; i++) d.qpos[i] = qpos[i];
@@ -715,7 +754,9 @@ int orc_collide_geoms(const sim_model_desc* m, const float* hv, const int32_t* h
 int orc_hull_support_flat(const sim_model_desc* m, const float* hv, const int32_t* hadr,
                           const int32_t* hadj, int g, const double* dirs, int n, int use_graph,
                           int32_t* out) {
-  orc_model om = {m, hv, hadr, hadj, 1.0, -1.0, 1.0};
+  int32_t seeds[SIM_MAXGEOM * ORC_NSEED];
+  if (hv) orc_hull_seeds(m, hv, seeds);
+  orc_model om = {m, hv, hadr, hadj, hv ? seeds : NULL, 1.0, -1.0, 1.0};
   for (int i = 0; i < n; i++) out[i] = orc_hull_support_ex(&om, g, dirs + 3 * i, use_graph);
   return 0;
 }
