@@ -15,6 +15,7 @@ pass (before that substep's position update) while ``qpos`` is the new one.
 :class:`SOARM101VecEnv` is the batched form of the same API: actions ``[n, 5]``,
 observations ``[n, 8]`` (torch tensors on the GPU, or numpy on request).
 """
+import os
 from typing import Dict, Optional, Tuple
 
 import numpy as np
@@ -46,15 +47,21 @@ class SOARM101VecEnv:
                  device: int = 0, model=None, seed: int = 0, env_offset: int = 0, **compile_kw):
         if model is None:
             from ..mjcf import SCENE_XML
-            model = compile_mjcf(xml_path or SCENE_XML, **compile_kw)
+            xml_path = xml_path or SCENE_XML
+            if not os.path.exists(xml_path):  # SOARM101_Env.py:35-36
+                raise FileNotFoundError(f"XML file not found: {xml_path}")
+            model = compile_mjcf(xml_path, **compile_kw)
         self.model = model
+        try:
+            self.ee_site_id = model.site("gripperframe")
+        except (KeyError, ValueError):  # SOARM101_Env.py:51-52
+            raise ValueError("Site 'gripperframe' not found in model") from None
+        self.joint_ids = [model.joint(n) for n in self.joint_names]
         self.sim = BatchSim(model, num_envs, device)
         self.num_envs = num_envs
         # SOARM101_Env.py:39-40
         self.frame_skip = max(1, int(np.round(dt / model.timestep)))
         self.dt = model.timestep * self.frame_skip
-        self.joint_ids = [model.joint(n) for n in self.joint_names]
-        self.ee_site_id = model.site("gripperframe")
         self.udim = 5
         self.max_speed = 0.5
         self.xdim = 8

@@ -5,6 +5,8 @@ import ctypes as C
 import os
 import re
 
+import pytest
+
 from lerobot_mujoco_sim2real_amd import abi, build
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -67,3 +69,15 @@ def test_philox_mirror_known_answer():
     from lerobot_mujoco_sim2real_amd.sim import philox4x32
     out = philox4x32(np.zeros((1, 4), np.uint32), (0, 0))[0]
     assert [hex(x) for x in out] == ["0x6627e8d5", "0xe169c58d", "0xbc57ac4c", "0x9b00dbd8"]
+
+
+def test_env_errors_match_reference():
+    """SOARM101_Env.py:35-36 (missing XML) and :51-52 (missing EE site) raise before any GPU use."""
+    from lerobot_mujoco_sim2real_amd.SOARM101.SOARM101_Env import SOARM101Env
+    from lerobot_mujoco_sim2real_amd.mjcf import compile_mjcf, SCENE_XML
+    with pytest.raises(FileNotFoundError):
+        SOARM101Env(xml_path="/nonexistent/scene.xml")
+    cm = compile_mjcf(SCENE_XML)
+    cm.site_names = [n + "_x" for n in cm.site_names]
+    with pytest.raises(ValueError):
+        SOARM101Env(model=cm)
