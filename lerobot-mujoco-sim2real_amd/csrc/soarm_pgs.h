@@ -9,14 +9,17 @@
 // the oracle's.
 //
 // Where the rows live (one lane = one env, one wave per SIMD at 4096 envs, so
-// every sweep is a latency chain and nothing may come from global memory):
-//  * fixed rows: registers; J = +-e_i, W = M^-1 J' is a column of the arm
-//    block's explicit inverse;
+// every sweep is an issue-bound chain and nothing may come from global memory):
+//  * dof-frictionloss rows: registers; J = e_i, W = M^-1 J' is a column of the
+//    arm block's explicit inverse;
+//  * joint-limit rows (rare): a compact list of active rows in LDS;
 //  * contacts 0..LDS_CON-1: LDS, [field][lane] (conflict-free), one record per
 //    contact holding the 12-dof J_n, J_t1, J_t2; the 4 pyramid edges
-//    J_n +- mu J_tk are formed on the fly and W_e = M^-1 J_e comes from the
-//    block inverses in registers; arm / free-body halves are skipped by a
-//    per-contact flag (a cube-on-table contact touches only the 6 cube dofs);
+//    J_n +- mu J_tk are formed on the fly.  A contact that touches only the
+//    free body (cube on table) is swept in its 3-D Gram form: the residuals of
+//    its 4 edges are affine in (J_n v, J_t1 v, J_t2 v), so one sweep over the
+//    contact costs three 6-dof dots, 4 scalar edge updates and one 6-dof
+//    velocity update — the same Gauss-Seidel sequence as updating v per edge;
 //  * contacts LDS_CON..SIM_MAXCON-1 (rare): per-edge J/W slab in global
 //    scratch, [row][env] SoA.
 // PGS on the resting cube's 16 redundant edges needs ~96 sweeps per substep
@@ -28,16 +31,23 @@
 namespace soarm {
 
 constexpr int LDS_CON = 8;  // contacts whose rows stay in LDS
-constexpr int CF = 56;      // LDS floats per contact record
+constexpr int CF = 67;      // LDS floats per contact record
 // record fields: [0, 3*12) J_n | J_t1 | J_t2 (12 slots each), 36..39 aref_e,
-// 40..43 ARdiag_e, 44..47 force_e, 48..51 1/ARdiag_e, 52 mu, 53 R (pyramid), 54 flags
-enum { F_AREF = 36, F_ARD = 40, F_FRC = 44, F_IARD = 48, F_MU = 52, F_R = 53, F_FLAGS = 54 };
+// 40..43 ARdiag_e / 2, 44..47 force_e, 48..51 1/ARdiag_e, 52 mu, 53 R (pyramid),
+// 54 flags, 55..66 per edge e the Gram column (J_n, J_t1, J_t2) . M^-1 J_e'
+// (cube-only contacts: the free body's diagonal M^-1)
+enum { F_AREF = 36, F_HARD = 40, F_FRC = 44, F_IARD = 48, F_MU = 52, F_R = 53, F_FLAGS = 54, F_COEF = 55 };
 enum { TOUCH_ARM = 1, TOUCH_FREE = 2 };
+// joint-limit rows (rare): compact list, one record per active limit
+constexpr int LF = 7;  // dof, sign, aref, R, ARdiag, 1/ARdiag, force
+enum { L_DOF = 0, L_SGN = 1, L_AREF = 2, L_R = 3, L_ARD = 4, L_IARD = 5, L_FRC = 6 };
 
 struct RowLds {
-  float (*a)[64];  // [LDS_CON * CF][64]
+  float (*a)[64];    // [LDS_CON * CF][64] contact records (null: contact-free kernel)
+  float (*lim)[64];  // [NA * LF][64] active joint-limit records
   int lane;
   DEVI float& at(int c, int f) const { return a[c * CF + f][lane]; }
+  DEVI float& lm(int l, int f) const { return lim[l * LF + f][lane]; }
 };
 
 template <int NA, int NF>
@@ -122,156 +132,216 @@ DEVI void edge_J(const float jn[NV], const float jt1[NV], const float jt2[NV], i
   for (int i = 0; i < NV; i++) J[i] = jn[i] + s * jt[i];
 }
 
+// Lane-varying dof index i < N without dynamic register indexing (which would put
+// the arrays in scratch): one-hot weights, then dots.
+template <int N>
+DEVI void one_hot(int i, float* oh) {
+#pragma unroll
+  for (int k = 0; k < N; k++) oh[k] = (i == k) ? 1.f : 0.f;
+}
+template <int N>
+DEVI float pick(const float* v, const float* oh) {
+  float r = 0.f;
+#pragma unroll
+  for (int k = 0; k < N; k++) r = fmaf(oh[k], v[k], r);
+  return r;
+}
+
+// v_arm += M^-1 e_i * sgf for the one-hot dof oh
+template <int NA, int NF>
+DEVI void add_arm_col(const MInv<NA, NF>& Mi, float* v, const float* oh, float sgf) {
+#pragma unroll
+  for (int k = 0; k < NA; k++) {
+    float a = 0.f;
+#pragma unroll
+    for (int j = 0; j < NA; j++) a = fmaf(oh[j], Mi.a(k, j), a);
+    v[k] = fmaf(a, sgf, v[k]);
+  }
+}
+
 // Builds every constraint row, solves the dual by PGS, sets S.qacc / S.fcon.
-// Contacts are read straight from the collide output (cbuf/ccount, pair order).
-// Returns the number of contacts used.
+// Contacts are read straight from the collide output (pair mask + cbuf, pair
+// order).  Returns the number of contacts used.
 template <int NA, int NF, bool CON>
 DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const int* __restrict__ ccount,
-                           int n, int e, const RowLds& L, const ContactRows<NA, NF>& cr) {
+                           const uint32_t* __restrict__ pmask, int n, int e, const RowLds& L,
+                           const ContactRows<NA, NF>& cr) {
   constexpr int NV = Sim<NA, NF>::NV;
   const DModel& m = *S.mp;
   S.solve_m(S.qacc_s, S.fsmooth);
   MInv<NA, NF> Mi;
   Mi.build(S);
 
-  // ---- fixed slots: [friction_i], then per joint [lower_i, upper_i]
-  float f[3 * NA], aref[3 * NA], R[3 * NA], ARd[3 * NA];
-  bool act[3 * NA];
+  // ---- dof frictionloss rows (MuJoCo row order: all of them first)
+  float ff[NA], fa[NA], fR[NA], fhD[NA], fiD[NA];
 #pragma unroll
   for (int i = 0; i < NA; i++) {
-    act[i] = m.dof_frictionloss[i] > 0.f;
-    R[i] = m.dof_fricR[i];
-    aref[i] = -m.dof_fricB[i] * S.qvel[i];
-    ARd[i] = Mi.a(i, i) + R[i];
+    fR[i] = m.dof_fricR[i];
+    fa[i] = -m.dof_fricB[i] * S.qvel[i];
+    const float ard = Mi.a(i, i) + fR[i];
+    fhD[i] = 0.5f * ard;
+    fiD[i] = 1.f / ard;
+  }
+  // ---- joint-limit rows: joint by joint, lower then upper; compact list in LDS
+  int nlim = 0;
+#pragma unroll
+  for (int i = 0; i < NA; i++) {
 #pragma unroll
     for (int side = 0; side < 2; side++) {
-      const int s = NA + 2 * i + side;
       const float dist = side == 0 ? S.qpos[i] - m.jnt_range[i][0] : m.jnt_range[i][1] - S.qpos[i];
-      act[s] = m.jnt_limited[i] && dist < m.jnt_margin[i];
-      const float imp = impedance(m.jnt_solimp[i], dist, m.jnt_margin[i]);
-      R[s] = fmaxf(MINVALF, (1.f - imp) * m.dof_invweight0[i] / imp);
-      const float vel = side == 0 ? S.qvel[i] : -S.qvel[i];
-      aref[s] = -m.jnt_KB[i][1] * vel - m.jnt_KB[i][0] * imp * (dist - m.jnt_margin[i]);
-      ARd[s] = Mi.a(i, i) + R[s];
+      if (m.jnt_limited[i] && dist < m.jnt_margin[i]) {
+        const float imp = impedance(m.jnt_solimp[i], dist, m.jnt_margin[i]);
+        const float R = fmaxf(MINVALF, (1.f - imp) * m.dof_invweight0[i] / imp);
+        const float vel = side == 0 ? S.qvel[i] : -S.qvel[i];
+        const float ard = Mi.a(i, i) + R;
+        L.lm(nlim, L_DOF) = (float)i;
+        L.lm(nlim, L_SGN) = side == 0 ? 1.f : -1.f;
+        L.lm(nlim, L_AREF) = -m.jnt_KB[i][1] * vel - m.jnt_KB[i][0] * imp * (dist - m.jnt_margin[i]);
+        L.lm(nlim, L_R) = R;
+        L.lm(nlim, L_ARD) = ard;
+        L.lm(nlim, L_IARD) = 1.f / ard;
+        nlim++;
+      }
     }
   }
-  auto slot_dof = [](int s) { return s < NA ? s : (s - NA) >> 1; };
-  auto slot_sgn = [](int s) { return (s < NA || ((s - NA) & 1) == 0) ? 1.f : -1.f; };
-  float iARd[3 * NA];
-#pragma unroll
-  for (int s = 0; s < 3 * NA; s++) iARd[s] = 1.f / ARd[s];
 
   // ---- contact rows, straight from the collide output in pair order
   int ncon = 0;
   if constexpr (CON) {
-    if (ccount != nullptr)
-    for (int p = 0; p < m.npair; p++) {
-      const int cnt = ccount[(size_t)p * n + e];
-      const int s0 = m.pair_slot[p];
-      for (int k = 0; k < cnt; k++) {
-        if (ncon >= SIM_MAXCON) {
-          S.status |= SIM_ST_CONOVERFLOW;
-          break;
-        }
-        const size_t base = (size_t)(s0 + k) * 7;
-        const float cdist = cbuf[base * n + e];
-        const float cpos[3] = {cbuf[(base + 1) * n + e], cbuf[(base + 2) * n + e], cbuf[(base + 3) * n + e]};
-        float fr[9] = {cbuf[(base + 4) * n + e], cbuf[(base + 5) * n + e], cbuf[(base + 6) * n + e], 0, 0, 0, 0, 0, 0};
-        {  // contact frame (mju_makeFrame)
-          float y[3];
-          if (fabsf(fr[1]) < 0.5f)
-            y[0] = 0, y[1] = 1, y[2] = 0;
-          else
-            y[0] = 0, y[1] = 0, y[2] = 1;
-          const float dd = dot3(fr, y);
-          y[0] -= dd * fr[0], y[1] -= dd * fr[1], y[2] -= dd * fr[2];
-          const float inv = rsqrtf(dot3(y, y));
-          fr[3] = y[0] * inv, fr[4] = y[1] * inv, fr[5] = y[2] * inv;
-          cross(fr + 6, fr, fr + 3);
-        }
-        const int b1 = m.geom_bodyid[m.pair_geom1[p]], b2 = m.geom_bodyid[m.pair_geom2[p]];
-        // relative translational Jacobian (body2 - body1) at the contact point, contact frame
-        float jd[3][NV];
-#pragma unroll
-        for (int i = 0; i < NV; i++) jd[0][i] = jd[1][i] = jd[2][i] = 0.f;
-        int flags = 0;
-#pragma unroll
-        for (int side = 0; side < 2; side++) {
-          const int b = side ? b2 : b1;
-          const float sg = side ? 1.f : -1.f;
-          if (b >= 2 && b < 2 + NA) flags |= TOUCH_ARM;
-#pragma unroll
-          for (int i = 0; i < NA; i++) {
-            if (b >= i + 2 && b < 2 + NA) {  // hinge i moves chain bodies i+2.. (reference point: origin)
-              float l[3];
-              cross(l, S.cdof[i], cpos);
-              const float jp[3] = {S.cdof[i][3] + l[0], S.cdof[i][4] + l[1], S.cdof[i][5] + l[2]};
-#pragma unroll
-              for (int q = 0; q < 3; q++) jd[q][i] += sg * dot3(fr + 3 * q, jp);
+    if (ccount != nullptr) {
+      const int nw = (m.npair + 31) >> 5;
+      for (int w = 0; w < nw; w++) {
+        uint32_t bits = pmask[(size_t)w * n + e];
+        while (bits) {
+          const int p = 32 * w + __builtin_ctz(bits);
+          bits &= bits - 1;
+          const int cnt = ccount[(size_t)p * n + e];
+          const int s0 = m.pair_slot[p];
+          for (int k = 0; k < cnt; k++) {
+            if (ncon >= SIM_MAXCON) {
+              S.status |= SIM_ST_CONOVERFLOW;
+              break;
             }
-          }
+            const size_t base = (size_t)(s0 + k) * 7;
+            const float cdist = cbuf[base * n + e];
+            const float cpos[3] = {cbuf[(base + 1) * n + e], cbuf[(base + 2) * n + e], cbuf[(base + 3) * n + e]};
+            float fr[9] = {cbuf[(base + 4) * n + e], cbuf[(base + 5) * n + e], cbuf[(base + 6) * n + e], 0, 0, 0, 0, 0, 0};
+            {  // contact frame (mju_makeFrame)
+              float y[3];
+              if (fabsf(fr[1]) < 0.5f)
+                y[0] = 0, y[1] = 1, y[2] = 0;
+              else
+                y[0] = 0, y[1] = 0, y[2] = 1;
+              const float dd = dot3(fr, y);
+              y[0] -= dd * fr[0], y[1] -= dd * fr[1], y[2] -= dd * fr[2];
+              const float inv = rsqrtf(dot3(y, y));
+              fr[3] = y[0] * inv, fr[4] = y[1] * inv, fr[5] = y[2] * inv;
+              cross(fr + 6, fr, fr + 3);
+            }
+            const int b1 = m.geom_bodyid[m.pair_geom1[p]], b2 = m.geom_bodyid[m.pair_geom2[p]];
+            // relative translational Jacobian (body2 - body1) at the contact point, contact frame
+            float jd[3][NV];
 #pragma unroll
-          for (int ff = 0; ff < NF; ff++) {
-            const int fb = 2 + NA + ff, d0 = NA + 6 * ff;
-            if (b == fb) {
-              flags |= TOUCH_FREE;
-              const float off[3] = {cpos[0] - S.xpos[fb][0], cpos[1] - S.xpos[fb][1], cpos[2] - S.xpos[fb][2]};
+            for (int i = 0; i < NV; i++) jd[0][i] = jd[1][i] = jd[2][i] = 0.f;
+            int flags = 0;
 #pragma unroll
-              for (int i = 0; i < 6; i++) {
-                float l[3];
-                cross(l, S.cdof[d0 + i], off);
-                const float jp[3] = {S.cdof[d0 + i][3] + l[0], S.cdof[d0 + i][4] + l[1], S.cdof[d0 + i][5] + l[2]};
+            for (int side = 0; side < 2; side++) {
+              const int b = side ? b2 : b1;
+              const float sg = side ? 1.f : -1.f;
+              if (b >= 2 && b < 2 + NA) flags |= TOUCH_ARM;
 #pragma unroll
-                for (int q = 0; q < 3; q++) jd[q][d0 + i] += sg * dot3(fr + 3 * q, jp);
+              for (int i = 0; i < NA; i++) {
+                if (b >= i + 2 && b < 2 + NA) {  // hinge i moves chain bodies i+2.. (reference point: origin)
+                  float l[3];
+                  cross(l, S.cdof[i], cpos);
+                  const float jp[3] = {S.cdof[i][3] + l[0], S.cdof[i][4] + l[1], S.cdof[i][5] + l[2]};
+#pragma unroll
+                  for (int q = 0; q < 3; q++) jd[q][i] += sg * dot3(fr + 3 * q, jp);
+                }
+              }
+#pragma unroll
+              for (int ff2 = 0; ff2 < NF; ff2++) {
+                const int fb = 2 + NA + ff2, d0 = NA + 6 * ff2;
+                if (b == fb) {
+                  flags |= TOUCH_FREE;
+                  const float off[3] = {cpos[0] - S.xpos[fb][0], cpos[1] - S.xpos[fb][1], cpos[2] - S.xpos[fb][2]};
+#pragma unroll
+                  for (int i = 0; i < 6; i++) {
+                    float l[3];
+                    cross(l, S.cdof[d0 + i], off);
+                    const float jp[3] = {S.cdof[d0 + i][3] + l[0], S.cdof[d0 + i][4] + l[1], S.cdof[d0 + i][5] + l[2]};
+#pragma unroll
+                    for (int q = 0; q < 3; q++) jd[q][d0 + i] += sg * dot3(fr + 3 * q, jp);
+                  }
+                }
               }
             }
-          }
-        }
-        const bool ta = flags & TOUCH_ARM, tf = flags & TOUCH_FREE;
-        const float mu = S.fric >= 0.f ? S.fric : m.pair_friction[p];
-        const float tran = m.pair_tran[p];
-        const float margin = m.pair_margin[p];
-        const float imp = impedance(m.pair_solimp[p], cdist, margin);
-        const float diag = tran + mu * mu * tran;
-        const float R0 = fmaxf(MINVALF, (1.f - imp) * diag / imp);
-        const float Rpy = 2.f * mu * mu * R0 / m.impratio;
-        const bool lds = ncon < LDS_CON;
-        if (lds) {
+            const bool ta = flags & TOUCH_ARM, tf = flags & TOUCH_FREE;
+            const float mu = S.fric >= 0.f ? S.fric : m.pair_friction[p];
+            const float tran = m.pair_tran[p];
+            const float margin = m.pair_margin[p];
+            const float imp = impedance(m.pair_solimp[p], cdist, margin);
+            const float diag = tran + mu * mu * tran;
+            const float R0 = fmaxf(MINVALF, (1.f - imp) * diag / imp);
+            const float Rpy = 2.f * mu * mu * R0 / m.impratio;
+            const bool lds = ncon < LDS_CON;
+            if (lds) {
 #pragma unroll
-          for (int q = 0; q < 3; q++)
+              for (int q = 0; q < 3; q++)
 #pragma unroll
-            for (int i = 0; i < NV; i++) L.at(ncon, 12 * q + i) = jd[q][i];
-          L.at(ncon, F_MU) = mu;
-          L.at(ncon, F_R) = Rpy;
-          L.at(ncon, F_FLAGS) = (float)flags;
-        }
+                for (int i = 0; i < NV; i++) L.at(ncon, 12 * q + i) = jd[q][i];
+              L.at(ncon, F_MU) = mu;
+              L.at(ncon, F_R) = Rpy;
+              L.at(ncon, F_FLAGS) = (float)flags;
+              if constexpr (NF == 1) {
+                if (!ta) {  // Gram form of a free-body-only contact: G = [Jn;Jt1;Jt2] Fd [Jn;Jt1;Jt2]'
+                  float G[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int ed = 0; ed < 4; ed++) {
-          float J[NV], W[NV];
-          edge_J<NV>(jd[0], jd[1], jd[2], ed, mu, J);
-          float vel = 0.f;
+                  for (int i = 0; i < 6; i++) {
+                    const float w = S_FD(Mi, i), x = jd[0][NA + i], y = jd[1][NA + i], z = jd[2][NA + i];
+                    G[0] += w * x * x, G[1] += w * x * y, G[2] += w * x * z;
+                    G[3] += w * y * y, G[4] += w * y * z, G[5] += w * z * z;
+                  }
 #pragma unroll
-          for (int i = 0; i < NV; i++) vel += J[i] * S.qvel[i];
-          Mi.mul(J, W, ta, tf);
-          const float ard = dotv<NA, NF>(J, W, ta, tf) + Rpy;
-          const float ar = -m.pair_KB[p][1] * vel - m.pair_KB[p][0] * imp * (cdist - margin);
-          if (lds) {
-            L.at(ncon, F_AREF + ed) = ar;
-            L.at(ncon, F_ARD + ed) = ard;
-            L.at(ncon, F_IARD + ed) = 1.f / ard;
-          } else {
-            const int r = 4 * ncon + ed;
-#pragma unroll
-            for (int i = 0; i < NV; i++) {
-              cr.J(r, i) = J[i];
-              cr.W(r, i) = W[i];
+                  for (int ed = 0; ed < 4; ed++) {  // column of G for J_e = J_n + s J_tk
+                    const float s = (ed & 1) ? -mu : mu;
+                    const bool k2 = ed >> 1;
+                    L.at(ncon, F_COEF + 3 * ed + 0) = G[0] + s * (k2 ? G[2] : G[1]);
+                    L.at(ncon, F_COEF + 3 * ed + 1) = G[1] + s * (k2 ? G[4] : G[3]);
+                    L.at(ncon, F_COEF + 3 * ed + 2) = G[2] + s * (k2 ? G[5] : G[4]);
+                  }
+                }
+              }
             }
-            cr.S(r, 0) = ar;
-            cr.S(r, 1) = Rpy;
-            cr.S(r, 2) = ard;
+#pragma unroll
+            for (int ed = 0; ed < 4; ed++) {
+              float J[NV], W[NV];
+              edge_J<NV>(jd[0], jd[1], jd[2], ed, mu, J);
+              float vel = 0.f;
+#pragma unroll
+              for (int i = 0; i < NV; i++) vel += J[i] * S.qvel[i];
+              Mi.mul(J, W, ta, tf);
+              const float ard = dotv<NA, NF>(J, W, ta, tf) + Rpy;
+              const float ar = -m.pair_KB[p][1] * vel - m.pair_KB[p][0] * imp * (cdist - margin);
+              if (lds) {
+                L.at(ncon, F_AREF + ed) = ar;
+                L.at(ncon, F_HARD + ed) = 0.5f * ard;
+                L.at(ncon, F_IARD + ed) = 1.f / ard;
+              } else {
+                const int r = 4 * ncon + ed;
+#pragma unroll
+                for (int i = 0; i < NV; i++) {
+                  cr.J(r, i) = J[i];
+                  cr.W(r, i) = W[i];
+                }
+                cr.S(r, 0) = ar;
+                cr.S(r, 1) = Rpy;
+                cr.S(r, 2) = ard;
+              }
+            }
+            ncon++;
           }
         }
-        ncon++;
       }
     }
   }
@@ -282,22 +352,23 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
 #pragma unroll
   for (int i = 0; i < NV; i++) v[i] = S.qacc_s[i];
 #pragma unroll
-  for (int s = 0; s < 3 * NA; s++) {
-    const int i = slot_dof(s);
-    const float sg = slot_sgn(s);
-    const float jar = sg * S.warm[i] - aref[s];
-    float fs;
-    if (s < NA) {
-      const float fl = m.dof_frictionloss[i];
-      fs = (jar <= -fl * R[s]) ? fl : (jar >= fl * R[s]) ? -fl : -jar / R[s];
-    } else {
-      fs = jar < 0.f ? -jar / R[s] : 0.f;
-    }
-    f[s] = act[s] ? fs : 0.f;
+  for (int i = 0; i < NA; i++) {
+    const float fl = m.dof_frictionloss[i];
+    const float jar = S.warm[i] - fa[i];
+    const float fs = (jar <= -fl * fR[i]) ? fl : (jar >= fl * fR[i]) ? -fl : -jar / fR[i];
+    ff[i] = fl > 0.f ? fs : 0.f;
 #pragma unroll
-    for (int k = 0; k < NA; k++) v[k] += Mi.a(i, k) * sg * f[s];
+    for (int k = 0; k < NA; k++) v[k] += Mi.a(i, k) * ff[i];
   }
-  float cost = 0.f;
+  for (int l = 0; l < nlim; l++) {
+    float oh[NA];
+    one_hot<NA>((int)L.lm(l, L_DOF), oh);
+    const float sg = L.lm(l, L_SGN);
+    const float jar = sg * pick<NA>(S.warm, oh) - L.lm(l, L_AREF);
+    const float fs = jar < 0.f ? -jar / L.lm(l, L_R) : 0.f;
+    L.lm(l, L_FRC) = fs;
+    add_arm_col(Mi, v, oh, sg * fs);
+  }
   for (int c = 0; c < nl; c++) {
     const int fl = (int)L.at(c, F_FLAGS);
     const bool ta = fl & TOUCH_ARM, tf = fl & TOUCH_FREE;
@@ -331,11 +402,15 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       for (int i = 0; i < NV; i++) v[i] += cr.W(r, i) * fs;
     }
   // dual cost of the warm start: sum_r 0.5 f_r (J_r v - aref_r + R_r f_r) + 0.5 f_r (J_r qacc_smooth - aref_r)
+  float cost = 0.f;
 #pragma unroll
-  for (int s = 0; s < 3 * NA; s++) {
-    const int i = slot_dof(s);
-    const float sg = slot_sgn(s);
-    cost += 0.5f * f[s] * (sg * v[i] - aref[s] + R[s] * f[s]) + 0.5f * f[s] * (sg * S.qacc_s[i] - aref[s]);
+  for (int i = 0; i < NA; i++)
+    cost += 0.5f * ff[i] * (v[i] - fa[i] + fR[i] * ff[i]) + 0.5f * ff[i] * (S.qacc_s[i] - fa[i]);
+  for (int l = 0; l < nlim; l++) {
+    float oh[NA];
+    one_hot<NA>((int)L.lm(l, L_DOF), oh);
+    const float sg = L.lm(l, L_SGN), f = L.lm(l, L_FRC), ar = L.lm(l, L_AREF);
+    cost += 0.5f * f * (sg * pick<NA>(v, oh) - ar + L.lm(l, L_R) * f) + 0.5f * f * (sg * pick<NA>(S.qacc_s, oh) - ar);
   }
   for (int c = 0; c < nl; c++) {
     const int fl = (int)L.at(c, F_FLAGS);
@@ -369,7 +444,8 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
     }
   if (cost > 0.f) {
 #pragma unroll
-    for (int s = 0; s < 3 * NA; s++) f[s] = 0.f;
+    for (int i = 0; i < NA; i++) ff[i] = 0.f;
+    for (int l = 0; l < nlim; l++) L.lm(l, L_FRC) = 0.f;
     for (int c = 0; c < nl; c++)
 #pragma unroll
       for (int ed = 0; ed < 4; ed++) L.at(c, F_FRC + ed) = 0.f;
@@ -383,67 +459,80 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
 #pragma unroll
   for (int i = 0; i < NA; i++) tr += S.MA[i * (i + 1) / 2 + i];
 #pragma unroll
-  for (int ff = 0; ff < NF; ff++)
+  for (int f2 = 0; f2 < NF; f2++)
 #pragma unroll
-    for (int i = 0; i < 6; i++) tr += S.MF[ff][i * (i + 1) / 2 + i];
+    for (int i = 0; i < 6; i++) tr += S.MF[f2][i * (i + 1) / 2 + i];
   const float scale = 1.f / tr;
   for (int it = 0; it < m.iterations; it++) {
     float improvement = 0.f;
 #pragma unroll
-    for (int s = 0; s < 3 * NA; s++) {
-      if (!act[s]) continue;
-      const int i = slot_dof(s);
-      const float sg = slot_sgn(s);
-      const float res = sg * v[i] - aref[s] + R[s] * f[s];
-      float fn = f[s] - res * iARd[s];
-      if (s < NA) {
-        const float fl = m.dof_frictionloss[i];
-        fn = fminf(fmaxf(fn, -fl), fl);
-      } else {
-        fn = fmaxf(fn, 0.f);
-      }
-      const float df = fn - f[s];
+    for (int i = 0; i < NA; i++) {
+      const float fl = m.dof_frictionloss[i];
+      if (!(fl > 0.f)) continue;  // model constant: wave-uniform
+      const float res = v[i] - fa[i] + fR[i] * ff[i];
+      const float fn = fminf(fmaxf(ff[i] - res * fiD[i], -fl), fl);
+      const float df = fn - ff[i];
 #pragma unroll
-      for (int k = 0; k < NA; k++) v[k] += Mi.a(i, k) * sg * df;
-      f[s] = fn;
-      improvement -= df * res + 0.5f * ARd[s] * df * df;
+      for (int k = 0; k < NA; k++) v[k] += Mi.a(i, k) * df;
+      ff[i] = fn;
+      improvement -= df * (res + fhD[i] * df);
+    }
+    for (int l = 0; l < nlim; l++) {
+      float oh[NA];
+      one_hot<NA>((int)L.lm(l, L_DOF), oh);
+      const float sg = L.lm(l, L_SGN), fo = L.lm(l, L_FRC);
+      const float res = sg * pick<NA>(v, oh) - L.lm(l, L_AREF) + L.lm(l, L_R) * fo;
+      const float fn = fmaxf(fo - res * L.lm(l, L_IARD), 0.f);
+      const float df = fn - fo;
+      add_arm_col(Mi, v, oh, sg * df);
+      L.lm(l, L_FRC) = fn;
+      improvement -= df * (res + 0.5f * L.lm(l, L_ARD) * df);
     }
     for (int c = 0; c < nl; c++) {
       const int fl = (int)L.at(c, F_FLAGS);
       const bool ta = fl & TOUCH_ARM, tf = fl & TOUCH_FREE;
       if constexpr (NF == 1) {
-        // Fast path, wave-uniform: no active lane's contact c touches the arm (cube on the
-        // table).  6-dof math on the free body only, every LDS load of the record issued up
-        // front, forces read once / written once.  Same arithmetic as the general path.
+        // Gram path, wave-uniform: no active lane's contact c touches the arm (cube on the
+        // table).  a, b, c = J_n v, J_t1 v, J_t2 v; each edge's residual is a + s b (or c),
+        // and its force step moves (a, b, c) by the stored Gram column; v itself is
+        // updated once per contact.
         if (__all(!ta)) {
-          float jn[6], jt1[6], jt2[6], fo[4], ar[4], ia[4], ad[4];
+          float jn[6], j1[6], j2[6], fo[4], ar[4], ia[4], hd[4], cf[12];
 #pragma unroll
           for (int i = 0; i < 6; i++)
-            jn[i] = L.at(c, NA + i), jt1[i] = L.at(c, 12 + NA + i), jt2[i] = L.at(c, 24 + NA + i);
+            jn[i] = L.at(c, NA + i), j1[i] = L.at(c, 12 + NA + i), j2[i] = L.at(c, 24 + NA + i);
 #pragma unroll
           for (int ed = 0; ed < 4; ed++)
             fo[ed] = L.at(c, F_FRC + ed), ar[ed] = L.at(c, F_AREF + ed), ia[ed] = L.at(c, F_IARD + ed),
-            ad[ed] = L.at(c, F_ARD + ed);
+            hd[ed] = L.at(c, F_HARD + ed);
+#pragma unroll
+          for (int k = 0; k < 12; k++) cf[k] = L.at(c, F_COEF + k);
           const float mu = L.at(c, F_MU), Rp = L.at(c, F_R);
+          float a = 0.f, b = 0.f, cc = 0.f;
+#pragma unroll
+          for (int i = 0; i < 6; i++) {
+            a += jn[i] * v[NA + i];
+            b += j1[i] * v[NA + i];
+            cc += j2[i] * v[NA + i];
+          }
+          float df[4];
 #pragma unroll
           for (int ed = 0; ed < 4; ed++) {
             const float s = (ed & 1) ? -mu : mu;
-            float J6[6], W6[6];
-#pragma unroll
-            for (int i = 0; i < 6; i++) {
-              J6[i] = jn[i] + s * ((ed >> 1) ? jt2[i] : jt1[i]);
-              W6[i] = S_FD(Mi, i) * J6[i];
-            }
-            const float d0 = J6[0] * v[NA] + J6[1] * v[NA + 1] + J6[2] * v[NA + 2];
-            const float d1 = J6[3] * v[NA + 3] + J6[4] * v[NA + 4] + J6[5] * v[NA + 5];
-            const float res = (d0 + d1) - ar[ed] + Rp * fo[ed];
+            const float res = (a + s * ((ed >> 1) ? cc : b)) - ar[ed] + Rp * fo[ed];
             const float fnew = fmaxf(fo[ed] - res * ia[ed], 0.f);
-            const float df = fnew - fo[ed];
-#pragma unroll
-            for (int i = 0; i < 6; i++) v[NA + i] += W6[i] * df;
-            improvement -= df * res + 0.5f * ad[ed] * df * df;
+            df[ed] = fnew - fo[ed];
+            a += cf[3 * ed] * df[ed];
+            b += cf[3 * ed + 1] * df[ed];
+            cc += cf[3 * ed + 2] * df[ed];
+            improvement -= df[ed] * (res + hd[ed] * df[ed]);
             fo[ed] = fnew;
           }
+          // sum_e J_e df_e = J_n (df0+df1+df2+df3) + mu J_t1 (df0-df1) + mu J_t2 (df2-df3)
+          const float Dn = (df[0] + df[1]) + (df[2] + df[3]);
+          const float D1 = mu * (df[0] - df[1]), D2 = mu * (df[2] - df[3]);
+#pragma unroll
+          for (int i = 0; i < 6; i++) v[NA + i] += S_FD(Mi, i) * (jn[i] * Dn + j1[i] * D1 + j2[i] * D2);
 #pragma unroll
           for (int ed = 0; ed < 4; ed++) L.at(c, F_FRC + ed) = fo[ed];
           continue;
@@ -465,7 +554,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       for (int ed = 0; ed < 4; ed++) {
         float J[NV];
         edge_J<NV>(jn, jt1, jt2, ed, mu, J);
-        const float fo = L.at(c, F_FRC + ed), ard = L.at(c, F_ARD + ed);
+        const float fo = L.at(c, F_FRC + ed);
         const float res = dotv<NA, NF>(J, v, ta, tf) - L.at(c, F_AREF + ed) + Rp * fo;
         const float fnew = fmaxf(fo - res * L.at(c, F_IARD + ed), 0.f);
         const float df = fnew - fo;
@@ -475,7 +564,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
 #pragma unroll
           for (int i = 0; i < NV; i++) v[i] += W[i] * df;
           L.at(c, F_FRC + ed) = fnew;
-          improvement -= df * res + 0.5f * ard * df * df;
+          improvement -= df * (res + L.at(c, F_HARD + ed) * df);
         }
       }
     }
@@ -503,7 +592,14 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
     S.fcon[i] = 0.f;
   }
 #pragma unroll
-  for (int s = 0; s < 3 * NA; s++) S.fcon[slot_dof(s)] += slot_sgn(s) * f[s];
+  for (int i = 0; i < NA; i++) S.fcon[i] += ff[i];
+  for (int l = 0; l < nlim; l++) {
+    float oh[NA];
+    one_hot<NA>((int)L.lm(l, L_DOF), oh);
+    const float t = L.lm(l, L_SGN) * L.lm(l, L_FRC);
+#pragma unroll
+    for (int k = 0; k < NA; k++) S.fcon[k] = fmaf(oh[k], t, S.fcon[k]);
+  }
   for (int c = 0; c < nl; c++) {
     float jn[NV], jt1[NV], jt2[NV];
 #pragma unroll

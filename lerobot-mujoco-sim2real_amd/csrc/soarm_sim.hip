@@ -51,6 +51,7 @@ struct sim_batch {
   float* d_gpose = nullptr;    // geom world poses [geom*12+k][env]
   float* d_cbuf = nullptr;     // collide output [slot*7+f][env]
   int* d_ccount = nullptr;     // contacts per pair [pair][env]
+  uint32_t* d_pmask = nullptr; // pairs with contacts, bit p%32 of word p/32: [word][env]
   // profiling (sim_profile_begin/end)
   bool prof = false;
   std::vector<hipEvent_t> ev_pool;
@@ -132,13 +133,13 @@ DEVI void write_obs(const Sim<NA, NF>& S, float* obs, int e) {
 // one mj_forward (position + velocity + acceleration stages); the contacts
 // (cbuf/ccount, may be null) were produced by k_collide from this substep's positions
 template <int NA, int NF, bool CON>
-DEVI int forward(Sim<NA, NF>& S, const float* cbuf, const int* ccount, int n, int e, const RowLds& L,
-                 const ContactRows<NA, NF>& cr) {
+DEVI int forward(Sim<NA, NF>& S, const float* cbuf, const int* ccount, const uint32_t* pmask, int n, int e,
+                 const RowLds& L, const ContactRows<NA, NF>& cr) {
   S.kinematics();
   S.com_crb();
   S.factor();
   S.smooth_forces();
-  return solve_constraints<NA, NF, CON>(S, cbuf, ccount, n, e, L, cr);
+  return solve_constraints<NA, NF, CON>(S, cbuf, ccount, pmask, n, e, L, cr);
 }
 
 // contact-free scenes (mjDSBL_CONTACT): all frame_skip substeps fused in one launch
@@ -157,15 +158,16 @@ __global__ __launch_bounds__(64) void k_step(const DModel* __restrict__ dm, int 
     for (int k = 0; k < NA; k++)
       if (k < m.nact) S.ctrl[k] = action[(size_t)e * m.nact + k];
   }
-  const RowLds L{nullptr, 0};
+  __shared__ float s_lim[NA * LF][64];
+  const RowLds L{nullptr, s_lim, (int)threadIdx.x};
   const ContactRows<NA, NF> cr{nullptr, n};
   for (int s = 0; s < nsub; s++) {
     S.relaunder();
     S.check_state();
-    forward<NA, NF, false>(S, nullptr, nullptr, n, e, L, cr);
+    forward<NA, NF, false>(S, nullptr, nullptr, nullptr, n, e, L, cr);
     if (S.acc_bad()) {
       S.soft_reset(SIM_ST_BADQACC);
-      forward<NA, NF, false>(S, nullptr, nullptr, n, e, L, cr);
+      forward<NA, NF, false>(S, nullptr, nullptr, nullptr, n, e, L, cr);
     }
     S.integrate();
   }
@@ -188,7 +190,8 @@ __global__ __launch_bounds__(64) void k_geom(const DModel* __restrict__ dm, int 
 // mj_collision, one lane per (env, candidate pair); blockIdx.y = pair
 __global__ __launch_bounds__(256) void k_collide(const DModel* __restrict__ dm, int n,
                                                  const float* __restrict__ gpose,
-                                                 float* __restrict__ cbuf, int* __restrict__ ccount) {
+                                                 float* __restrict__ cbuf, int* __restrict__ ccount,
+                                                 uint32_t* __restrict__ pmask) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   const int p = blockIdx.y;
   if (e >= n) return;
@@ -199,6 +202,7 @@ __global__ __launch_bounds__(256) void k_collide(const DModel* __restrict__ dm, 
   PairOut o;
   collide_pair(m, p, P1, P2, o);
   ccount[(size_t)p * n + e] = o.n;
+  if (o.n > 0) atomicOr(&pmask[(size_t)(p >> 5) * n + e], 1u << (p & 31));
   const int s0 = m.pair_slot[p];
 #pragma unroll
   for (int k = 0; k < PAIR_MAXCON; k++)
@@ -240,6 +244,7 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
                                                 float* __restrict__ scratch,
                                                 const float* __restrict__ cbuf,
                                                 const int* __restrict__ ccount,
+                                                uint32_t* __restrict__ pmask,
                                                 float* __restrict__ gpose) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
@@ -253,17 +258,20 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
       if (k < m.nact) S.ctrl[k] = action[(size_t)e * m.nact + k];
   }
   __shared__ float s_rows[LDS_CON * CF][64];
-  const RowLds L{s_rows, (int)threadIdx.x};
+  __shared__ float s_lim[NA * LF][64];
+  const RowLds L{s_rows, s_lim, (int)threadIdx.x};
   const ContactRows<NA, NF> cr{scratch + e, n};
   const int st0 = S.status;
   S.check_state();
   // a soft reset moved the env: the collide output no longer applies
   const bool use = S.status == st0 && ccount != nullptr;
-  int ncon = forward<NA, NF, true>(S, use ? cbuf : nullptr, use ? ccount : nullptr, n, e, L, cr);
+  int ncon = forward<NA, NF, true>(S, use ? cbuf : nullptr, use ? ccount : nullptr, pmask, n, e, L, cr);
   if (S.acc_bad()) {
     S.soft_reset(SIM_ST_BADQACC);
-    ncon = forward<NA, NF, true>(S, nullptr, nullptr, n, e, L, cr);
+    ncon = forward<NA, NF, true>(S, nullptr, nullptr, nullptr, n, e, L, cr);
   }
+  if (pmask)  // consumed: clear for the next collide
+    for (int w = 0; w < (m.npair + 31) >> 5; w++) pmask[(size_t)w * n + e] = 0u;
   const float ee[3] = {S.ee[0], S.ee[1], S.ee[2]};
   S.integrate();
   store_state(S, st, n, e);
@@ -281,10 +289,11 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
 // diagnostic: compacted contact list [N][SIM_MAXCON][8] (dist, pos, normal, pair) + count
 __global__ __launch_bounds__(64) void k_gather(const DModel* __restrict__ dm, int n,
                                                const float* __restrict__ cbuf,
-                                               const int* __restrict__ ccount, float* __restrict__ out,
-                                               int* __restrict__ nout) {
+                                               const int* __restrict__ ccount, uint32_t* __restrict__ pmask,
+                                               float* __restrict__ out, int* __restrict__ nout) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
+  for (int w = 0; w < (dm->npair + 31) >> 5; w++) pmask[(size_t)w * n + e] = 0u;
   __shared__ float s_con[SIM_MAXCON * 8][64];
   const ConLds C{s_con, (int)threadIdx.x};
   int status = 0;
@@ -722,6 +731,9 @@ int sim_batch_create(const sim_model* m, int n_envs, int device, sim_batch** out
     HIPCHECK(hipMalloc(&B->d_gpose, (size_t)m->desc.ngeom * 12 * n_envs * sizeof(float)));
     HIPCHECK(hipMalloc(&B->d_cbuf, (size_t)(m->dm.nslot > 0 ? m->dm.nslot : 1) * 7 * n_envs * sizeof(float)));
     HIPCHECK(hipMalloc(&B->d_ccount, (size_t)(m->desc.npair > 0 ? m->desc.npair : 1) * n_envs * sizeof(int)));
+    const size_t nw = (size_t)((m->desc.npair + 31) / 32 > 0 ? (m->desc.npair + 31) / 32 : 1);
+    HIPCHECK(hipMalloc(&B->d_pmask, nw * n_envs * sizeof(uint32_t)));
+    HIPCHECK(hipMemset(B->d_pmask, 0, nw * n_envs * sizeof(uint32_t)));
   }
   *out = B;
   return SIM_OK;
@@ -739,6 +751,7 @@ void sim_batch_free(sim_batch* b) {
   (void)hipFree(b->d_gpose);
   (void)hipFree(b->d_cbuf);
   (void)hipFree(b->d_ccount);
+  (void)hipFree(b->d_pmask);
   for (auto e : b->ev_pool) (void)hipEventDestroy(e);
   delete b;
 }
@@ -801,14 +814,15 @@ int sim_step(sim_batch* b, const sim_state* s, const float* action, int frame_sk
       if (np > 0) {
         prof_mark(b, 1, st);
         hipLaunchKernelGGL(k_collide, dim3((b->n + 255) / 256, np), dim3(256), 0, st, b->d_model, b->n,
-                           b->d_gpose, b->d_cbuf, b->d_ccount);
+                           b->d_gpose, b->d_cbuf, b->d_ccount, b->d_pmask);
         prof_mark(b, -1, st);
       }
       const bool last = sub == frame_skip - 1;
       prof_mark(b, 2, st);
       hipLaunchKernelGGL((k_substep<NA, NF>), grid_for(b->n), dim3(64), 0, st, b->d_model, b->n, *s,
                          sub == 0 ? action : nullptr, last ? obs : nullptr, b->params, b->d_scratch,
-                         b->d_cbuf, np > 0 ? b->d_ccount : nullptr, last ? nullptr : b->d_gpose);
+                         b->d_cbuf, np > 0 ? b->d_ccount : nullptr, np > 0 ? b->d_pmask : nullptr,
+                         last ? nullptr : b->d_gpose);
       prof_mark(b, -1, st);
     }
   });
@@ -853,8 +867,8 @@ int sim_contacts(sim_batch* b, const sim_state* s, float* out, int32_t* ncon, vo
   });
   if (np > 0)
     hipLaunchKernelGGL(k_collide, dim3((b->n + 255) / 256, np), dim3(256), 0, st, b->d_model, b->n,
-                       b->d_gpose, b->d_cbuf, b->d_ccount);
-  hipLaunchKernelGGL(k_gather, grid_for(b->n), dim3(64), 0, st, b->d_model, b->n, b->d_cbuf, b->d_ccount,
+                       b->d_gpose, b->d_cbuf, b->d_ccount, b->d_pmask);
+  hipLaunchKernelGGL(k_gather, grid_for(b->n), dim3(64), 0, st, b->d_model, b->n, b->d_cbuf, b->d_ccount, b->d_pmask,
                      out, ncon);
   HIPCHECK(hipGetLastError());
   return SIM_OK;

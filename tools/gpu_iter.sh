@@ -7,4 +7,4 @@ rc=$?
 echo "pytest rc=$rc" >> gpurun_out/pytest_gpu.log
 grep -E "passed|failed|Error|assert" gpurun_out/pytest_gpu.log | tail -25
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-timeout -k 10 600 python bench.py --steps 30 --warmup 5 --no-cpu-baseline > gpurun_out/bench_contact.json 2> gpurun_out/bench_contact.err && cat gpurun_out/bench_contact.json
+timeout -k 10 600 python bench.py --no-cpu-baseline > gpurun_out/bench_contact.json 2> gpurun_out/bench_contact.err && cat gpurun_out/bench_contact.json
