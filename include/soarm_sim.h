@@ -248,6 +248,11 @@ int sim_observe(sim_batch* b, const sim_state* s, float* obs, void* stream);
    int32 bits), ncon [N].  Contact order = candidate-pair order (MuJoCo's). */
 int sim_contacts(sim_batch* b, const sim_state* s, float* out, int32_t* ncon, void* stream);
 
+/* diagnostic: geom poses + one collide pass with per-pair timing; cycles [npair]
+   (host) = sum over waves of each wave's shader-clock cycles for that pair.
+   Synchronous. */
+int sim_collide_profile(sim_batch* b, const sim_state* s, double* cycles, void* stream);
+
 /* kernel timing: between begin and end, sim_step brackets every kernel launch
    with HIP events on its stream; end synchronises and returns the summed
    milliseconds and launch counts per kernel kind

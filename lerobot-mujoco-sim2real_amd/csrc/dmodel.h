@@ -5,6 +5,8 @@
 // step but that depend only on the model (frictionloss-row impedance, K/B of
 // each solref, rotation matrices of fixed quaternions) are folded here.
 #pragma once
+#include <hip/hip_runtime.h>
+#include <math.h>
 #include <stdint.h>
 
 #include "../../include/soarm_sim.h"
@@ -60,21 +62,50 @@ struct DModel {
   float act_ctrlrange[MAXU][2], act_forcerange[MAXU][2];
 
   // hull data (device pointers)
-  const float4* hull_vert;  // xyz, w unused
-  const int32_t* hull_adr;  // CSR offsets per global vertex (+1)
-  const int32_t* hull_adj;  // local neighbour ids
-  const int32_t* hull_seed; // per mesh geom: HULL_NSEED local start vertices for hill climbing
+  const float4* hull_vert;   // xyz; w = bits (adjacency start << 8 | degree) of the vertex
+  const int32_t* hull_adr;   // CSR offsets per global vertex (+1)
+  const int32_t* hull_adj;   // local neighbour ids
+  const uint16_t* hull_lut;  // per mesh geom: HULL_LUT_CELLS start vertices (cube-map of directions)
+  int geom_lutadr[MAXG];     // first LUT entry of each mesh geom (-1: not a mesh)
 };
 
-// Hill-climbing seeds: the argmax vertex of each hull for HULL_NSEED directions
-// on a Fibonacci sphere.  Climbing starts at the best seed for the query
-// direction, so a support query walks a few edges instead of crossing the hull.
-constexpr int HULL_NSEED = 32;
-inline void fibonacci_dir(int k, double d[3]) {
-  const double z = 1.0 - (2.0 * k + 1.0) / HULL_NSEED;
-  const double r = __builtin_sqrt(1.0 - z * z);
-  const double phi = k * 2.399963229728653;  // pi * (3 - sqrt 5)
-  d[0] = r * __builtin_cos(phi), d[1] = r * __builtin_sin(phi), d[2] = z;
+// Support-point start table: a cube map of HULL_LUT_K x HULL_LUT_K cells per
+// face; each cell holds the hull's argmax vertex for the cell-centre
+// direction.  Hill climbing starts there, so a query walks ~1 edge (the
+// final step only verifies the local maximum).
+constexpr int HULL_LUT_K = 16;
+constexpr int HULL_LUT_CELLS = 6 * HULL_LUT_K * HULL_LUT_K;
+
+// cube-map cell of a (not necessarily unit) direction; same mapping on host and device
+inline __host__ __device__ int lut_cell(float l0, float l1, float l2) {
+  const float a0 = fabsf(l0), a1 = fabsf(l1), a2 = fabsf(l2);
+  int face;
+  float u, v, m;
+  if (a0 >= a1 && a0 >= a2) {
+    face = l0 >= 0.f ? 0 : 1, m = a0, u = l1, v = l2;
+  } else if (a1 >= a2) {
+    face = l1 >= 0.f ? 2 : 3, m = a1, u = l0, v = l2;
+  } else {
+    face = l2 >= 0.f ? 4 : 5, m = a2, u = l0, v = l1;
+  }
+  if (!(m > 0.f)) return 0;
+  const float s = 0.5f * HULL_LUT_K / m;
+  int i = (int)((u + m) * s), j = (int)((v + m) * s);
+  i = i < 0 ? 0 : (i >= HULL_LUT_K ? HULL_LUT_K - 1 : i);
+  j = j < 0 ? 0 : (j >= HULL_LUT_K ? HULL_LUT_K - 1 : j);
+  return (face * HULL_LUT_K + i) * HULL_LUT_K + j;
+}
+
+// centre direction of a cube-map cell (inverse of lut_cell)
+inline void lut_dir(int cell, double d[3]) {
+  const int face = cell / (HULL_LUT_K * HULL_LUT_K), i = (cell / HULL_LUT_K) % HULL_LUT_K, j = cell % HULL_LUT_K;
+  const double u = -1.0 + (2.0 * i + 1.0) / HULL_LUT_K, v = -1.0 + (2.0 * j + 1.0) / HULL_LUT_K;
+  const double sg = (face & 1) ? -1.0 : 1.0;
+  switch (face >> 1) {
+    case 0: d[0] = sg, d[1] = u, d[2] = v; break;
+    case 1: d[0] = u, d[1] = sg, d[2] = v; break;
+    default: d[0] = u, d[1] = v, d[2] = sg; break;
+  }
 }
 
 }  // namespace soarm

@@ -59,35 +59,36 @@ struct PairOut {
 // hill-climbing support on a mesh hull; returns the local vertex
 DEVI float3 hull_support(const DModel& m, int g, const float l[3]) {
   const float4* v = m.hull_vert + m.geom_hulladr[g];
-  const int32_t* adr = m.hull_adr + m.geom_hulladr[g];
   const int nvert = m.geom_hullnum[g];
-  // best seed (the seed vertices are shared by every lane of the wave: cache-line broadcast)
-  const int32_t* seed = m.hull_seed + g * HULL_NSEED;
-  int cur = seed[0];
+  // start at the cube-map cell's vertex (the table is shared by the whole wave: one
+  // pair per block, so these loads hit the same few cache lines)
+  int cur = m.hull_lut[m.geom_lutadr[g] + lut_cell(l[0], l[1], l[2])];
   float4 cv = v[cur];
   float cd = l[0] * cv.x + l[1] * cv.y + l[2] * cv.z;
-#pragma unroll 8
-  for (int k = 1; k < HULL_NSEED; k++) {
-    const int s = seed[k];
-    const float4 w = v[s];
-    const float d = l[0] * w.x + l[1] * w.y + l[2] * w.z;
-    if (d > cd) cd = d, cur = s;
-  }
   for (int guard = 0; guard < nvert; guard++) {
+    // the vertex record carries its adjacency range: one dependent round trip for the
+    // neighbour ids, one for their coordinates (8 at a time, loads issued together)
+    const uint32_t w = __float_as_uint(cv.w);
+    const int a0 = (int)(w >> 8), a1 = a0 + (int)(w & 255u);
     int nxt = cur;
     float nd = cd;
-    const int a0 = adr[cur], a1 = adr[cur + 1];
-    for (int a = a0; a < a1; a++) {
-      const int u = m.hull_adj[a];
-      const float4 w = v[u];
-      const float s = l[0] * w.x + l[1] * w.y + l[2] * w.z;
-      if (s > nd) nd = s, nxt = u;
+    float4 nv = cv;
+    for (int a = a0; a < a1; a += 8) {
+      int u[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) u[k] = (a + k < a1) ? m.hull_adj[a + k] : cur;
+      float4 wv[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) wv[k] = v[u[k]];
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const float s = l[0] * wv[k].x + l[1] * wv[k].y + l[2] * wv[k].z;
+        if (s > nd) nd = s, nxt = u[k], nv = wv[k];
+      }
     }
     if (nxt == cur) break;
-    cur = nxt;
-    cd = nd;
+    cur = nxt, cd = nd, cv = nv;
   }
-  cv = v[cur];
   return make_float3(cv.x, cv.y, cv.z);
 }
 
@@ -636,6 +637,13 @@ DEVI void collide_pair(const DModel& m, int p, const GeomPose& P1, const GeomPos
     if (sep) return;
   }
   if (t1 == SIM_GEOM_PLANE) {
+    // bounding sphere of geom2 entirely above the plane (beyond the margin): no contact
+    if (m.geom_rbound[g2] > 0.f) {
+      float c2[3];
+      geom_center(m, g2, P2, c2);
+      const float h = (c2[0] - P1.p[0]) * P1.R[2] + (c2[1] - P1.p[1]) * P1.R[5] + (c2[2] - P1.p[2]) * P1.R[8];
+      if (h > m.geom_rbound[g2] + m.pair_margin[p]) return;
+    }
     if (t2 == SIM_GEOM_BOX)
       plane_box(m, g1, g2, P1, P2, o);
     else if (t2 == SIM_GEOM_MESH)
@@ -645,6 +653,31 @@ DEVI void collide_pair(const DModel& m, int p, const GeomPose& P1, const GeomPos
   if (t1 == SIM_GEOM_BOX && t2 == SIM_GEOM_BOX) {
     box_box(m, g1, g2, P1, P2, o);
     return;
+  }
+  if (t1 == SIM_GEOM_BOX && t2 == SIM_GEOM_MESH) {
+    // separating-axis pre-test on the box face that faces the hull's centre most: if
+    // the hull's extreme point toward the box lies beyond that face, they are apart
+    // (exact; MPR would find no contact).  One support query instead of an MPR run.
+    float c2[3];
+    geom_center(m, g2, P2, c2);
+    const float r[3] = {c2[0] - P1.p[0], c2[1] - P1.p[1], c2[2] - P1.p[2]};
+    float best = -3.0e38f, ax[3] = {0.f, 0.f, 1.f}, h = 0.f;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      const float a[3] = {P1.R[k], P1.R[3 + k], P1.R[6 + k]};
+      const float dk = dot3(r, a);
+      const float gap = fabsf(dk) - m.geom_size[g1][k];
+      if (gap > best) {
+        const float sg = dk >= 0.f ? 1.f : -1.f;
+        best = gap, h = m.geom_size[g1][k];
+        ax[0] = sg * a[0], ax[1] = sg * a[1], ax[2] = sg * a[2];
+      }
+    }
+    const float nd[3] = {-ax[0], -ax[1], -ax[2]};
+    float sp[3];
+    support(m, g2, P2, nd, sp);
+    const float dist = (sp[0] - P1.p[0]) * ax[0] + (sp[1] - P1.p[1]) * ax[1] + (sp[2] - P1.p[2]) * ax[2] - h;
+    if (dist > m.pair_margin[p]) return;
   }
   MPair mp{m, g1, g2, P1, P2};
   float depth, dir[3], pos[3];

@@ -36,7 +36,9 @@ struct sim_model {
   sim_model_desc desc;
   DModel dm;  // host copy; hull pointers filled per batch
   std::vector<float4> hull_vert;
-  std::vector<int32_t> hull_adr, hull_adj, hull_seed;
+  std::vector<int32_t> hull_adr, hull_adj;
+  std::vector<uint16_t> hull_lut;
+  int lutadr[SIM_MAXGEOM];
   int na = 0, nf = 0;
 };
 
@@ -45,7 +47,8 @@ struct sim_batch {
   int n = 0, device = 0;
   DModel* d_model = nullptr;
   float4* d_hv = nullptr;
-  int32_t *d_hadr = nullptr, *d_hadj = nullptr, *d_hseed = nullptr;
+  int32_t *d_hadr = nullptr, *d_hadj = nullptr;
+  uint16_t* d_hlut = nullptr;
   float* d_scratch = nullptr;  // contact rows, [slot][env]
   size_t scratch_floats = 0;
   float* d_gpose = nullptr;    // geom world poses [geom*12+k][env]
@@ -191,10 +194,12 @@ __global__ __launch_bounds__(64) void k_geom(const DModel* __restrict__ dm, int 
 __global__ __launch_bounds__(256) void k_collide(const DModel* __restrict__ dm, int n,
                                                  const float* __restrict__ gpose,
                                                  float* __restrict__ cbuf, int* __restrict__ ccount,
-                                                 uint32_t* __restrict__ pmask) {
+                                                 uint32_t* __restrict__ pmask,
+                                                 unsigned long long* __restrict__ pcyc) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   const int p = blockIdx.y;
   if (e >= n) return;
+  const long long t0 = pcyc ? clock64() : 0;
   const DModel& m = *dm;
   GeomPose P1, P2;
   load_pose(gpose, n, e, m.pair_geom1[p], P1);
@@ -209,6 +214,7 @@ __global__ __launch_bounds__(256) void k_collide(const DModel* __restrict__ dm, 
     if (k < o.n)
 #pragma unroll
       for (int f = 0; f < 7; f++) cbuf[((size_t)(s0 + k) * 7 + f) * n + e] = o.c[k][f];
+  if (pcyc && (threadIdx.x & 63) == 0) atomicAdd(&pcyc[p], (unsigned long long)(clock64() - t0));
 }
 
 // walk the pairs in order and append their contacts (deterministic indexing)
@@ -674,22 +680,43 @@ int sim_model_create(const sim_model_desc* desc, const float* hull_vert, const i
     M->hull_adr.assign(hull_adr, hull_adr + desc->nhullvert + 1);
     M->hull_adj.assign(hull_adj, hull_adj + desc->nhulladj);
   }
-  // hill-climbing seeds: per mesh geom, the argmax vertex for each Fibonacci direction
-  M->hull_seed.assign((size_t)std::max(desc->ngeom, 1) * HULL_NSEED, 0);
-  for (int g = 0; g < desc->ngeom; g++) {
+  // vertex records carry their adjacency range (start << 8 | degree) in w
+  for (int i = 0; i < desc->nhullvert; i++) {
+    const int32_t a0 = M->hull_adr[i], deg = M->hull_adr[i + 1] - a0;
+    if (a0 < 0 || a0 >= (1 << 24) || deg < 0 || deg > 255) {
+      delete M;
+      return fail(SIM_E_MODEL, "hull graph too large for packed vertex records");
+    }
+    const uint32_t bits = ((uint32_t)a0 << 8) | (uint32_t)deg;
+    float wf;
+    memcpy(&wf, &bits, sizeof(wf));
+    M->hull_vert[i].w = wf;
+  }
+  // support start table: per mesh geom, the argmax vertex of each cube-map cell's centre direction
+  int nmesh = 0;
+  for (int g = 0; g < desc->ngeom; g++) nmesh += desc->geom_type[g] == SIM_GEOM_MESH;
+  M->hull_lut.assign((size_t)std::max(nmesh, 1) * HULL_LUT_CELLS, 0);
+  for (int g = 0, k = 0; g < desc->ngeom; g++) {
+    M->lutadr[g] = -1;
     if (desc->geom_type[g] != SIM_GEOM_MESH) continue;
+    if (desc->geom_hullnum[g] > 65535) {
+      delete M;
+      return fail(SIM_E_MODEL, "hull with more than 65535 vertices");
+    }
+    M->lutadr[g] = k * HULL_LUT_CELLS;
     const float* hv = hull_vert + 3 * (size_t)desc->geom_hulladr[g];
-    for (int k = 0; k < HULL_NSEED; k++) {
+    for (int c = 0; c < HULL_LUT_CELLS; c++) {
       double d[3];
-      fibonacci_dir(k, d);
+      lut_dir(c, d);
       int best = 0;
       double bd = -1e300;
       for (int i = 0; i < desc->geom_hullnum[g]; i++) {
         const double s = d[0] * hv[3 * i] + d[1] * hv[3 * i + 1] + d[2] * hv[3 * i + 2];
         if (s > bd) bd = s, best = i;
       }
-      M->hull_seed[(size_t)g * HULL_NSEED + k] = best;
+      M->hull_lut[(size_t)k * HULL_LUT_CELLS + c] = (uint16_t)best;
     }
+    k++;
   }
   *out = M;
   return SIM_OK;
@@ -719,9 +746,10 @@ int sim_batch_create(const sim_model* m, int n_envs, int device, sim_batch** out
   dm.hull_vert = B->d_hv;
   dm.hull_adr = B->d_hadr;
   dm.hull_adj = B->d_hadj;
-  HIPCHECK(hipMalloc(&B->d_hseed, m->hull_seed.size() * sizeof(int32_t)));
-  HIPCHECK(hipMemcpy(B->d_hseed, m->hull_seed.data(), m->hull_seed.size() * sizeof(int32_t), hipMemcpyHostToDevice));
-  dm.hull_seed = B->d_hseed;
+  HIPCHECK(hipMalloc(&B->d_hlut, m->hull_lut.size() * sizeof(uint16_t)));
+  HIPCHECK(hipMemcpy(B->d_hlut, m->hull_lut.data(), m->hull_lut.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+  dm.hull_lut = B->d_hlut;
+  for (int g = 0; g < MAXG; g++) dm.geom_lutadr[g] = g < m->desc.ngeom ? m->lutadr[g] : -1;
   HIPCHECK(hipMalloc(&B->d_model, sizeof(DModel)));
   HIPCHECK(hipMemcpy(B->d_model, &dm, sizeof(DModel), hipMemcpyHostToDevice));
   if (!m->desc.disable_contact) {
@@ -746,7 +774,7 @@ void sim_batch_free(sim_batch* b) {
   (void)hipFree(b->d_hv);
   (void)hipFree(b->d_hadr);
   (void)hipFree(b->d_hadj);
-  (void)hipFree(b->d_hseed);
+  (void)hipFree(b->d_hlut);
   (void)hipFree(b->d_scratch);
   (void)hipFree(b->d_gpose);
   (void)hipFree(b->d_cbuf);
@@ -814,7 +842,7 @@ int sim_step(sim_batch* b, const sim_state* s, const float* action, int frame_sk
       if (np > 0) {
         prof_mark(b, 1, st);
         hipLaunchKernelGGL(k_collide, dim3((b->n + 255) / 256, np), dim3(256), 0, st, b->d_model, b->n,
-                           b->d_gpose, b->d_cbuf, b->d_ccount, b->d_pmask);
+                           b->d_gpose, b->d_cbuf, b->d_ccount, b->d_pmask, nullptr);
         prof_mark(b, -1, st);
       }
       const bool last = sub == frame_skip - 1;
@@ -867,10 +895,36 @@ int sim_contacts(sim_batch* b, const sim_state* s, float* out, int32_t* ncon, vo
   });
   if (np > 0)
     hipLaunchKernelGGL(k_collide, dim3((b->n + 255) / 256, np), dim3(256), 0, st, b->d_model, b->n,
-                       b->d_gpose, b->d_cbuf, b->d_ccount, b->d_pmask);
+                       b->d_gpose, b->d_cbuf, b->d_ccount, b->d_pmask, nullptr);
   hipLaunchKernelGGL(k_gather, grid_for(b->n), dim3(64), 0, st, b->d_model, b->n, b->d_cbuf, b->d_ccount, b->d_pmask,
                      out, ncon);
   HIPCHECK(hipGetLastError());
+  return SIM_OK;
+}
+
+int sim_collide_profile(sim_batch* b, const sim_state* s, double* cycles, void* stream) {
+  if (int rc = check_state(b, s)) return rc;
+  if (!cycles) return fail(SIM_E_ARG, "null output");
+  if (b->model->desc.disable_contact) return fail(SIM_E_ARG, "model compiled with contacts disabled");
+  hipStream_t st = (hipStream_t)stream;
+  const int np = b->model->desc.npair;
+  if (np <= 0) return SIM_OK;
+  unsigned long long* d_cyc = nullptr;
+  HIPCHECK(hipMalloc(&d_cyc, np * sizeof(unsigned long long)));
+  HIPCHECK(hipMemsetAsync(d_cyc, 0, np * sizeof(unsigned long long), st));
+  dispatch_nf(b->model->nf, [&](auto nfc) {
+    constexpr int NA = 6, NF = decltype(nfc)::value;
+    hipLaunchKernelGGL((k_geom<NA, NF>), grid_for(b->n), dim3(64), 0, st, b->d_model, b->n, *s,
+                       b->d_gpose);
+  });
+  hipLaunchKernelGGL(k_collide, dim3((b->n + 255) / 256, np), dim3(256), 0, st, b->d_model, b->n,
+                     b->d_gpose, b->d_cbuf, b->d_ccount, b->d_pmask, d_cyc);
+  HIPCHECK(hipMemsetAsync(b->d_pmask, 0, (size_t)((np + 31) / 32) * b->n * sizeof(uint32_t), st));
+  std::vector<unsigned long long> h(np);
+  HIPCHECK(hipMemcpyAsync(h.data(), d_cyc, np * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipStreamSynchronize(st));
+  HIPCHECK(hipFree(d_cyc));
+  for (int p = 0; p < np; p++) cycles[p] = (double)h[p];
   return SIM_OK;
 }
 

@@ -176,6 +176,13 @@ class BatchSim:
                                                   self._stream()))
         return out, nc
 
+    def collide_profile(self):
+        """Per candidate pair, summed wave cycles of one collide pass (numpy [npair])."""
+        cyc = np.zeros(max(self.cm.desc.npair, 1), dtype=np.float64)
+        abi.check(self.lib, self.lib.sim_collide_profile(self._batch, C.byref(self._state),
+                                                         cyc.ctypes.data, self._stream()))
+        return cyc[:self.cm.desc.npair]
+
     def ik(self, target, q=None, tol=1e-6, regularization_threshold=0.1, regularization_strength=1e-2,
            max_update_norm=2.0, progress_thresh=20.0, max_steps=100, ndof=5):
         """Batched position-only DLS IK of the observed site.  target [n, 3];

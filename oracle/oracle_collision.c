@@ -28,6 +28,11 @@
 
 /* algorithmic flop counter for collision work (SURVEY.md §8d binding procedure) */
 static __thread double g_cflops;
+/* collision statistics (diagnostic): [0] pairs tested, [1] midphase passes,
+   [2] MPR calls, [3] MPR hits, [4] support calls, [5] hull climb steps, [6] box-box, [7] plane */
+static double g_cstat[8];
+static double g_pstat[SIM_MAXPAIR][2]; /* per pair: midphase passes, support calls */
+static __thread int g_curpair = -1;
 
 static double dot3(const double a[3], const double b[3]) {
   return a[0] * b[0] + a[1] * b[1] + a[2] * b[2];
@@ -73,7 +78,7 @@ static void geom_center(const orc_model* om, const orc_data* d, int g, double c[
 }
 
 /* Support vertex of a mesh geom's hull for a LOCAL direction: steepest-ascent
-   hill climbing over the hull's vertex graph from vertex 0 (on a convex hull a
+   hill climbing over the hull's vertex graph from the best precomputed seed (on a convex hull a
    local maximum of a linear function is global).  With graph == NULL this is
    the brute-force argmax used to test the climber. */
 int orc_hull_support_ex(const orc_model* om, int g, const double l[3], int use_graph) {
@@ -110,9 +115,12 @@ int orc_hull_support_ex(const orc_model* om, int g, const double l[3], int use_g
     }
     g_cflops += 5.0 * ORC_NSEED;
   }
+  g_cstat[4] += 1;
+  if (g_curpair >= 0) g_pstat[g_curpair][1] += 1;
   for (int guard = 0; guard < nvert; guard++) {
     int nxt = cur;
     double nd = cd;
+    g_cstat[5] += 1;
     g_cflops += 5.0 * (adr[cur + 1] - adr[cur]);
     for (int a = adr[cur]; a < adr[cur + 1]; a++) {
       int u = om->hull_adj[a];
@@ -659,6 +667,7 @@ int orc_collide_pair(const orc_model* om, const orc_data* d, int g1, int g2, orc
   const sim_model_desc* m = om->m;
   int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
   if (maxout <= 0) return 0;
+  g_cstat[0] += 1;
   /* bounding-sphere midphase (planes have rbound 0 and skip it) */
   if (m->geom_rbound[g1] > 0 && m->geom_rbound[g2] > 0) {
     double a[3], b[3], r[3];
@@ -677,19 +686,57 @@ int orc_collide_pair(const orc_model* om, const orc_data* d, int g1, int g2, orc
     }
   }
   g_cflops += 60; /* midphase sphere + AABB */
+  g_cstat[1] += 1;
+  if (g_curpair >= 0) g_pstat[g_curpair][0] += 1;
   if (t1 == SIM_GEOM_PLANE) {
+    /* bounding sphere of geom2 entirely above the plane (beyond the margin): no contact */
+    if (m->geom_rbound[g2] > 0) {
+      double c[3], h = 0;
+      const double* R = d->geom_xmat[g1];
+      geom_center(om, d, g2, c);
+      for (int k = 0; k < 3; k++) h += (c[k] - d->geom_xpos[g1][k]) * R[3 * k + 2];
+      double mg = m->geom_margin[g1] > m->geom_margin[g2] ? m->geom_margin[g1] : m->geom_margin[g2];
+      if (h > m->geom_rbound[g2] + mg) return 0;
+    }
+    g_cstat[7] += 1;
     g_cflops += 150;
     if (t2 == SIM_GEOM_BOX) return plane_box(om, d, g1, g2, out, maxout);
     if (t2 == SIM_GEOM_MESH) return plane_convex(om, d, g1, g2, out);
     return 0;
   }
   if (t1 == SIM_GEOM_BOX && t2 == SIM_GEOM_BOX) {
+    g_cstat[6] += 1;
     g_cflops += 700; /* 15-axis SAT + face clipping */
     return box_box(om, d, g1, g2, out, maxout);
   }
+  if (t1 == SIM_GEOM_BOX && t2 == SIM_GEOM_MESH) {
+    /* separating-axis pre-test on the box face that faces the hull's centre most:
+       the hull's extreme point toward the box beyond that face -> apart (exact) */
+    double c[3], r[3], best = -1e300, ax[3] = {0, 0, 1}, h = 0;
+    const double* R = d->geom_xmat[g1];
+    geom_center(om, d, g2, c);
+    sub3(r, c, d->geom_xpos[g1]);
+    for (int k = 0; k < 3; k++) {
+      double a[3] = {R[k], R[3 + k], R[6 + k]};
+      double dk = dot3(r, a), gap = fabs(dk) - m->geom_size[g1][k];
+      if (gap > best) {
+        double sg = dk >= 0 ? 1 : -1;
+        best = gap, h = m->geom_size[g1][k];
+        for (int q = 0; q < 3; q++) ax[q] = sg * a[q];
+      }
+    }
+    double nd[3] = {-ax[0], -ax[1], -ax[2]}, sp[3], dist = -h;
+    support(om, d, g2, nd, sp);
+    for (int q = 0; q < 3; q++) dist += (sp[q] - d->geom_xpos[g1][q]) * ax[q];
+    g_cflops += 60 + 36 + 10;
+    double mg = m->geom_margin[g1] > m->geom_margin[g2] ? m->geom_margin[g1] : m->geom_margin[g2];
+    if (dist > mg) return 0;
+  }
   mpair P = {om, d, g1, g2};
   double depth, dir[3], pos[3];
+  g_cstat[2] += 1;
   if (!mpr_penetration(&P, &depth, dir, pos)) return 0;
+  g_cstat[3] += 1;
   out->dist = -depth;
   memcpy(out->pos, pos, sizeof(pos));
   memcpy(out->frame, dir, sizeof(dir));
@@ -704,7 +751,9 @@ void orc_collision(const orc_model* om, orc_data* d) {
   for (int p = 0; p < m->npair; p++) {
     int g1 = m->pair_geom1[p], g2 = m->pair_geom2[p];
     orc_contact tmp[8];
+    g_curpair = p;
     int n = orc_collide_pair(om, d, g1, g2, tmp, 8);
+    g_curpair = -1;
     for (int i = 0; i < n; i++) {
       if (d->ncon >= SIM_MAXCON) {
         d->status |= SIM_ST_CONOVERFLOW;
@@ -759,4 +808,17 @@ int orc_hull_support_flat(const sim_model_desc* m, const float* hv, const int32_
   orc_model om = {m, hv, hadr, hadj, hv ? seeds : NULL, 1.0, -1.0, 1.0};
   for (int i = 0; i < n; i++) out[i] = orc_hull_support_ex(&om, g, dirs + 3 * i, use_graph);
   return 0;
+}
+
+/* diagnostic counters (single-threaded use) */
+void orc_collision_stats(double* out, int reset) {
+  for (int k = 0; k < 8; k++) {
+    out[k] = g_cstat[k];
+    if (reset) g_cstat[k] = 0;
+  }
+  for (int p = 0; p < SIM_MAXPAIR; p++)
+    for (int k = 0; k < 2; k++) {
+      out[8 + 2 * p + k] = g_pstat[p][k];
+      if (reset) g_pstat[p][k] = 0;
+    }
 }
