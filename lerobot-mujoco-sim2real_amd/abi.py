@@ -106,7 +106,7 @@ LIB_PATH = os.path.join(PKG_DIR, "csrc", "libsoarm_sim.so")
 EXPORTS = [
     "sim_last_error", "sim_version", "sim_model_create", "sim_model_free",
     "sim_batch_create", "sim_batch_free", "sim_batch_set_params", "sim_reset",
-    "sim_step", "sim_substeps", "sim_observe", "sim_contacts", "sim_collide_profile", "sim_ik_dls",
+    "sim_step", "sim_substeps", "sim_observe", "sim_contacts", "sim_collide_profile", "sim_phase_profile", "sim_ik_dls",
     "sim_profile_begin", "sim_profile_end",
 ]
 PROF_KINDS = ["step_fused", "collide", "substep", "geom"]
@@ -140,6 +140,7 @@ def load_lib(path=None):
     lib.sim_observe.argtypes = [vp, C.POINTER(SimState), vp, vp]
     lib.sim_contacts.argtypes = [vp, C.POINTER(SimState), vp, vp, vp]
     lib.sim_collide_profile.argtypes = [vp, C.POINTER(SimState), vp, vp]
+    lib.sim_phase_profile.argtypes = [vp, ip]
     lib.sim_profile_begin.argtypes = [vp]
     lib.sim_profile_end.argtypes = [vp, vp, vp]
     lib.sim_ik_dls.argtypes = [vp, vp, vp, vp, vp, C.POINTER(IkOpts), vp]

@@ -30,20 +30,25 @@
 
 namespace soarm {
 
+#ifdef SOARM_PHASE_PROF
+// diagnostic build only: per-env PGS start/end clock, sweep count, fast-path flag (env < 65536)
+__device__ long long g_pgs_prof[65536 * 6];
+#endif
+
 constexpr int LDS_CON = 8;  // contacts whose rows stay in LDS
-constexpr int CF = 67;      // LDS floats per contact record
+constexpr int CF = 61;      // LDS floats per contact record
 // record fields: [0, 3*12) J_n | J_t1 | J_t2 (12 slots each), 36..39 aref_e,
 // 40..43 ARdiag_e / 2, 44..47 force_e, 48..51 1/ARdiag_e, 52 mu, 53 R (pyramid),
-// 54 flags, 55..66 per edge e the Gram column (J_n, J_t1, J_t2) . M^-1 J_e'
-// (cube-only contacts: the free body's diagonal M^-1)
-enum { F_AREF = 36, F_HARD = 40, F_FRC = 44, F_IARD = 48, F_MU = 52, F_R = 53, F_FLAGS = 54, F_COEF = 55 };
+// 54 flags, 55..60 Gram matrix G = [J_n; J_t1; J_t2] M^-1 [..]' (nn, n1, n2, 11, 12, 22)
+// of a contact that touches only the free body (diagonal M^-1)
+enum { F_AREF = 36, F_HARD = 40, F_FRC = 44, F_IARD = 48, F_MU = 52, F_R = 53, F_FLAGS = 54, F_GRAM = 55 };
 enum { TOUCH_ARM = 1, TOUCH_FREE = 2 };
 // joint-limit rows (rare): compact list, one record per active limit
 constexpr int LF = 7;  // dof, sign, aref, R, ARdiag, 1/ARdiag, force
 enum { L_DOF = 0, L_SGN = 1, L_AREF = 2, L_R = 3, L_ARD = 4, L_IARD = 5, L_FRC = 6 };
 
 struct RowLds {
-  float (*a)[64];    // [LDS_CON * CF][64] contact records (null: contact-free kernel)
+  float (*a)[64];    // [(LDS_CON + 1) * CF][64] contact records + a zero record (null: contact-free kernel)
   float (*lim)[64];  // [NA * LF][64] active joint-limit records
   int lane;
   DEVI float& at(int c, int f) const { return a[c * CF + f][lane]; }
@@ -157,6 +162,54 @@ DEVI void add_arm_col(const MInv<NA, NF>& Mi, float* v, const float* oh, float s
     for (int j = 0; j < NA; j++) a = fmaf(oh[j], Mi.a(k, j), a);
     v[k] = fmaf(a, sgf, v[k]);
   }
+}
+
+// Per edge e of a contact, the column of its Gram matrix for J_e = J_n + s J_tk
+// (s = +-mu): how (J_n v, J_t1 v, J_t2 v) move per unit force on edge e.
+DEVI void gram_coefs(const float G[6], float mu, float cf[12]) {
+#pragma unroll
+  for (int ed = 0; ed < 4; ed++) {
+    const float s = (ed & 1) ? -mu : mu;
+    const bool k2 = ed >> 1;
+    cf[3 * ed + 0] = G[0] + s * (k2 ? G[2] : G[1]);
+    cf[3 * ed + 1] = G[1] + s * (k2 ? G[4] : G[3]);
+    cf[3 * ed + 2] = G[2] + s * (k2 ? G[5] : G[4]);
+  }
+}
+
+// One Gauss-Seidel pass over the 4 pyramid edges of a free-body-only contact in
+// Gram form: a, b, c = J_n v, J_t1 v, J_t2 v; each edge's residual is a + s b
+// (or c) - aref + R f; its force step moves (a, b, c) by the Gram column; the
+// free body's velocity block v6 is updated once at the end.  Same sequence as
+// updating v after every edge.
+DEVI void gram_step(float* v6, const float* jn, const float* j1, const float* j2, const float* cf,
+                    const float* ar, const float* ia, const float* hd, float* fo, float mu, float Rp,
+                    const float* Fd, float& improvement) {
+  float a = 0.f, b = 0.f, cc = 0.f;
+#pragma unroll
+  for (int i = 0; i < 6; i++) {
+    a += jn[i] * v6[i];
+    b += j1[i] * v6[i];
+    cc += j2[i] * v6[i];
+  }
+  float df[4];
+#pragma unroll
+  for (int ed = 0; ed < 4; ed++) {
+    const float s = (ed & 1) ? -mu : mu;
+    const float res = (a + s * ((ed >> 1) ? cc : b)) - ar[ed] + Rp * fo[ed];
+    const float fnew = fmaxf(fo[ed] - res * ia[ed], 0.f);
+    df[ed] = fnew - fo[ed];
+    a += cf[3 * ed] * df[ed];
+    b += cf[3 * ed + 1] * df[ed];
+    cc += cf[3 * ed + 2] * df[ed];
+    improvement -= df[ed] * (res + hd[ed] * df[ed]);
+    fo[ed] = fnew;
+  }
+  // sum_e J_e df_e = J_n (df0+df1+df2+df3) + mu J_t1 (df0-df1) + mu J_t2 (df2-df3)
+  const float Dn = (df[0] + df[1]) + (df[2] + df[3]);
+  const float D1 = mu * (df[0] - df[1]), D2 = mu * (df[2] - df[3]);
+#pragma unroll
+  for (int i = 0; i < 6; i++) v6[i] += Fd[i] * (jn[i] * Dn + j1[i] * D1 + j2[i] * D2);
 }
 
 // Builds every constraint row, solves the dual by PGS, sets S.qacc / S.fcon.
@@ -293,24 +346,17 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
               L.at(ncon, F_MU) = mu;
               L.at(ncon, F_R) = Rpy;
               L.at(ncon, F_FLAGS) = (float)flags;
-              if constexpr (NF == 1) {
-                if (!ta) {  // Gram form of a free-body-only contact: G = [Jn;Jt1;Jt2] Fd [Jn;Jt1;Jt2]'
-                  float G[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                  for (int i = 0; i < 6; i++) {
-                    const float w = S_FD(Mi, i), x = jd[0][NA + i], y = jd[1][NA + i], z = jd[2][NA + i];
-                    G[0] += w * x * x, G[1] += w * x * y, G[2] += w * x * z;
-                    G[3] += w * y * y, G[4] += w * y * z, G[5] += w * z * z;
-                  }
-#pragma unroll
-                  for (int ed = 0; ed < 4; ed++) {  // column of G for J_e = J_n + s J_tk
-                    const float s = (ed & 1) ? -mu : mu;
-                    const bool k2 = ed >> 1;
-                    L.at(ncon, F_COEF + 3 * ed + 0) = G[0] + s * (k2 ? G[2] : G[1]);
-                    L.at(ncon, F_COEF + 3 * ed + 1) = G[1] + s * (k2 ? G[4] : G[3]);
-                    L.at(ncon, F_COEF + 3 * ed + 2) = G[2] + s * (k2 ? G[5] : G[4]);
-                  }
-                }
+              {  // Gram matrix G = [Jn; Jt1; Jt2] M^-1 [Jn; Jt1; Jt2]'
+                float W0[NV], W1[NV], W2[NV];
+                Mi.mul(jd[0], W0, ta, tf);
+                Mi.mul(jd[1], W1, ta, tf);
+                Mi.mul(jd[2], W2, ta, tf);
+                L.at(ncon, F_GRAM + 0) = dotv<NA, NF>(jd[0], W0, ta, tf);
+                L.at(ncon, F_GRAM + 1) = dotv<NA, NF>(jd[0], W1, ta, tf);
+                L.at(ncon, F_GRAM + 2) = dotv<NA, NF>(jd[0], W2, ta, tf);
+                L.at(ncon, F_GRAM + 3) = dotv<NA, NF>(jd[1], W1, ta, tf);
+                L.at(ncon, F_GRAM + 4) = dotv<NA, NF>(jd[1], W2, ta, tf);
+                L.at(ncon, F_GRAM + 5) = dotv<NA, NF>(jd[2], W2, ta, tf);
               }
             }
 #pragma unroll
@@ -463,8 +509,12 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
 #pragma unroll
     for (int i = 0; i < 6; i++) tr += S.MF[f2][i * (i + 1) / 2 + i];
   const float scale = 1.f / tr;
-  for (int it = 0; it < m.iterations; it++) {
-    float improvement = 0.f;
+#ifdef SOARM_PHASE_PROF
+  if (e < 65536) g_pgs_prof[6 * e] = clock64();
+  int nsweep = m.iterations;
+#endif
+  // dof-frictionloss rows (J = e_i): one pass
+  auto fric_rows = [&](float& improvement) {
 #pragma unroll
     for (int i = 0; i < NA; i++) {
       const float fl = m.dof_frictionloss[i];
@@ -477,6 +527,9 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       ff[i] = fn;
       improvement -= df * (res + fhD[i] * df);
     }
+  };
+  // active joint-limit rows (LDS list; usually empty)
+  auto limit_rows = [&](float& improvement) {
     for (int l = 0; l < nlim; l++) {
       float oh[NA];
       one_hot<NA>((int)L.lm(l, L_DOF), oh);
@@ -488,86 +541,67 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       L.lm(l, L_FRC) = fn;
       improvement -= df * (res + 0.5f * L.lm(l, L_ARD) * df);
     }
-    for (int c = 0; c < nl; c++) {
-      const int fl = (int)L.at(c, F_FLAGS);
-      const bool ta = fl & TOUCH_ARM, tf = fl & TOUCH_FREE;
-      if constexpr (NF == 1) {
-        // Gram path, wave-uniform: no active lane's contact c touches the arm (cube on the
-        // table).  a, b, c = J_n v, J_t1 v, J_t2 v; each edge's residual is a + s b (or c),
-        // and its force step moves (a, b, c) by the stored Gram column; v itself is
-        // updated once per contact.
-        if (__all(!ta)) {
-          float jn[6], j1[6], j2[6], fo[4], ar[4], ia[4], hd[4], cf[12];
+  };
+  // contact c from its LDS record, in Gram form: a 6-dof free-body update when
+  // (wave-uniformly) it touches only the free body, otherwise full-width dots and one
+  // M^-1 product per sweep for the velocity update
+  auto lds_contact = [&](int c, float& improvement) {
+    const bool ta = (int)L.at(c, F_FLAGS) & TOUCH_ARM;
+    float G[6], cf[12], fo[4], ar[4], ia[4], hd[4];
 #pragma unroll
-          for (int i = 0; i < 6; i++)
-            jn[i] = L.at(c, NA + i), j1[i] = L.at(c, 12 + NA + i), j2[i] = L.at(c, 24 + NA + i);
+    for (int ed = 0; ed < 4; ed++)
+      fo[ed] = L.at(c, F_FRC + ed), ar[ed] = L.at(c, F_AREF + ed), ia[ed] = L.at(c, F_IARD + ed),
+      hd[ed] = L.at(c, F_HARD + ed);
 #pragma unroll
-          for (int ed = 0; ed < 4; ed++)
-            fo[ed] = L.at(c, F_FRC + ed), ar[ed] = L.at(c, F_AREF + ed), ia[ed] = L.at(c, F_IARD + ed),
-            hd[ed] = L.at(c, F_HARD + ed);
+    for (int k = 0; k < 6; k++) G[k] = L.at(c, F_GRAM + k);
+    const float mu = L.at(c, F_MU), Rp = L.at(c, F_R);
+    gram_coefs(G, mu, cf);
+    if constexpr (NF == 1) {
+      if (__all(!ta)) {
+        float jn[6], j1[6], j2[6];
 #pragma unroll
-          for (int k = 0; k < 12; k++) cf[k] = L.at(c, F_COEF + k);
-          const float mu = L.at(c, F_MU), Rp = L.at(c, F_R);
-          float a = 0.f, b = 0.f, cc = 0.f;
+        for (int i = 0; i < 6; i++)
+          jn[i] = L.at(c, NA + i), j1[i] = L.at(c, 12 + NA + i), j2[i] = L.at(c, 24 + NA + i);
+        gram_step(v + NA, jn, j1, j2, cf, ar, ia, hd, fo, mu, Rp, Mi.Fd[0], improvement);
 #pragma unroll
-          for (int i = 0; i < 6; i++) {
-            a += jn[i] * v[NA + i];
-            b += j1[i] * v[NA + i];
-            cc += j2[i] * v[NA + i];
-          }
-          float df[4];
-#pragma unroll
-          for (int ed = 0; ed < 4; ed++) {
-            const float s = (ed & 1) ? -mu : mu;
-            const float res = (a + s * ((ed >> 1) ? cc : b)) - ar[ed] + Rp * fo[ed];
-            const float fnew = fmaxf(fo[ed] - res * ia[ed], 0.f);
-            df[ed] = fnew - fo[ed];
-            a += cf[3 * ed] * df[ed];
-            b += cf[3 * ed + 1] * df[ed];
-            cc += cf[3 * ed + 2] * df[ed];
-            improvement -= df[ed] * (res + hd[ed] * df[ed]);
-            fo[ed] = fnew;
-          }
-          // sum_e J_e df_e = J_n (df0+df1+df2+df3) + mu J_t1 (df0-df1) + mu J_t2 (df2-df3)
-          const float Dn = (df[0] + df[1]) + (df[2] + df[3]);
-          const float D1 = mu * (df[0] - df[1]), D2 = mu * (df[2] - df[3]);
-#pragma unroll
-          for (int i = 0; i < 6; i++) v[NA + i] += S_FD(Mi, i) * (jn[i] * Dn + j1[i] * D1 + j2[i] * D2);
-#pragma unroll
-          for (int ed = 0; ed < 4; ed++) L.at(c, F_FRC + ed) = fo[ed];
-          continue;
-        }
-      }
-      float jn[NV], jt1[NV], jt2[NV];
-#pragma unroll
-      for (int i = 0; i < NV; i++) jn[i] = jt1[i] = jt2[i] = 0.f;
-      if (ta) {
-#pragma unroll
-        for (int i = 0; i < NA; i++) jn[i] = L.at(c, i), jt1[i] = L.at(c, 12 + i), jt2[i] = L.at(c, 24 + i);
-      }
-      if (tf) {
-#pragma unroll
-        for (int i = NA; i < NV; i++) jn[i] = L.at(c, i), jt1[i] = L.at(c, 12 + i), jt2[i] = L.at(c, 24 + i);
-      }
-      const float mu = L.at(c, F_MU), Rp = L.at(c, F_R);
-#pragma unroll
-      for (int ed = 0; ed < 4; ed++) {
-        float J[NV];
-        edge_J<NV>(jn, jt1, jt2, ed, mu, J);
-        const float fo = L.at(c, F_FRC + ed);
-        const float res = dotv<NA, NF>(J, v, ta, tf) - L.at(c, F_AREF + ed) + Rp * fo;
-        const float fnew = fmaxf(fo - res * L.at(c, F_IARD + ed), 0.f);
-        const float df = fnew - fo;
-        if (df != 0.f) {
-          float W[NV];
-          Mi.mul(J, W, ta, tf);
-#pragma unroll
-          for (int i = 0; i < NV; i++) v[i] += W[i] * df;
-          L.at(c, F_FRC + ed) = fnew;
-          improvement -= df * (res + L.at(c, F_HARD + ed) * df);
-        }
+        for (int ed = 0; ed < 4; ed++) L.at(c, F_FRC + ed) = fo[ed];
+        return;
       }
     }
+    // the record holds zeros in the halves the contact does not touch: full-width,
+    // branch-free dots (divergent half-selection would run both sides anyway)
+    float jn[NV], j1[NV], j2[NV];
+#pragma unroll
+    for (int i = 0; i < NV; i++) jn[i] = L.at(c, i), j1[i] = L.at(c, 12 + i), j2[i] = L.at(c, 24 + i);
+    float a = 0.f, b = 0.f, cc = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; i++) a += jn[i] * v[i], b += j1[i] * v[i], cc += j2[i] * v[i];
+    float df[4];
+#pragma unroll
+    for (int ed = 0; ed < 4; ed++) {
+      const float s = (ed & 1) ? -mu : mu;
+      const float res = (a + s * ((ed >> 1) ? cc : b)) - ar[ed] + Rp * fo[ed];
+      const float fnew = fmaxf(fo[ed] - res * ia[ed], 0.f);
+      df[ed] = fnew - fo[ed];
+      a += cf[3 * ed] * df[ed];
+      b += cf[3 * ed + 1] * df[ed];
+      cc += cf[3 * ed + 2] * df[ed];
+      improvement -= df[ed] * (res + hd[ed] * df[ed]);
+      fo[ed] = fnew;
+    }
+    const float Dn = (df[0] + df[1]) + (df[2] + df[3]);
+    const float D1 = mu * (df[0] - df[1]), D2 = mu * (df[2] - df[3]);
+    float u[NV], w[NV];
+#pragma unroll
+    for (int i = 0; i < NV; i++) u[i] = jn[i] * Dn + j1[i] * D1 + j2[i] * D2;
+    Mi.mul(u, w, true, true);
+#pragma unroll
+    for (int i = 0; i < NV; i++) v[i] += w[i];
+#pragma unroll
+    for (int ed = 0; ed < 4; ed++) L.at(c, F_FRC + ed) = fo[ed];
+  };
+  // contacts beyond LDS_CON: per-edge J/W rows in global scratch (rare)
+  auto scratch_rows = [&](float& improvement) {
     for (int r = 4 * nl; r < 4 * ncon; r++) {
       float res = -cr.S(r, 0) + cr.S(r, 1) * cr.S(r, 3);
 #pragma unroll
@@ -582,8 +616,91 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
         improvement -= df * res + 0.5f * cr.S(r, 2) * df * df;
       }
     }
-    if (improvement * scale < m.tolerance) break;
+  };
+
+  // Register block: the first run of up to FC consecutive contacts that touch only
+  // the free body (the cube's box-box contacts with the table) keeps all its row data
+  // in registers for the whole solve, so the common sweep is straight-line code in
+  // which the arm's friction chain and the cube's contact chain (independent: M is
+  // block diagonal) interleave.  Contacts before / after the run go through their
+  // LDS records in row order.  Slots beyond the run are zero rows (1/ARdiag = 0).
+  constexpr int FC = (NF == 1 && CON) ? 4 : 1;
+  int c0 = nl, nrun = 0;
+  if constexpr (NF == 1 && CON) {
+    for (int c = 0; c < nl; c++)
+      if ((int)L.at(c, F_FLAGS) == TOUCH_FREE) {
+        c0 = c;
+        break;
+      }
+    while (nrun < FC && c0 + nrun < nl && (int)L.at(c0 + nrun, F_FLAGS) == TOUCH_FREE) nrun++;
   }
+  // registers: the block's forces (updated every sweep); everything else is re-read
+  // from LDS each sweep — those loads are independent of the Gauss-Seidel chains, so in
+  // straight-line code they issue ahead of use
+  float cfo[FC][4];
+  int cslot[FC];
+  if constexpr (NF == 1 && CON) {
+#pragma unroll
+    for (int i = 0; i < 6; i++)  // the zero record: Jacobian, Gram, 1/ARdiag, ARdiag/2, aref, mu, R
+      L.at(LDS_CON, NA + i) = L.at(LDS_CON, 12 + NA + i) = L.at(LDS_CON, 24 + NA + i) = L.at(LDS_CON, F_GRAM + i) = 0.f;
+#pragma unroll
+    for (int ed = 0; ed < 4; ed++)
+      L.at(LDS_CON, F_IARD + ed) = L.at(LDS_CON, F_HARD + ed) = L.at(LDS_CON, F_AREF + ed) = 0.f;
+    L.at(LDS_CON, F_MU) = L.at(LDS_CON, F_R) = 0.f;
+#pragma unroll
+    for (int k = 0; k < FC; k++) {
+      const bool on = k < nrun;
+      cslot[k] = on ? c0 + k : LDS_CON;
+#pragma unroll
+      for (int ed = 0; ed < 4; ed++) cfo[k][ed] = on ? L.at(c0 + k, F_FRC + ed) : 0.f;
+    }
+  }
+  const int c1 = c0 + nrun;
+  for (int it = 0; it < m.iterations; it++) {
+    float improvement = 0.f;
+    fric_rows(improvement);
+    limit_rows(improvement);
+    // contacts in row order: [0, c0) from LDS, the register block for [c0, c1), then
+    // [c1, nl) from LDS (lanes with different c0 / c1 are masked in the two loops; the
+    // block runs once per sweep for the whole wave)
+    for (int c = 0; c < c0; c++) lds_contact(c, improvement);
+    if constexpr (NF == 1 && CON) {
+#pragma unroll
+      for (int k = 0; k < FC; k++) {
+        const int c = cslot[k];
+        float jn[6], j1[6], j2[6], G[6], cf[12], ar[4], ia[4], hd[4];
+#pragma unroll
+        for (int i = 0; i < 6; i++)
+          jn[i] = L.at(c, NA + i), j1[i] = L.at(c, 12 + NA + i), j2[i] = L.at(c, 24 + NA + i), G[i] = L.at(c, F_GRAM + i);
+#pragma unroll
+        for (int ed = 0; ed < 4; ed++)
+          ar[ed] = L.at(c, F_AREF + ed), ia[ed] = L.at(c, F_IARD + ed), hd[ed] = L.at(c, F_HARD + ed);
+        const float mu = L.at(c, F_MU), Rp = L.at(c, F_R);
+        gram_coefs(G, mu, cf);
+        gram_step(v + NA, jn, j1, j2, cf, ar, ia, hd, cfo[k], mu, Rp, Mi.Fd[0], improvement);
+      }
+    }
+    for (int c = c1; c < nl; c++) lds_contact(c, improvement);
+    scratch_rows(improvement);
+    if (improvement * scale < m.tolerance) {
+#ifdef SOARM_PHASE_PROF
+      nsweep = it + 1;
+#endif
+      break;
+    }
+  }
+  if constexpr (NF == 1 && CON) {
+#pragma unroll
+    for (int k = 0; k < FC; k++)
+      if (k < nrun)
+#pragma unroll
+        for (int ed = 0; ed < 4; ed++) L.at(c0 + k, F_FRC + ed) = cfo[k][ed];
+  }
+#ifdef SOARM_PHASE_PROF
+  if (e < 65536)
+    g_pgs_prof[6 * e + 1] = clock64(), g_pgs_prof[6 * e + 2] = nsweep,
+    g_pgs_prof[6 * e + 3] = (nrun == ncon && nlim == 0), g_pgs_prof[6 * e + 4] = nlim, g_pgs_prof[6 * e + 5] = ncon;
+#endif
 
   // ---- qacc and qfrc_constraint = J' f
 #pragma unroll

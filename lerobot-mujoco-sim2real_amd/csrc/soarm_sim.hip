@@ -133,6 +133,21 @@ DEVI void write_obs(const Sim<NA, NF>& S, float* obs, int e) {
   }
 }
 
+#ifdef SOARM_PHASE_PROF
+// diagnostic build: summed wave cycles per k_substep phase
+//   [0] state load + checks, [1] kinematics..smooth forces, [2] constraint rows,
+//   [3] PGS sweeps, [4] qacc/fcon + Euler + obs + geom poses, [5] waves,
+//   [6] sum over envs of PGS sweeps, [7] env count, [8] max wave cycles,
+//   [9] waves on the register fast path, [10] max wave PGS cycles,
+//   [11] sum over waves of the wave's max sweep count, [12] waves with an active
+//   joint limit, [13] waves with a contact outside the register block, [14] waves
+//   with more than LDS_CON contacts, [15] max contacts of an env
+__device__ unsigned long long g_phase[16];
+#define PHASE_T(v) const long long v = clock64()
+#else
+#define PHASE_T(v)
+#endif
+
 // one mj_forward (position + velocity + acceleration stages); the contacts
 // (cbuf/ccount, may be null) were produced by k_collide from this substep's positions
 template <int NA, int NF, bool CON>
@@ -254,6 +269,7 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
                                                 float* __restrict__ gpose) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
+  PHASE_T(t0);
   const DModel& m = *dm;
   Sim<NA, NF> S(dm, pp.mass_scale ? pp.mass_scale[e] : 1.f, pp.friction ? pp.friction[e] : -1.f,
                 pp.damping_scale ? pp.damping_scale[e] : 1.f);
@@ -263,7 +279,7 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
     for (int k = 0; k < NA; k++)
       if (k < m.nact) S.ctrl[k] = action[(size_t)e * m.nact + k];
   }
-  __shared__ float s_rows[LDS_CON * CF][64];
+  __shared__ float s_rows[(LDS_CON + 1) * CF][64];  // + one all-zero record
   __shared__ float s_lim[NA * LF][64];
   const RowLds L{s_rows, s_lim, (int)threadIdx.x};
   const ContactRows<NA, NF> cr{scratch + e, n};
@@ -271,7 +287,17 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
   S.check_state();
   // a soft reset moved the env: the collide output no longer applies
   const bool use = S.status == st0 && ccount != nullptr;
+#ifdef SOARM_PHASE_PROF
+  PHASE_T(t1);
+  S.kinematics();
+  S.com_crb();
+  S.factor();
+  S.smooth_forces();
+  PHASE_T(t2);
+  int ncon = solve_constraints<NA, NF, true>(S, use ? cbuf : nullptr, use ? ccount : nullptr, pmask, n, e, L, cr);
+#else
   int ncon = forward<NA, NF, true>(S, use ? cbuf : nullptr, use ? ccount : nullptr, pmask, n, e, L, cr);
+#endif
   if (S.acc_bad()) {
     S.soft_reset(SIM_ST_BADQACC);
     ncon = forward<NA, NF, true>(S, nullptr, nullptr, nullptr, n, e, L, cr);
@@ -290,6 +316,34 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
     S.kinematics();
     write_geom_poses(S, gpose, n, e);
   }
+#ifdef SOARM_PHASE_PROF
+  PHASE_T(t5);
+  const long long p0 = g_pgs_prof[6 * e], p1 = g_pgs_prof[6 * e + 1];
+  const int nsw = (int)g_pgs_prof[6 * e + 2];
+  const bool anylim = __any(g_pgs_prof[6 * e + 4] > 0), anyslow = __any(g_pgs_prof[6 * e + 3] == 0),
+             anyovf = __any(g_pgs_prof[6 * e + 5] > LDS_CON);
+  atomicMax(&g_phase[15], (unsigned long long)g_pgs_prof[6 * e + 5]);
+  atomicAdd(&g_phase[6], (unsigned long long)nsw);
+  atomicAdd(&g_phase[7], 1ull);
+  int wmax = nsw;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, __shfl_xor(wmax, o));
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(&g_phase[0], (unsigned long long)(t1 - t0));
+    atomicAdd(&g_phase[1], (unsigned long long)(t2 - t1));
+    atomicAdd(&g_phase[2], (unsigned long long)(p0 - t2));
+    atomicAdd(&g_phase[3], (unsigned long long)(p1 - p0));
+    atomicAdd(&g_phase[4], (unsigned long long)(t5 - p1));
+    atomicMax(&g_phase[8], (unsigned long long)(t5 - t0));
+    atomicAdd(&g_phase[9], (unsigned long long)g_pgs_prof[6 * e + 3]);
+    atomicAdd(&g_phase[12], (unsigned long long)anylim);
+    atomicAdd(&g_phase[13], (unsigned long long)anyslow);
+    atomicAdd(&g_phase[14], (unsigned long long)anyovf);
+    atomicMax(&g_phase[10], (unsigned long long)(p1 - p0));
+    atomicAdd(&g_phase[11], (unsigned long long)wmax);
+    atomicAdd(&g_phase[5], 1ull);
+  }
+#endif
 }
 
 // diagnostic: compacted contact list [N][SIM_MAXCON][8] (dist, pos, normal, pair) + count
@@ -926,6 +980,25 @@ int sim_collide_profile(sim_batch* b, const sim_state* s, double* cycles, void* 
   HIPCHECK(hipFree(d_cyc));
   for (int p = 0; p < np; p++) cycles[p] = (double)h[p];
   return SIM_OK;
+}
+
+int sim_phase_profile(double* out, int reset) {
+  if (!out) return fail(SIM_E_ARG, "null output");
+#ifdef SOARM_PHASE_PROF
+  unsigned long long h[16];
+  HIPCHECK(hipDeviceSynchronize());
+  HIPCHECK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_phase), sizeof(h)));
+  for (int k = 0; k < 16; k++) out[k] = (double)h[k];
+  if (reset) {
+    const unsigned long long z[16] = {};
+    HIPCHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof(z)));
+  }
+  return SIM_OK;
+#else
+  (void)reset;
+  for (int k = 0; k < 16; k++) out[k] = 0.0;
+  return SIM_E_ARG;  // not a profiling build
+#endif
 }
 
 int sim_substeps(sim_batch* b, const sim_state* s, int nsub, void* stream) {

@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""Diagnostic: where a contact substep spends its cycles.
+
+Needs the profiling build (tools/phase_prof.py --build compiles
+csrc/soarm_sim.hip with -DSOARM_PHASE_PROF into tools/_prof/); on the GPU it
+runs the bench's contact workload and prints the per-phase share of wave
+cycles and the mean PGS sweep count."""
+import ctypes
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "tools", "_prof", "libsoarm_sim_prof.so")
+SRC = os.path.join(ROOT, "lerobot-mujoco-sim2real_amd", "csrc", "soarm_sim.hip")
+
+if "--build" in sys.argv:
+    os.makedirs(os.path.dirname(LIB), exist_ok=True)
+    subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+                           "-DSOARM_PHASE_PROF", "-o", LIB, SRC])
+    sys.exit(0)
+
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import soarm_pkg  # noqa: E402,F401
+from lerobot_mujoco_sim2real_amd import abi, workloads as W  # noqa: E402
+
+lib = abi.load_lib(LIB)
+abi._lib = lib
+from lerobot_mujoco_sim2real_amd.sim import BatchSim  # noqa: E402
+
+n = int(os.environ.get("ENVS", 4096))
+T = int(sys.argv[1]) if len(sys.argv) > 1 else 120
+cm = W.model("contact")
+ids = np.arange(n)
+sim = BatchSim(cm, n, 0)
+q0 = W.initial_qpos(cm, ids, 0)
+sim.reset(init_qpos=q0[:, :5], extra_qpos=q0, seed=0)
+tab = {k: (torch.as_tensor(v, dtype=torch.float32, device="cuda") if isinstance(v, np.ndarray) else v)
+       for k, v in W.chirp_tables(ids, 0).items()}
+out = (ctypes.c_double * 16)()
+res = {}
+for t in range(T):
+    if t in (0, T // 2, T - 10):
+        torch.cuda.synchronize()
+        lib.sim_phase_profile(ctypes.cast(out, ctypes.c_void_p), 1)
+    sim.step(W.chirp_action(tab, float(t), lib=torch))
+    if t in (9, T // 2 + 9, T - 1):
+        torch.cuda.synchronize()
+        lib.sim_phase_profile(ctypes.cast(out, ctypes.c_void_p), 1)
+        v = list(out)
+        tot = sum(v[:5])
+        names = ["load", "smooth", "rows", "pgs", "integrate+out"]
+        r = {nm: v[i] / tot for i, nm in enumerate(names)}
+        r["cycles_per_wave"] = tot / max(v[5], 1)
+        r["max_wave_cycles"] = v[8]
+        r["fast_wave_frac"] = v[9] / max(v[5], 1)
+        r["max_wave_pgs_cycles"] = v[10]
+        r["mean_sweeps"] = v[6] / max(v[7], 1)
+        r["mean_wave_max_sweeps"] = v[11] / max(v[5], 1)
+        r["waves_with_limit"] = v[12] / max(v[5], 1)
+        r["waves_with_nonblock_contact"] = v[13] / max(v[5], 1)
+        r["waves_with_lds_overflow"] = v[14] / max(v[5], 1)
+        r["max_ncon"] = v[15]
+        res[t] = r
+        print(t, json.dumps(r), flush=True)
+json.dump(res, open(os.path.join(ROOT, "gpurun_out", "phase_prof.json"), "w"), indent=1)
