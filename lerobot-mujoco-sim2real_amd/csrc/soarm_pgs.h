@@ -634,10 +634,10 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       }
     while (nrun < FC && c0 + nrun < nl && (int)L.at(c0 + nrun, F_FLAGS) == TOUCH_FREE) nrun++;
   }
-  // registers: the block's forces (updated every sweep); everything else is re-read
-  // from LDS each sweep — those loads are independent of the Gauss-Seidel chains, so in
-  // straight-line code they issue ahead of use
-  float cfo[FC][4];
+  // registers: the block's forces (updated every sweep) and Gram columns; the rest is
+  // re-read from LDS each sweep — those loads are independent of the Gauss-Seidel
+  // chains, so in straight-line code they issue ahead of use
+  float cfo[FC][4], ccf[FC][12];
   int cslot[FC];
   if constexpr (NF == 1 && CON) {
 #pragma unroll
@@ -653,34 +653,45 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       cslot[k] = on ? c0 + k : LDS_CON;
 #pragma unroll
       for (int ed = 0; ed < 4; ed++) cfo[k][ed] = on ? L.at(c0 + k, F_FRC + ed) : 0.f;
+      float G[6];
+#pragma unroll
+      for (int i = 0; i < 6; i++) G[i] = L.at(cslot[k], F_GRAM + i);
+      gram_coefs(G, L.at(cslot[k], F_MU), ccf[k]);
     }
   }
   const int c1 = c0 + nrun;
+  // Contacts before the block that do not touch the free body commute with the block's
+  // rows (disjoint dofs, block-diagonal M), so they may run after it: then one masked
+  // loop covers every lane's non-block contacts (e.g. an arm-table contact, which
+  // precedes the cube's rows in pair order, in one lane and an arm-cube contact, which
+  // follows them, in another) instead of one loop before and one after the block.
+  int npre = 0;
+  for (int c = 0; c < c0; c++)
+    if ((int)L.at(c, F_FLAGS) & TOUCH_FREE) npre = c0;
+  const int npost = (c0 - npre) + (nl - c1);
   for (int it = 0; it < m.iterations; it++) {
     float improvement = 0.f;
     fric_rows(improvement);
     limit_rows(improvement);
-    // contacts in row order: [0, c0) from LDS, the register block for [c0, c1), then
-    // [c1, nl) from LDS (lanes with different c0 / c1 are masked in the two loops; the
-    // block runs once per sweep for the whole wave)
-    for (int c = 0; c < c0; c++) lds_contact(c, improvement);
+    // contacts: [0, npre) from LDS, the register block for [c0, c1), then the rest
+    // ([npre, c0) and [c1, nl)) from LDS; the block runs once per sweep for the wave
+    for (int c = 0; c < npre; c++) lds_contact(c, improvement);
     if constexpr (NF == 1 && CON) {
 #pragma unroll
       for (int k = 0; k < FC; k++) {
         const int c = cslot[k];
-        float jn[6], j1[6], j2[6], G[6], cf[12], ar[4], ia[4], hd[4];
+        float jn[6], j1[6], j2[6], ar[4], ia[4], hd[4];
 #pragma unroll
         for (int i = 0; i < 6; i++)
-          jn[i] = L.at(c, NA + i), j1[i] = L.at(c, 12 + NA + i), j2[i] = L.at(c, 24 + NA + i), G[i] = L.at(c, F_GRAM + i);
+          jn[i] = L.at(c, NA + i), j1[i] = L.at(c, 12 + NA + i), j2[i] = L.at(c, 24 + NA + i);
 #pragma unroll
         for (int ed = 0; ed < 4; ed++)
           ar[ed] = L.at(c, F_AREF + ed), ia[ed] = L.at(c, F_IARD + ed), hd[ed] = L.at(c, F_HARD + ed);
         const float mu = L.at(c, F_MU), Rp = L.at(c, F_R);
-        gram_coefs(G, mu, cf);
-        gram_step(v + NA, jn, j1, j2, cf, ar, ia, hd, cfo[k], mu, Rp, Mi.Fd[0], improvement);
+        gram_step(v + NA, jn, j1, j2, ccf[k], ar, ia, hd, cfo[k], mu, Rp, Mi.Fd[0], improvement);
       }
     }
-    for (int c = c1; c < nl; c++) lds_contact(c, improvement);
+    for (int j = 0; j < npost; j++) lds_contact(j < c0 - npre ? npre + j : c1 + j - (c0 - npre), improvement);
     scratch_rows(improvement);
     if (improvement * scale < m.tolerance) {
 #ifdef SOARM_PHASE_PROF
