@@ -34,7 +34,8 @@ def parse():
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--envs", type=int, default=None, help="envs per GPU (default 4096; 8192 for dr)")
-    p.add_argument("--config", default="contact", choices=["contact", "nocontact", "dr"])
+    p.add_argument("--config", default="contact", choices=["contact", "nocontact", "dr", "rollout"])
+    p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal on one GPU)")
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -71,8 +72,16 @@ def cpu_baseline(cfg_name, seconds, seed):
             p = W.dr_params(ids, seed)
             prm = np.stack([p["mass_scale"], p["friction"], p["damping_scale"]], 1).astype(np.float64)
         rng = np.random.default_rng(chunk)
+        phase = W.ik_phase(ids, seed)
+        qstar = q.astype(np.float64)
         for t in range(T):
-            a = W.chirp_action(tab, t) if cfg["action"] == "chirp" else rng.uniform(-0.5, 0.5, (n, 5))
+            if cfg["action"] == "chirp":
+                a = W.chirp_action(tab, t)
+            elif cfg["action"] == "ik_fig8":
+                qstar, _, _ = orc.ik(W.fig8_targets(t, phase), qstar)
+                a = W.ik_action(qstar[:, :5], st["qpos"][:, :5])
+            else:
+                a = rng.uniform(-0.5, 0.5, (n, 5))
             orc.step(st, a, params=prm, nthreads=cores)
             done += n
         chunk += 1
@@ -96,17 +105,21 @@ def main():
     from lerobot_mujoco_sim2real_amd.sim import BatchSim
 
     build.build()
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    gpu = local % max(torch.cuda.device_count(), 1)  # > 1 rank per GPU only in gloo rehearsals
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if world > 1:
-        dist.init_process_group("nccl", init_method="env://", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", init_method="env://", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend, init_method="env://")
 
     name = args.config
     cfg = W.CONFIGS[name]
     n = args.envs or (8192 if name == "dr" else 4096)
     ids = np.arange(rank * n, (rank + 1) * n)
     cm = W.model(name)
-    sim = BatchSim(cm, n, local)
+    sim = BatchSim(cm, n, gpu)
     q0 = W.initial_qpos(cm, ids, args.seed)
     sim.reset(init_qpos=q0[:, :5], extra_qpos=q0, seed=args.seed, env_offset=rank * n)
     if cfg["dr"]:
@@ -117,13 +130,38 @@ def main():
     gen.manual_seed(args.seed * 1000003 + rank)
     act = torch.empty((n, 5), dtype=torch.float32, device=dev)
 
+    rollout = cfg["action"] == "ik_fig8"
+    if rollout:
+        # config 5: DLS-IK toward each env's Fig8 target, action = clip((q* - q)/dt), rows
+        # [u | obs] recorded on device for every timed step, gathered to rank 0 at the end
+        phase = torch.as_tensor(W.ik_phase(ids, args.seed), dtype=torch.float32, device=dev)
+        qstar = sim.qpos.clone()
+        rows = torch.empty((args.steps + 1, n, 13), dtype=torch.float32, device=dev)
+        rec = {"i": -1}
+
     def one_step(t):
-        if cfg["action"] == "chirp":
+        if rollout:
+            nonlocal qstar
+            qstar, _, _ = sim.ik(W.fig8_targets(float(t), phase, lib=torch), q=qstar)
+            act.copy_(W.ik_action(qstar[:5].T, sim.obs[:, 3:8], lib=torch))
+        elif cfg["action"] == "chirp":
             act.copy_(W.chirp_action(tab, float(t), lib=torch))
         else:
             torch.rand((n, 5), generator=gen, device=dev, out=act)
             act.sub_(0.5)
-        sim.step(act)
+        obs = sim.step(act)
+        if rollout and rec["i"] >= 0:
+            rows[rec["i"], :, :5] = act
+            rows[rec["i"] + 1, :, 5:] = obs
+            rec["i"] += 1
+
+    def gather_rows():
+        """Rollout rows of every rank to rank 0 (RCCL gather over xGMI)."""
+        if world == 1:
+            return
+        src = rows if args.dist_backend == "nccl" else rows.cpu()
+        bufs = [torch.empty_like(src) for _ in range(world)] if rank == 0 else None
+        dist.gather(src, bufs, dst=0)
 
     t = 0
     for _ in range(args.warmup):
@@ -138,9 +176,15 @@ def main():
 
     sync()
     t0 = time.perf_counter()
+    if rollout:
+        rows[0, :, 5:] = sim.obs
+        rec["i"] = 0
     for _ in range(args.steps):
         one_step(t)
         t += 1
+    if rollout:
+        rec["i"] = -1
+        gather_rows()
     sync()
     dt = time.perf_counter() - t0
     ncon = float(sim.ncon.sum().item())

@@ -14,6 +14,12 @@ batch runs on 1 or 8 GPUs.
 * ``dr`` (config 4): ``contact`` + per-env domain randomisation: body mass
   x U(0.8, 1.2) (inertia scaled alike), sliding friction U(0.5, 1.5), dof
   damping x U(0.8, 1.2).
+* ``rollout`` (config 5, build-defined extension ii of SURVEY.md §8a): the
+  reference scene (arm + table, contacts on); each env follows a Fig8 path
+  (``control/TrajectoryGenerator.py:138-152``) with a per-env phase; every
+  env-step runs position-only DLS IK (warm-started) and applies
+  ``clip((q* - q) / dt, +-max_speed)`` (``SOARM101_Env.py:57``); rows
+  ``[u(5) | ee(3) | q(5)]`` as in ``SOARM101_DataCollection.py:106-134``.
 """
 import numpy as np
 
@@ -27,6 +33,9 @@ CONFIGS = {
                     desc="4096 SO-ARM101 envs, tabletop+cube contacts, PGS (config 3, pick scene)"),
     "dr": dict(xml=CUBE_SCENE_XML, disable_contact=False, action="chirp", dr=True,
                desc="SO-ARM101 pick scene with per-env mass/friction/damping DR (config 4)"),
+    "rollout": dict(xml=SCENE_XML, disable_contact=False, action="ik_fig8", dr=False,
+                    desc="SOARM101_DataCollection rollout: batched DLS-IK actions toward Fig8 targets, "
+                         "rows [T+1, N, 13] on device, gathered to rank 0 (config 5)"),
 }
 
 
@@ -77,3 +86,23 @@ def chirp_action(tab, t, lib=np, T_total=200):
 def dr_params(ids, seed=0):
     u = philox_uniform(seed + 3, ids, 3)
     return dict(mass_scale=0.8 + 0.4 * u[:, 0], friction=0.5 + 1.0 * u[:, 1], damping_scale=0.8 + 0.4 * u[:, 2])
+
+
+def ik_phase(ids, seed=0):
+    """Per-env phase of the Fig8 target stream (config 5)."""
+    return 2 * np.pi * philox_uniform(seed + 4, ids, 1)[:, 0].astype(np.float64)
+
+
+def fig8_targets(t, phase, lib=np):
+    """Fig8 target of env-step t (``TrajectoryGenerator.py:138-152``, idx 1, scale 0.5):
+    parameter 1.6 + 0.02 (t + 1) + phase."""
+    tp = 1.6 + 0.02 * (t + 1) + phase
+    one = lib.ones_like(tp)
+    s, c = lib.sin(tp), lib.cos(tp)
+    a = b = 0.2 * 0.5
+    return lib.stack([0.4 * one, b * c / (1 + s ** 2), 0.2 + 2 * a * s * c / (1 + s ** 2)], -1)
+
+
+def ik_action(qstar, q, dt=0.02, max_speed=0.5, lib=np):
+    """action = clip((q* - q) / dt, +-max_speed) over the 5 arm joints."""
+    return lib.clip((qstar - q) / dt, -max_speed, max_speed)

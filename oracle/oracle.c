@@ -990,6 +990,9 @@ void orc_ik_dls(const sim_model_desc* m, int n, const double* target, double* q,
                 double max_update, double progress_thresh, int max_steps, int site, int ndof) {
   orc_model om;
   make_om(&om, m, NULL, NULL, NULL, NULL);
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 16)
+#endif
   for (int e = 0; e < n; e++) {
     orc_data d;
     orc_reset_data(&om, &d);

@@ -43,8 +43,15 @@ def main():
             prm = np.stack([p["mass_scale"], p["friction"], p["damping_scale"]], 1).astype(np.float64)
         rng = np.random.default_rng(0)
         tot = col = 0.0
+        phase, qstar = W.ik_phase(ids), q.astype(np.float64)
         for t in range(T):
-            a = W.chirp_action(tab, t) if c["action"] == "chirp" else rng.uniform(-0.5, 0.5, (N, 5))
+            if c["action"] == "chirp":
+                a = W.chirp_action(tab, t)
+            elif c["action"] == "ik_fig8":  # IK flops are not counted: physics only
+                qstar, _, _ = orc.ik(W.fig8_targets(t, phase), qstar)
+                a = W.ik_action(qstar[:, :5], st["qpos"][:, :5])
+            else:
+                a = rng.uniform(-0.5, 0.5, (N, 5))
             orc.step(st, a, params=prm, nthreads=8)
             tot += orc.last_flops
             col += orc.last_collision_flops
