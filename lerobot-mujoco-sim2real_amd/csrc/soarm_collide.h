@@ -22,7 +22,13 @@
 namespace soarm {
 
 constexpr int CON_MAXG = 16;  // collidable geoms supported by the contact kernel
-constexpr float FEPS = 1.1920929e-07f;
+// MPR's zero tests.  libccd (and the oracle) use DBL_EPSILON as an ABSOLUTE
+// threshold, i.e. effectively exact sign tests on lengths, triple products and
+// squared cross products.  An fp32 epsilon (1.2e-7) in that role is NOT small
+// for these unnormalised quantities at centimetre scale (|v0 x v1|^2 ~ 1e-7 m^4
+// for 2 cm geoms): it declared non-collinear portals collinear and produced
+// phantom penetrations several millimetres deep.  So: exact-sign tests here too.
+constexpr float FEPS = 1e-30f;
 constexpr float MPR_TOLF = 1e-6f;
 constexpr int MPR_ITERS = 50;
 

@@ -513,12 +513,12 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   if (e < 65536) g_pgs_prof[6 * e] = clock64();
   int nsweep = m.iterations;
 #endif
-  // dof-frictionloss rows (J = e_i): one pass
+  // dof-frictionloss rows (J = e_i): one pass.  Branch-free: a dof with frictionloss 0
+  // (no row in MuJoCo) clamps to [0, 0] and stays an exact no-op.
   auto fric_rows = [&](float& improvement) {
 #pragma unroll
     for (int i = 0; i < NA; i++) {
       const float fl = m.dof_frictionloss[i];
-      if (!(fl > 0.f)) continue;  // model constant: wave-uniform
       const float res = v[i] - fa[i] + fR[i] * ff[i];
       const float fn = fminf(fmaxf(ff[i] - res * fiD[i], -fl), fl);
       const float df = fn - ff[i];
@@ -669,13 +669,8 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   for (int c = 0; c < c0; c++)
     if ((int)L.at(c, F_FLAGS) & TOUCH_FREE) npre = c0;
   const int npost = (c0 - npre) + (nl - c1);
-  for (int it = 0; it < m.iterations; it++) {
-    float improvement = 0.f;
-    fric_rows(improvement);
-    limit_rows(improvement);
-    // contacts: [0, npre) from LDS, the register block for [c0, c1), then the rest
-    // ([npre, c0) and [c1, nl)) from LDS; the block runs once per sweep for the wave
-    for (int c = 0; c < npre; c++) lds_contact(c, improvement);
+  // the block's sweep (straight-line: one basic block with the friction rows)
+  auto block_rows = [&](float& improvement) {
     if constexpr (NF == 1 && CON) {
 #pragma unroll
       for (int k = 0; k < FC; k++) {
@@ -690,6 +685,24 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
         const float mu = L.at(c, F_MU), Rp = L.at(c, F_R);
         gram_step(v + NA, jn, j1, j2, ccf[k], ar, ia, hd, cfo[k], mu, Rp, Mi.Fd[0], improvement);
       }
+    }
+  };
+  // When no lane has a pre-block contact on the free body (always, for pair-ordered
+  // scenes where the cube's world contacts come first), the block commutes with every
+  // arm row before it: run it beside the friction rows so the two independent chains
+  // share one straight-line region, then limits and the remaining contacts.
+  const bool block_first = __all(npre == 0);
+  for (int it = 0; it < m.iterations; it++) {
+    float improvement = 0.f;
+    if (block_first) {
+      fric_rows(improvement);
+      block_rows(improvement);
+      limit_rows(improvement);
+    } else {
+      fric_rows(improvement);
+      limit_rows(improvement);
+      for (int c = 0; c < npre; c++) lds_contact(c, improvement);
+      block_rows(improvement);
     }
     for (int j = 0; j < npost; j++) lds_contact(j < c0 - npre ? npre + j : c1 + j - (c0 - npre), improvement);
     scratch_rows(improvement);

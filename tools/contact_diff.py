@@ -59,7 +59,11 @@ for name in ("arm", "cube"):
     for e in range(n):
         rc = orc.forward(full[e])["contacts"]
         if len(rc) != nc[e]:
-            print(name, e, "count", nc[e], len(rc))
+            gp = [(cm.geom_names[d.pair_geom1[x]], cm.geom_names[d.pair_geom2[x]], round(float(out[e, k, 0]), 6))
+                  for k, x in enumerate(pid[e, :nc[e]])]
+            op = [(cm.geom_names[int(a)], cm.geom_names[int(b)], round(float(dd), 6)) for dd, a, b in rc[:, [0, 7, 8]]]
+            print(name, e, "count", nc[e], len(rc), "gpu-only", [x for x in gp if x[:2] not in [y[:2] for y in op]],
+                  "oracle-only", [y for y in op if y[:2] not in [x[:2] for x in gp]], "q", np.round(full[e], 4).tolist())
             continue
         for k in range(nc[e]):
             tot += 1
