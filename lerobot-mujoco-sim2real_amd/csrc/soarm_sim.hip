@@ -212,7 +212,7 @@ __global__ __launch_bounds__(256) void k_collide(const DModel* __restrict__ dm, 
                                                  uint32_t* __restrict__ pmask,
                                                  unsigned long long* __restrict__ pcyc) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  const int p = blockIdx.y;
+  const int p = gridDim.y - 1 - blockIdx.y;  // later pairs (self / cube-arm: MPR-heavy) dispatch first
   if (e >= n) return;
   const long long t0 = pcyc ? clock64() : 0;
   const DModel& m = *dm;
