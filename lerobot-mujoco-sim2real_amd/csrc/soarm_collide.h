@@ -436,7 +436,9 @@ DEVI void box_box(const DModel& m, int g1, int g2, const GeomPose& P1, const Geo
   sub(t, P2.p, P1.p);
   float best = 3.0e38f, bn[3] = {0, 0, 0};
   int bcode = -1;
-  for (int code = 0; code < 15; code++) {
+  bool sep = false;
+#pragma unroll
+  for (int code = 0; code < 15; code++) {  // unrolled: A / B rows by compile-time index
     float L[3];
     if (code < 3)
       L[0] = A[code][0], L[1] = A[code][1], L[2] = A[code][2];
@@ -445,14 +447,14 @@ DEVI void box_box(const DModel& m, int g1, int g2, const GeomPose& P1, const Geo
     else
       cross(L, A[(code - 6) / 3], B[(code - 6) % 3]);
     const float ln = sqrtf(dot3(L, L));
-    if (ln < 1e-6f) continue;
+    if (ln < 1e-6f) continue;  // parallel edges: no axis
     L[0] /= ln, L[1] /= ln, L[2] /= ln;
     float r1 = 0.f, r2 = 0.f;
 #pragma unroll
     for (int k = 0; k < 3; k++) r1 += h1[k] * fabsf(dot3(A[k], L)), r2 += h2[k] * fabsf(dot3(B[k], L));
     const float tl = dot3(t, L);
     const float ov = r1 + r2 - fabsf(tl);
-    if (ov < 0.f) return;
+    sep = sep || ov < 0.f;
     const float score = code < 6 ? ov : ov * 1.05f + 1e-9f;
     if (score < best) {
       best = score;
@@ -461,7 +463,7 @@ DEVI void box_box(const DModel& m, int g1, int g2, const GeomPose& P1, const Geo
       bn[0] = sg * L[0], bn[1] = sg * L[1], bn[2] = sg * L[2];
     }
   }
-  if (bcode < 0) return;
+  if (sep || bcode < 0) return;
   if (bcode < 6) {
     const bool ref1 = bcode < 3;
     const int fa = ref1 ? bcode : bcode - 3;
