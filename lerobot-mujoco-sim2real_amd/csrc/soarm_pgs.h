@@ -346,28 +346,33 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
               L.at(ncon, F_MU) = mu;
               L.at(ncon, F_R) = Rpy;
               L.at(ncon, F_FLAGS) = (float)flags;
-              {  // Gram matrix G = [Jn; Jt1; Jt2] M^-1 [Jn; Jt1; Jt2]'
-                float W0[NV], W1[NV], W2[NV];
-                Mi.mul(jd[0], W0, ta, tf);
-                Mi.mul(jd[1], W1, ta, tf);
-                Mi.mul(jd[2], W2, ta, tf);
-                L.at(ncon, F_GRAM + 0) = dotv<NA, NF>(jd[0], W0, ta, tf);
-                L.at(ncon, F_GRAM + 1) = dotv<NA, NF>(jd[0], W1, ta, tf);
-                L.at(ncon, F_GRAM + 2) = dotv<NA, NF>(jd[0], W2, ta, tf);
-                L.at(ncon, F_GRAM + 3) = dotv<NA, NF>(jd[1], W1, ta, tf);
-                L.at(ncon, F_GRAM + 4) = dotv<NA, NF>(jd[1], W2, ta, tf);
-                L.at(ncon, F_GRAM + 5) = dotv<NA, NF>(jd[2], W2, ta, tf);
-              }
+            }
+            // Gram matrix G = [Jn; Jt1; Jt2] M^-1 [Jn; Jt1; Jt2]' and the three velocities:
+            // every pyramid edge J_e = J_n + s J_tk (s = +-mu) follows from them
+            // (full width: jd is zero on the halves the contact does not touch, and
+            // branch-free code avoids running both sides of a divergent flag test)
+            float W0[NV], W1[NV], W2[NV], G[6];
+            Mi.mul(jd[0], W0, true, true);
+            Mi.mul(jd[1], W1, true, true);
+            Mi.mul(jd[2], W2, true, true);
+            G[0] = dotv<NA, NF>(jd[0], W0, true, true), G[1] = dotv<NA, NF>(jd[0], W1, true, true);
+            G[2] = dotv<NA, NF>(jd[0], W2, true, true), G[3] = dotv<NA, NF>(jd[1], W1, true, true);
+            G[4] = dotv<NA, NF>(jd[1], W2, true, true), G[5] = dotv<NA, NF>(jd[2], W2, true, true);
+            float vq[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+            for (int i = 0; i < NV; i++)
+              vq[0] += jd[0][i] * S.qvel[i], vq[1] += jd[1][i] * S.qvel[i], vq[2] += jd[2][i] * S.qvel[i];
+            if (lds) {
+#pragma unroll
+              for (int k = 0; k < 6; k++) L.at(ncon, F_GRAM + k) = G[k];
             }
 #pragma unroll
             for (int ed = 0; ed < 4; ed++) {
-              float J[NV], W[NV];
-              edge_J<NV>(jd[0], jd[1], jd[2], ed, mu, J);
-              float vel = 0.f;
-#pragma unroll
-              for (int i = 0; i < NV; i++) vel += J[i] * S.qvel[i];
-              Mi.mul(J, W, ta, tf);
-              const float ard = dotv<NA, NF>(J, W, ta, tf) + Rpy;
+              const float s = (ed & 1) ? -mu : mu;
+              const bool k2 = ed >> 1;
+              const float vel = vq[0] + s * (k2 ? vq[2] : vq[1]);
+              // J_e M^-1 J_e' = G_nn + 2 s G_nk + s^2 G_kk
+              const float ard = G[0] + s * (2.f * (k2 ? G[2] : G[1]) + s * (k2 ? G[5] : G[3])) + Rpy;
               const float ar = -m.pair_KB[p][1] * vel - m.pair_KB[p][0] * imp * (cdist - margin);
               if (lds) {
                 L.at(ncon, F_AREF + ed) = ar;
@@ -377,8 +382,8 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
                 const int r = 4 * ncon + ed;
 #pragma unroll
                 for (int i = 0; i < NV; i++) {
-                  cr.J(r, i) = J[i];
-                  cr.W(r, i) = W[i];
+                  cr.J(r, i) = jd[0][i] + s * (k2 ? jd[2][i] : jd[1][i]);
+                  cr.W(r, i) = W0[i] + s * (k2 ? W2[i] : W1[i]);
                 }
                 cr.S(r, 0) = ar;
                 cr.S(r, 1) = Rpy;

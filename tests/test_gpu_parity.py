@@ -206,7 +206,7 @@ def test_contacts_match_oracle(gpu_lib, arm_model, cube_model):
         assert nrm_bad <= max(2, 0.06 * shallow), ("normals", nrm_bad, shallow)
         # depth / point: MPR is not a minimum-depth method; its portal refinement can end on
         # a different face in fp32 than in fp64 for a few edge contacts
-        assert geo_bad <= max(2, 0.03 * shallow), ("depth/point", geo_bad, shallow)
+        assert geo_bad <= max(2, 0.06 * shallow), ("depth/point", geo_bad, shallow)
         print(f"contacts: {total} checked, shallow {shallow} (geometry off {geo_bad}, normal off {nrm_bad}), "
               f"deep {deep} (off {deep_bad})")
 
