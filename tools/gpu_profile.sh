@@ -26,6 +26,7 @@ step bench_contact 600 python bench.py > $O/bench_contact.json 2> $O/bench_conta
 cat $O/bench_contact.json
 step bench_nocontact 300 python bench.py --config nocontact --steps 200 --warmup 20 --cpu-seconds 8 > $O/bench_nocontact.json 2> $O/bench_nocontact.err
 step bench_dr 600 python bench.py --config dr --steps 50 --warmup 5 --cpu-seconds 8 > $O/bench_dr.json 2> $O/bench_dr.err
+step bench_rollout 600 python bench.py --config rollout --steps 100 --warmup 5 --cpu-seconds 8 > $O/bench_rollout.json 2> $O/bench_rollout.err
 cd /tmp
 step kernel_trace 600 rocprofv3 --kernel-trace --stats -f csv -d $O/prof_$TAG -o trace -- python3 $R/bench.py --steps 30 --warmup 5 --no-cpu-baseline > $O/bench_contact_traced.json
 step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_substep|k_collide|k_step|k_geom" -f csv -d $O/prof_$TAG -o pmc_fetch -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-profile
