@@ -32,7 +32,7 @@ namespace soarm {
 
 #ifdef SOARM_PHASE_PROF
 // diagnostic build only: per-env PGS start/end clock, sweep count, fast-path flag (env < 65536)
-__device__ long long g_pgs_prof[65536 * 6];
+__device__ long long g_pgs_prof[65536 * 8];
 #endif
 
 constexpr int LDS_CON = 8;  // contacts whose rows stay in LDS
@@ -397,6 +397,9 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
     }
   }
   const int nl = ncon < LDS_CON ? ncon : LDS_CON;
+#ifdef SOARM_PHASE_PROF
+  if (e < 65536) g_pgs_prof[8 * e + 6] = clock64();  // rows built
+#endif
 
   // ---- warm start from qacc_warmstart (forces implied by the primal), keep if it beats f = 0
   float v[NV];
@@ -420,26 +423,30 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
     L.lm(l, L_FRC) = fs;
     add_arm_col(Mi, v, oh, sg * fs);
   }
+  // contacts (Gram form: J_e x = J_n x + s J_tk x; one M^-1 product per contact)
   for (int c = 0; c < nl; c++) {
-    const int fl = (int)L.at(c, F_FLAGS);
-    const bool ta = fl & TOUCH_ARM, tf = fl & TOUCH_FREE;
     float jn[NV], jt1[NV], jt2[NV];
 #pragma unroll
     for (int i = 0; i < NV; i++) jn[i] = L.at(c, i), jt1[i] = L.at(c, 12 + i), jt2[i] = L.at(c, 24 + i);
     const float mu = L.at(c, F_MU), Rp = L.at(c, F_R);
+    float jw[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < NV; i++) jw[0] += jn[i] * S.warm[i], jw[1] += jt1[i] * S.warm[i], jw[2] += jt2[i] * S.warm[i];
+    float fs[4];
 #pragma unroll
     for (int ed = 0; ed < 4; ed++) {
-      float J[NV], W[NV];
-      edge_J<NV>(jn, jt1, jt2, ed, mu, J);
-      const float jar = dotv<NA, NF>(J, S.warm, ta, tf) - L.at(c, F_AREF + ed);
-      const float fs = jar < 0.f ? -jar / Rp : 0.f;
-      L.at(c, F_FRC + ed) = fs;
-      if (fs != 0.f) {
-        Mi.mul(J, W, ta, tf);
-#pragma unroll
-        for (int i = 0; i < NV; i++) v[i] += W[i] * fs;
-      }
+      const float s = (ed & 1) ? -mu : mu;
+      const float jar = jw[0] + s * jw[1 + (ed >> 1)] - L.at(c, F_AREF + ed);
+      fs[ed] = jar < 0.f ? -jar / Rp : 0.f;
+      L.at(c, F_FRC + ed) = fs[ed];
     }
+    const float Dn = (fs[0] + fs[1]) + (fs[2] + fs[3]), D1 = mu * (fs[0] - fs[1]), D2 = mu * (fs[2] - fs[3]);
+    float u[NV], w[NV];
+#pragma unroll
+    for (int i = 0; i < NV; i++) u[i] = jn[i] * Dn + jt1[i] * D1 + jt2[i] * D2;
+    Mi.mul(u, w, true, true);
+#pragma unroll
+    for (int i = 0; i < NV; i++) v[i] += w[i];
   }
   for (int c = nl; c < ncon; c++)
     for (int ed = 0; ed < 4; ed++) {
@@ -464,21 +471,22 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
     cost += 0.5f * f * (sg * pick<NA>(v, oh) - ar + L.lm(l, L_R) * f) + 0.5f * f * (sg * pick<NA>(S.qacc_s, oh) - ar);
   }
   for (int c = 0; c < nl; c++) {
-    const int fl = (int)L.at(c, F_FLAGS);
-    const bool ta = fl & TOUCH_ARM, tf = fl & TOUCH_FREE;
     float jn[NV], jt1[NV], jt2[NV];
 #pragma unroll
     for (int i = 0; i < NV; i++) jn[i] = L.at(c, i), jt1[i] = L.at(c, 12 + i), jt2[i] = L.at(c, 24 + i);
     const float mu = L.at(c, F_MU), Rp = L.at(c, F_R);
+    float jv[3] = {0.f, 0.f, 0.f}, jq[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < NV; i++) {
+      jv[0] += jn[i] * v[i], jv[1] += jt1[i] * v[i], jv[2] += jt2[i] * v[i];
+      jq[0] += jn[i] * S.qacc_s[i], jq[1] += jt1[i] * S.qacc_s[i], jq[2] += jt2[i] * S.qacc_s[i];
+    }
 #pragma unroll
     for (int ed = 0; ed < 4; ed++) {
-      const float fr = L.at(c, F_FRC + ed);
-      if (fr == 0.f) continue;
-      float J[NV];
-      edge_J<NV>(jn, jt1, jt2, ed, mu, J);
-      const float ar = L.at(c, F_AREF + ed);
-      cost += 0.5f * fr * (dotv<NA, NF>(J, v, ta, tf) - ar + Rp * fr) +
-              0.5f * fr * (dotv<NA, NF>(J, S.qacc_s, ta, tf) - ar);
+      const float s = (ed & 1) ? -mu : mu;
+      const float fr = L.at(c, F_FRC + ed), ar = L.at(c, F_AREF + ed);
+      cost += 0.5f * fr * (jv[0] + s * jv[1 + (ed >> 1)] - ar + Rp * fr) +
+              0.5f * fr * (jq[0] + s * jq[1 + (ed >> 1)] - ar);
     }
   }
   for (int c = nl; c < ncon; c++)
@@ -505,6 +513,9 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
     for (int i = 0; i < NV; i++) v[i] = S.qacc_s[i];
   }
 
+#ifdef SOARM_PHASE_PROF
+  if (e < 65536) g_pgs_prof[8 * e + 7] = clock64();  // warm start + cost done
+#endif
   // ---- projected Gauss-Seidel sweeps (MuJoCo improvement criterion, scaled by 1/trace(M))
   float tr = 0.f;
 #pragma unroll
@@ -515,7 +526,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
     for (int i = 0; i < 6; i++) tr += S.MF[f2][i * (i + 1) / 2 + i];
   const float scale = 1.f / tr;
 #ifdef SOARM_PHASE_PROF
-  if (e < 65536) g_pgs_prof[6 * e] = clock64();
+  if (e < 65536) g_pgs_prof[8 * e] = clock64();
   int nsweep = m.iterations;
 #endif
   // dof-frictionloss rows (J = e_i): one pass.  Branch-free: a dof with frictionloss 0
@@ -727,8 +738,8 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   }
 #ifdef SOARM_PHASE_PROF
   if (e < 65536)
-    g_pgs_prof[6 * e + 1] = clock64(), g_pgs_prof[6 * e + 2] = nsweep,
-    g_pgs_prof[6 * e + 3] = (nrun == ncon && nlim == 0), g_pgs_prof[6 * e + 4] = nlim, g_pgs_prof[6 * e + 5] = ncon;
+    g_pgs_prof[8 * e + 1] = clock64(), g_pgs_prof[8 * e + 2] = nsweep,
+    g_pgs_prof[8 * e + 3] = (nrun == ncon && nlim == 0), g_pgs_prof[8 * e + 4] = nlim, g_pgs_prof[8 * e + 5] = ncon;
 #endif
 
   // ---- qacc and qfrc_constraint = J' f

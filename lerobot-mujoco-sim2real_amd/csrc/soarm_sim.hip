@@ -141,8 +141,9 @@ DEVI void write_obs(const Sim<NA, NF>& S, float* obs, int e) {
 //   [9] waves on the register fast path, [10] max wave PGS cycles,
 //   [11] sum over waves of the wave's max sweep count, [12] waves with an active
 //   joint limit, [13] waves with a contact outside the register block, [14] waves
-//   with more than LDS_CON contacts, [15] max contacts of an env
-__device__ unsigned long long g_phase[16];
+//   with more than LDS_CON contacts, [15] max contacts of an env, [16] rows: up to
+//   the built contact rows, [17] rows: warm start + cost, [18] rows: block setup
+__device__ unsigned long long g_phase[19];
 #define PHASE_T(v) const long long v = clock64()
 #else
 #define PHASE_T(v)
@@ -318,11 +319,11 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
   }
 #ifdef SOARM_PHASE_PROF
   PHASE_T(t5);
-  const long long p0 = g_pgs_prof[6 * e], p1 = g_pgs_prof[6 * e + 1];
-  const int nsw = (int)g_pgs_prof[6 * e + 2];
-  const bool anylim = __any(g_pgs_prof[6 * e + 4] > 0), anyslow = __any(g_pgs_prof[6 * e + 3] == 0),
-             anyovf = __any(g_pgs_prof[6 * e + 5] > LDS_CON);
-  atomicMax(&g_phase[15], (unsigned long long)g_pgs_prof[6 * e + 5]);
+  const long long p0 = g_pgs_prof[8 * e], p1 = g_pgs_prof[8 * e + 1];
+  const int nsw = (int)g_pgs_prof[8 * e + 2];
+  const bool anylim = __any(g_pgs_prof[8 * e + 4] > 0), anyslow = __any(g_pgs_prof[8 * e + 3] == 0),
+             anyovf = __any(g_pgs_prof[8 * e + 5] > LDS_CON);
+  atomicMax(&g_phase[15], (unsigned long long)g_pgs_prof[8 * e + 5]);
   atomicAdd(&g_phase[6], (unsigned long long)nsw);
   atomicAdd(&g_phase[7], 1ull);
   int wmax = nsw;
@@ -335,7 +336,10 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
     atomicAdd(&g_phase[3], (unsigned long long)(p1 - p0));
     atomicAdd(&g_phase[4], (unsigned long long)(t5 - p1));
     atomicMax(&g_phase[8], (unsigned long long)(t5 - t0));
-    atomicAdd(&g_phase[9], (unsigned long long)g_pgs_prof[6 * e + 3]);
+    atomicAdd(&g_phase[9], (unsigned long long)g_pgs_prof[8 * e + 3]);
+    atomicAdd(&g_phase[16], (unsigned long long)(g_pgs_prof[8 * e + 6] - t2));
+    atomicAdd(&g_phase[17], (unsigned long long)(g_pgs_prof[8 * e + 7] - g_pgs_prof[8 * e + 6]));
+    atomicAdd(&g_phase[18], (unsigned long long)(p0 - g_pgs_prof[8 * e + 7]));
     atomicAdd(&g_phase[12], (unsigned long long)anylim);
     atomicAdd(&g_phase[13], (unsigned long long)anyslow);
     atomicAdd(&g_phase[14], (unsigned long long)anyovf);
@@ -985,18 +989,18 @@ int sim_collide_profile(sim_batch* b, const sim_state* s, double* cycles, void* 
 int sim_phase_profile(double* out, int reset) {
   if (!out) return fail(SIM_E_ARG, "null output");
 #ifdef SOARM_PHASE_PROF
-  unsigned long long h[16];
+  unsigned long long h[19];
   HIPCHECK(hipDeviceSynchronize());
   HIPCHECK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_phase), sizeof(h)));
-  for (int k = 0; k < 16; k++) out[k] = (double)h[k];
+  for (int k = 0; k < 19; k++) out[k] = (double)h[k];
   if (reset) {
-    const unsigned long long z[16] = {};
+    const unsigned long long z[19] = {};
     HIPCHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof(z)));
   }
   return SIM_OK;
 #else
   (void)reset;
-  for (int k = 0; k < 16; k++) out[k] = 0.0;
+  for (int k = 0; k < 19; k++) out[k] = 0.0;
   return SIM_E_ARG;  // not a profiling build
 #endif
 }

@@ -41,7 +41,7 @@ q0 = W.initial_qpos(cm, ids, 0)
 sim.reset(init_qpos=q0[:, :5], extra_qpos=q0, seed=0)
 tab = {k: (torch.as_tensor(v, dtype=torch.float32, device="cuda") if isinstance(v, np.ndarray) else v)
        for k, v in W.chirp_tables(ids, 0).items()}
-out = (ctypes.c_double * 16)()
+out = (ctypes.c_double * 19)()
 res = {}
 for t in range(T):
     if t in (0, T // 2, T - 10):
@@ -65,6 +65,7 @@ for t in range(T):
         r["waves_with_nonblock_contact"] = v[13] / max(v[5], 1)
         r["waves_with_lds_overflow"] = v[14] / max(v[5], 1)
         r["max_ncon"] = v[15]
+        r["rows_split"] = {"contact_rows": v[16] / tot, "warm_cost": v[17] / tot, "block_setup": v[18] / tot}
         res[t] = r
         print(t, json.dumps(r), flush=True)
 json.dump(res, open(os.path.join(ROOT, "gpurun_out", "phase_prof.json"), "w"), indent=1)
