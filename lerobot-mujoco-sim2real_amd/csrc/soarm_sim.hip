@@ -9,6 +9,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <type_traits>
@@ -61,6 +62,24 @@ struct sim_batch {
   size_t ev_used = 0;
   std::vector<std::pair<int, size_t>> ev_marks;  // (kind, index of start event)
   sim_params params{nullptr, nullptr, nullptr};
+  // hipGraph cache of the contact env-step's 1 + 2 x frame_skip launches, keyed by the
+  // buffers the kernels are bound to (SOARM_NO_GRAPH=1 disables)
+  struct GraphKey {
+    sim_state s;
+    const float* action;
+    float* obs;
+    int frame_skip;
+    bool operator==(const GraphKey& o) const {
+      return !memcmp(&s, &o.s, sizeof(s)) && action == o.action && obs == o.obs && frame_skip == o.frame_skip;
+    }
+  };
+  bool use_graphs = true;
+  hipStream_t cap_stream = nullptr;
+  std::vector<std::pair<GraphKey, hipGraphExec_t>> graphs;
+  void drop_graphs() {
+    for (auto& g : graphs) (void)hipGraphExecDestroy(g.second);
+    graphs.clear();
+  }
 };
 
 // ------------------------------------------------------------- Philox4x32-10
@@ -791,6 +810,7 @@ int sim_batch_create(const sim_model* m, int n_envs, int device, sim_batch** out
   sim_batch* B = new sim_batch();
   B->model = m;
   B->n = n_envs;
+  if (const char* ng = getenv("SOARM_NO_GRAPH")) B->use_graphs = ng[0] != '1';
   B->device = device;
   DModel dm = m->dm;
   if (!m->hull_vert.empty()) {
@@ -839,12 +859,15 @@ void sim_batch_free(sim_batch* b) {
   (void)hipFree(b->d_ccount);
   (void)hipFree(b->d_pmask);
   for (auto e : b->ev_pool) (void)hipEventDestroy(e);
+  b->drop_graphs();
+  if (b->cap_stream) (void)hipStreamDestroy(b->cap_stream);
   delete b;
 }
 
 int sim_batch_set_params(sim_batch* b, const sim_params* p) {
   if (!b) return fail(SIM_E_ARG, "null batch");
   b->params = p ? *p : sim_params{nullptr, nullptr, nullptr};
+  b->drop_graphs();  // the parameters are bound into captured launches
   return SIM_OK;
 }
 
@@ -890,29 +913,54 @@ int sim_step(sim_batch* b, const sim_state* s, const float* action, int frame_sk
   }
   // contacts: geom poses, then per substep (env, pair)-parallel collide + per-env dynamics
   const int np = b->model->desc.npair;
-  dispatch_nf(b->model->nf, [&](auto nfc) {
-    constexpr int NA = 6, NF = decltype(nfc)::value;
-    prof_mark(b, 3, st);
-    hipLaunchKernelGGL((k_geom<NA, NF>), grid_for(b->n), dim3(64), 0, st, b->d_model, b->n, *s,
-                       b->d_gpose);
-    prof_mark(b, -1, st);
-    for (int sub = 0; sub < frame_skip; sub++) {
-      if (np > 0) {
-        prof_mark(b, 1, st);
-        hipLaunchKernelGGL(k_collide, dim3((b->n + 255) / 256, np), dim3(256), 0, st, b->d_model, b->n,
-                           b->d_gpose, b->d_cbuf, b->d_ccount, b->d_pmask, nullptr);
-        prof_mark(b, -1, st);
+  auto enqueue = [&](hipStream_t q) {
+    dispatch_nf(b->model->nf, [&](auto nfc) {
+      constexpr int NA = 6, NF = decltype(nfc)::value;
+      prof_mark(b, 3, q);
+      hipLaunchKernelGGL((k_geom<NA, NF>), grid_for(b->n), dim3(64), 0, q, b->d_model, b->n, *s,
+                         b->d_gpose);
+      prof_mark(b, -1, q);
+      for (int sub = 0; sub < frame_skip; sub++) {
+        if (np > 0) {
+          prof_mark(b, 1, q);
+          hipLaunchKernelGGL(k_collide, dim3((b->n + 255) / 256, np), dim3(256), 0, q, b->d_model, b->n,
+                             b->d_gpose, b->d_cbuf, b->d_ccount, b->d_pmask, nullptr);
+          prof_mark(b, -1, q);
+        }
+        const bool last = sub == frame_skip - 1;
+        prof_mark(b, 2, q);
+        hipLaunchKernelGGL((k_substep<NA, NF>), grid_for(b->n), dim3(64), 0, q, b->d_model, b->n, *s,
+                           sub == 0 ? action : nullptr, last ? obs : nullptr, b->params, b->d_scratch,
+                           b->d_cbuf, np > 0 ? b->d_ccount : nullptr, np > 0 ? b->d_pmask : nullptr,
+                           last ? nullptr : b->d_gpose);
+        prof_mark(b, -1, q);
       }
-      const bool last = sub == frame_skip - 1;
-      prof_mark(b, 2, st);
-      hipLaunchKernelGGL((k_substep<NA, NF>), grid_for(b->n), dim3(64), 0, st, b->d_model, b->n, *s,
-                         sub == 0 ? action : nullptr, last ? obs : nullptr, b->params, b->d_scratch,
-                         b->d_cbuf, np > 0 ? b->d_ccount : nullptr, np > 0 ? b->d_pmask : nullptr,
-                         last ? nullptr : b->d_gpose);
-      prof_mark(b, -1, st);
+    });
+  };
+  if (b->prof || !b->use_graphs) {  // profiling brackets every launch with events: no graph
+    enqueue(st);
+    HIPCHECK(hipGetLastError());
+    return SIM_OK;
+  }
+  // replay a captured graph of the whole env-step (one launch instead of 1 + 2 x frame_skip)
+  const sim_batch::GraphKey key{*s, action, obs, frame_skip};
+  hipGraphExec_t exec = nullptr;
+  for (auto& g : b->graphs)
+    if (g.first == key) exec = g.second;
+  if (!exec) {
+    if (!b->cap_stream) HIPCHECK(hipStreamCreateWithFlags(&b->cap_stream, hipStreamNonBlocking));
+    HIPCHECK(hipStreamBeginCapture(b->cap_stream, hipStreamCaptureModeThreadLocal));
+    enqueue(b->cap_stream);
+    hipGraph_t graph = nullptr;
+    HIPCHECK(hipStreamEndCapture(b->cap_stream, &graph));
+    HIPCHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+    (void)hipGraphDestroy(graph);
+    if (b->graphs.size() >= 8) {  // small LRU-less cache: start over
+      b->drop_graphs();
     }
-  });
-  HIPCHECK(hipGetLastError());
+    b->graphs.emplace_back(key, exec);
+  }
+  HIPCHECK(hipGraphLaunch(exec, st));
   return SIM_OK;
 }
 
