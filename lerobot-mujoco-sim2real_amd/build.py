@@ -8,7 +8,10 @@ SRC_DIR = os.path.join(PKG_DIR, "csrc")
 SOURCES = ["soarm_sim.hip"]
 HEADERS = ["dmodel.h", "soarm_kernels.h", "soarm_step.h", "soarm_collide.h", "soarm_pgs.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared"]
+# -fno-slp-vectorize: the per-lane algebra gains nothing from v_pk_* packing; the
+# packing's operand shuffles (v_mov) and the extra register pressure (AGPR
+# round trips) cost ~13% of the PGS sweep's VALU issue (ISA count, k_substep).
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-fno-slp-vectorize"]
 
 
 def _stale():

@@ -16,9 +16,12 @@ LIB = os.path.join(ROOT, "tools", "_prof", "libsoarm_sim_prof.so")
 SRC = os.path.join(ROOT, "lerobot-mujoco-sim2real_amd", "csrc", "soarm_sim.hip")
 
 if "--build" in sys.argv:
+    sys.path.insert(0, ROOT)
+    import soarm_pkg  # noqa: F401
+    from lerobot_mujoco_sim2real_amd.build import FLAGS, HIPCC
+
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
-    subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-                           "-DSOARM_PHASE_PROF", "-o", LIB, SRC])
+    subprocess.check_call([HIPCC] + FLAGS + ["-DSOARM_PHASE_PROF", "-o", LIB, SRC])
     sys.exit(0)
 
 sys.path.insert(0, ROOT)
