@@ -119,7 +119,7 @@ def load_lib(path=None):
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = path or LIB_PATH
+    p = path or os.environ.get("SOARM_SIM_LIB") or LIB_PATH  # env override: A/B builds (tools/)
     if not os.path.exists(p):
         raise RuntimeError(
             f"HIP library {p} not built; run `python __graft_entry__.py` (build()) first")
