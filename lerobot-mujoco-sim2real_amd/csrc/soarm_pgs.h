@@ -26,6 +26,8 @@
 // (measured on the oracle with MuJoCo's improvement criterion), so the sweep
 // body is the hot loop of the contact scene.
 #pragma once
+#include <type_traits>
+
 #include "soarm_collide.h"
 
 namespace soarm {
@@ -584,6 +586,44 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
         return;
       }
     }
+    if (__all(!((int)L.at(c, F_FLAGS) & TOUCH_FREE))) {
+      // arm-only contact (link vs table / floor / link): NA-dof dots, one arm-block
+      // M^-1 product per sweep
+      float jn[NA], j1[NA], j2[NA];
+#pragma unroll
+      for (int i = 0; i < NA; i++) jn[i] = L.at(c, i), j1[i] = L.at(c, 12 + i), j2[i] = L.at(c, 24 + i);
+      float a = 0.f, b = 0.f, cc = 0.f;
+#pragma unroll
+      for (int i = 0; i < NA; i++) a += jn[i] * v[i], b += j1[i] * v[i], cc += j2[i] * v[i];
+      float df[4];
+#pragma unroll
+      for (int ed = 0; ed < 4; ed++) {
+        const float s = (ed & 1) ? -mu : mu;
+        const float res = (a + s * ((ed >> 1) ? cc : b)) - ar[ed] + Rp * fo[ed];
+        const float fnew = fmaxf(fo[ed] - res * ia[ed], 0.f);
+        df[ed] = fnew - fo[ed];
+        a += cf[3 * ed] * df[ed];
+        b += cf[3 * ed + 1] * df[ed];
+        cc += cf[3 * ed + 2] * df[ed];
+        improvement -= df[ed] * (res + hd[ed] * df[ed]);
+        fo[ed] = fnew;
+      }
+      const float Dn = (df[0] + df[1]) + (df[2] + df[3]);
+      const float D1 = mu * (df[0] - df[1]), D2 = mu * (df[2] - df[3]);
+      float u[NA];
+#pragma unroll
+      for (int i = 0; i < NA; i++) u[i] = jn[i] * Dn + j1[i] * D1 + j2[i] * D2;
+#pragma unroll
+      for (int i = 0; i < NA; i++) {
+        float w = 0.f;
+#pragma unroll
+        for (int k = 0; k < NA; k++) w += Mi.a(i, k) * u[k];
+        v[i] += w;
+      }
+#pragma unroll
+      for (int ed = 0; ed < 4; ed++) L.at(c, F_FRC + ed) = fo[ed];
+      return;
+    }
     // the record holds zeros in the halves the contact does not touch: full-width,
     // branch-free dots (divergent half-selection would run both sides anyway)
     float jn[NV], j1[NV], j2[NV];
@@ -708,27 +748,33 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   // arm row before it: run it beside the friction rows so the two independent chains
   // share one straight-line region, then limits and the remaining contacts.
   const bool block_first = __all(npre == 0);
-  for (int it = 0; it < m.iterations; it++) {
-    float improvement = 0.f;
-    if (block_first) {
-      fric_rows(improvement);
-      block_rows(improvement);
-      limit_rows(improvement);
-    } else {
-      fric_rows(improvement);
-      limit_rows(improvement);
-      for (int c = 0; c < npre; c++) lds_contact(c, improvement);
-      block_rows(improvement);
-    }
-    for (int j = 0; j < npost; j++) lds_contact(j < c0 - npre ? npre + j : c1 + j - (c0 - npre), improvement);
-    scratch_rows(improvement);
-    if (improvement * scale < m.tolerance) {
+  auto sweeps = [&](auto first) {
+    for (int it = 0; it < m.iterations; it++) {
+      float improvement = 0.f;
+      if constexpr (decltype(first)::value) {
+        fric_rows(improvement);  // same basic block as the register block: they interleave
+        block_rows(improvement);
+        limit_rows(improvement);
+      } else {
+        fric_rows(improvement);
+        limit_rows(improvement);
+        for (int c = 0; c < npre; c++) lds_contact(c, improvement);
+        block_rows(improvement);
+      }
+      for (int j = 0; j < npost; j++) lds_contact(j < c0 - npre ? npre + j : c1 + j - (c0 - npre), improvement);
+      scratch_rows(improvement);
+      if (improvement * scale < m.tolerance) {
 #ifdef SOARM_PHASE_PROF
-      nsweep = it + 1;
+        nsweep = it + 1;
 #endif
-      break;
+        break;
+      }
     }
-  }
+  };
+  if (block_first)  // wave-uniform: two copies of the loop, no branch inside the sweep
+    sweeps(std::true_type{});
+  else
+    sweeps(std::false_type{});
   if constexpr (NF == 1 && CON) {
 #pragma unroll
     for (int k = 0; k < FC; k++)
