@@ -37,7 +37,7 @@ namespace soarm {
 __device__ long long g_pgs_prof[65536 * 8];
 #endif
 
-constexpr int LDS_CON = 8;  // contacts whose rows stay in LDS
+constexpr int LDS_CON = 7;  // contacts whose rows stay in LDS
 constexpr int CF = 61;      // LDS floats per contact record
 // record fields: [0, 3*12) J_n | J_t1 | J_t2 (12 slots each), 36..39 aref_e,
 // 40..43 ARdiag_e / 2, 44..47 force_e, 48..51 1/ARdiag_e, 52 mu, 53 R (pyramid),
@@ -45,6 +45,12 @@ constexpr int CF = 61;      // LDS floats per contact record
 // of a contact that touches only the free body (diagonal M^-1)
 enum { F_AREF = 36, F_HARD = 40, F_FRC = 44, F_IARD = 48, F_MU = 52, F_R = 53, F_FLAGS = 54, F_GRAM = 55 };
 enum { TOUCH_ARM = 1, TOUCH_FREE = 2 };
+// Sim state not used by the sweeps but needed after them (mass matrix blocks for the
+// implicit-damping solve, smooth forces, observed site): parked in LDS so the sweep's
+// register budget is not spent holding it.  Arm block packed (21) + free-body diagonals
+// (6 per free body; the free block is diagonal, host-validated) + qfrc_smooth + ee.
+template <int NA, int NF>
+constexpr int keep_floats() { return NA * (NA + 1) / 2 + 6 * NF + (NA + 6 * NF) + 3; }
 // joint-limit rows (rare): compact list, one record per active limit
 constexpr int LF = 7;  // dof, sign, aref, R, ARdiag, 1/ARdiag, force
 enum { L_DOF = 0, L_SGN = 1, L_AREF = 2, L_R = 3, L_ARD = 4, L_IARD = 5, L_FRC = 6 };
@@ -52,6 +58,7 @@ enum { L_DOF = 0, L_SGN = 1, L_AREF = 2, L_R = 3, L_ARD = 4, L_IARD = 5, L_FRC =
 struct RowLds {
   float (*a)[64];    // [(LDS_CON + 1) * CF][64] contact records + a zero record (null: contact-free kernel)
   float (*lim)[64];  // [NA * LF][64] active joint-limit records
+  float (*keep)[64]; // [KEEP][64] state held in LDS across the PGS sweeps (null: kept in registers)
   int lane;
   DEVI float& at(int c, int f) const { return a[c * CF + f][lane]; }
   DEVI float& lm(int l, int f) const { return lim[l * LF + f][lane]; }
@@ -527,6 +534,19 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
 #pragma unroll
     for (int i = 0; i < 6; i++) tr += S.MF[f2][i * (i + 1) / 2 + i];
   const float scale = 1.f / tr;
+  if (L.keep) {  // park what only the post-solve stages need (restored below)
+    int k = 0;
+#pragma unroll
+    for (int i = 0; i < NA * (NA + 1) / 2; i++) L.keep[k++][L.lane] = S.MA[i];
+#pragma unroll
+    for (int f2 = 0; f2 < NF; f2++)
+#pragma unroll
+      for (int i = 0; i < 6; i++) L.keep[k++][L.lane] = S.MF[f2][i * (i + 1) / 2 + i];
+#pragma unroll
+    for (int i = 0; i < NV; i++) L.keep[k++][L.lane] = S.fsmooth[i];
+#pragma unroll
+    for (int i = 0; i < 3; i++) L.keep[k++][L.lane] = S.ee[i];
+  }
 #ifdef SOARM_PHASE_PROF
   if (e < 65536) g_pgs_prof[8 * e] = clock64();
   int nsweep = m.iterations;
@@ -781,6 +801,21 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       if (k < nrun)
 #pragma unroll
         for (int ed = 0; ed < 4; ed++) L.at(c0 + k, F_FRC + ed) = cfo[k][ed];
+  }
+  if (L.keep) {
+    int k = 0;
+#pragma unroll
+    for (int i = 0; i < NA * (NA + 1) / 2; i++) S.MA[i] = L.keep[k++][L.lane];
+#pragma unroll
+    for (int f2 = 0; f2 < NF; f2++)
+#pragma unroll
+      for (int i = 0; i < 6; i++)
+#pragma unroll
+        for (int j = 0; j <= i; j++) S.MF[f2][i * (i + 1) / 2 + j] = (i == j) ? L.keep[k++][L.lane] : 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; i++) S.fsmooth[i] = L.keep[k++][L.lane];
+#pragma unroll
+    for (int i = 0; i < 3; i++) S.ee[i] = L.keep[k++][L.lane];
   }
 #ifdef SOARM_PHASE_PROF
   if (e < 65536)

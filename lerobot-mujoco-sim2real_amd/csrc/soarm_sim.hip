@@ -197,7 +197,7 @@ __global__ __launch_bounds__(64) void k_step(const DModel* __restrict__ dm, int 
       if (k < m.nact) S.ctrl[k] = action[(size_t)e * m.nact + k];
   }
   __shared__ float s_lim[NA * LF][64];
-  const RowLds L{nullptr, s_lim, (int)threadIdx.x};
+  const RowLds L{nullptr, s_lim, nullptr, (int)threadIdx.x};
   const ContactRows<NA, NF> cr{nullptr, n};
   for (int s = 0; s < nsub; s++) {
     S.relaunder();
@@ -301,10 +301,14 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
   }
   __shared__ float s_rows[(LDS_CON + 1) * CF][64];  // + one all-zero record
   __shared__ float s_lim[NA * LF][64];
-  const RowLds L{s_rows, s_lim, (int)threadIdx.x};
+  __shared__ float s_keep[keep_floats<NA, NF>()][64];
+  const RowLds L{s_rows, s_lim, NF == 1 ? s_keep : nullptr, (int)threadIdx.x};
   const ContactRows<NA, NF> cr{scratch + e, n};
   const int st0 = S.status;
   S.check_state();
+  // positions / velocities are re-read from HBM after the solve instead of being held in
+  // registers through it: a soft reset must reach HBM first
+  if (S.status != st0) store_state(S, st, n, e);
   // a soft reset moved the env: the collide output no longer applies
   const bool use = S.status == st0 && ccount != nullptr;
 #ifdef SOARM_PHASE_PROF
@@ -320,7 +324,17 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
 #endif
   if (S.acc_bad()) {
     S.soft_reset(SIM_ST_BADQACC);
+    store_state(S, st, n, e);
     ncon = forward<NA, NF, true>(S, nullptr, nullptr, nullptr, n, e, L, cr);
+  }
+  if constexpr (NF == 1) {  // reload (laundered pointers: not CSE'd with the first load)
+    const float* qp = st.qpos;
+    const float* qv = st.qvel;
+    asm volatile("" : "+s"(qp), "+s"(qv));
+#pragma unroll
+    for (int i = 0; i < Sim<NA, NF>::NQ; i++) S.qpos[i] = qp[(size_t)i * n + e];
+#pragma unroll
+    for (int i = 0; i < Sim<NA, NF>::NV; i++) S.qvel[i] = qv[(size_t)i * n + e];
   }
   if (pmask)  // consumed: clear for the next collide
     for (int w = 0; w < (m.npair + 31) >> 5; w++) pmask[(size_t)w * n + e] = 0u;
