@@ -713,16 +713,13 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   // registers: the block's forces (updated every sweep) and Gram columns; the rest is
   // re-read from LDS each sweep — those loads are independent of the Gauss-Seidel
   // chains, so in straight-line code they issue ahead of use
+  if constexpr (CON) {
+#pragma unroll
+    for (int f = 0; f < CF; f++) L.at(LDS_CON, f) = 0.f;  // the all-zero record (absent rows)
+  }
   float cfo[FC][4], ccf[FC][12];
   int cslot[FC];
   if constexpr (NF == 1 && CON) {
-#pragma unroll
-    for (int i = 0; i < 6; i++)  // the zero record: Jacobian, Gram, 1/ARdiag, ARdiag/2, aref, mu, R
-      L.at(LDS_CON, NA + i) = L.at(LDS_CON, 12 + NA + i) = L.at(LDS_CON, 24 + NA + i) = L.at(LDS_CON, F_GRAM + i) = 0.f;
-#pragma unroll
-    for (int ed = 0; ed < 4; ed++)
-      L.at(LDS_CON, F_IARD + ed) = L.at(LDS_CON, F_HARD + ed) = L.at(LDS_CON, F_AREF + ed) = 0.f;
-    L.at(LDS_CON, F_MU) = L.at(LDS_CON, F_R) = 0.f;
 #pragma unroll
     for (int k = 0; k < FC; k++) {
       const bool on = k < nrun;
@@ -768,21 +765,35 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   // arm row before it: run it beside the friction rows so the two independent chains
   // share one straight-line region, then limits and the remaining contacts.
   const bool block_first = __all(npre == 0);
-  auto sweeps = [&](auto first) {
+  // Arm slot: when every lane's only non-block row is (at most) one arm-only contact
+  // (a link touching the table) and no limit is active, the sweep runs it right after
+  // the block with no loop around it (lanes without one run the zero record): it
+  // commutes with the cube block and follows the friction rows, as in MuJoCo's order.
+  const int ca = npost == 1 ? (c0 - npre > 0 ? npre : c1) : LDS_CON;
+  bool arm_ok = nlim == 0 && nl == ncon && npost <= 1;
+  if (npost == 1) arm_ok = arm_ok && (int)L.at(ca, F_FLAGS) == TOUCH_ARM;
+  const bool arm_slot = CON && block_first && __all(arm_ok) && __any(npost == 1);
+  auto sweeps = [&](auto first, auto arm) {
     for (int it = 0; it < m.iterations; it++) {
       float improvement = 0.f;
-      if constexpr (decltype(first)::value) {
+      if constexpr (decltype(arm)::value) {
+        fric_rows(improvement);  // friction and cube block, then the single arm contact
+        block_rows(improvement);
+        lds_contact(ca, improvement);
+      } else if constexpr (decltype(first)::value) {
         fric_rows(improvement);  // same basic block as the register block: they interleave
         block_rows(improvement);
         limit_rows(improvement);
+        for (int j = 0; j < npost; j++) lds_contact(j < c0 - npre ? npre + j : c1 + j - (c0 - npre), improvement);
+        scratch_rows(improvement);
       } else {
         fric_rows(improvement);
         limit_rows(improvement);
         for (int c = 0; c < npre; c++) lds_contact(c, improvement);
         block_rows(improvement);
+        for (int j = 0; j < npost; j++) lds_contact(j < c0 - npre ? npre + j : c1 + j - (c0 - npre), improvement);
+        scratch_rows(improvement);
       }
-      for (int j = 0; j < npost; j++) lds_contact(j < c0 - npre ? npre + j : c1 + j - (c0 - npre), improvement);
-      scratch_rows(improvement);
       if (improvement * scale < m.tolerance) {
 #ifdef SOARM_PHASE_PROF
         nsweep = it + 1;
@@ -791,11 +802,15 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       }
     }
   };
-  if (block_first)  // wave-uniform: two copies of the loop, no branch inside the sweep
-    sweeps(std::true_type{});
-  else
-    sweeps(std::false_type{});
-  if constexpr (NF == 1 && CON) {
+  // wave-uniform choice: separate copies of the loop, no branch inside the sweep
+  if (arm_slot) {
+    sweeps(std::true_type{}, std::true_type{});
+  } else if (block_first) {
+    sweeps(std::true_type{}, std::false_type{});
+  } else {
+    sweeps(std::false_type{}, std::false_type{});
+  }
+  if constexpr (NF == 1 && CON) {  // the block's forces back to their records (for J' f)
 #pragma unroll
     for (int k = 0; k < FC; k++)
       if (k < nrun)
