@@ -231,6 +231,97 @@ def test_one_substep_with_contacts(gpu_lib, cube_model):
     assert to_np(S.ncon).sum() == st["ncon"].sum()
 
 
+def _bench_states(name, n, steps, seed=0):
+    """Oracle states of a bench workload after `steps` env-steps (chirp inputs), fp32-rounded."""
+    from lerobot_mujoco_sim2real_amd import workloads as W
+    cm = W.model(name)
+    orc = Oracle(cm)
+    ids = np.arange(n)
+    st = orc.new_state(n)
+    q = W.initial_qpos(cm, ids, seed)
+    orc.reset(st, init_qpos=q[:, :5], extra_qpos=q)
+    tab = W.chirp_tables(ids, seed)
+    prm = None
+    if W.CONFIGS[name]["dr"]:
+        p = W.dr_params(ids, seed)
+        prm = np.stack([p["mass_scale"], p["friction"], p["damping_scale"]], 1).astype(np.float32).astype(np.float64)
+    for t in range(steps):
+        orc.step(st, W.chirp_action(tab, t), params=prm, nthreads=8)
+    return cm, orc, f32(st), prm
+
+
+def test_one_substep_bench_state_mixed_contacts(gpu_lib):
+    """One substep from late bench states (t = 120 env-steps of the contact workload): the
+    cube's 4 resting contacts plus, in some envs, arm-table contacts (the waves that take
+    the general contact paths)."""
+    cm, orc, st, _ = _bench_states("contact", 512, 120)
+    S = make_sim(cm, 512)
+    st["ncon"][:] = 0
+    load_state(S, st)
+    S.substeps(1)
+    orc.step(st, None, nsub=1)
+    assert st["ncon"].sum() > 4 * 512, "no arm contacts in the sample"
+    np.testing.assert_allclose(to_np(S.qpos).T, st["qpos"], atol=5e-6)
+    np.testing.assert_allclose(to_np(S.qvel).T, st["qvel"], atol=5e-3)
+    assert to_np(S.ncon).sum() == st["ncon"].sum()
+
+
+def test_one_substep_domain_randomised(gpu_lib):
+    """Config 4 DR (mass, friction, damping per env) through sim_batch_set_params."""
+    from lerobot_mujoco_sim2real_amd import workloads as W
+    cm, orc, st, prm = _bench_states("dr", 512, 10)
+    S = make_sim(cm, 512)
+    S.set_params(mass_scale=prm[:, 0], friction=prm[:, 1], damping_scale=prm[:, 2])
+    st["ncon"][:] = 0
+    load_state(S, st)
+    S.substeps(1)
+    orc.step(st, None, nsub=1, params=prm)
+    np.testing.assert_allclose(to_np(S.qpos).T, st["qpos"], atol=5e-6)
+    np.testing.assert_allclose(to_np(S.qvel).T, st["qvel"], atol=5e-3)
+    assert to_np(S.ncon).sum() == st["ncon"].sum()
+
+
+@pytest.mark.parametrize("n", [1, 100])
+def test_odd_batch_sizes(gpu_lib, cube_model, n):
+    """Batches that are not a multiple of the 64-lane wave (tail lanes masked)."""
+    cm = cube_model
+    S, orc = make_sim(cm, n), Oracle(cm)
+    st = orc.new_state(n)
+    orc.reset(st, init_qpos=RNG.uniform(-0.3, 0.3, (n, 5)), extra_qpos=cube_qpos(cm, n, RNG))
+    for _ in range(3):
+        orc.step(st, RNG.uniform(-0.5, 0.5, (n, 5)))
+    st = f32(st)
+    st["ncon"][:] = 0
+    load_state(S, st)
+    S.substeps(1)
+    orc.step(st, None, nsub=1)
+    np.testing.assert_allclose(to_np(S.qpos).T, st["qpos"], atol=5e-6)
+    np.testing.assert_allclose(to_np(S.qvel).T, st["qvel"], atol=5e-3)
+
+
+def test_ik_rollout_tracks_fig8(gpu_lib):
+    """Config 5 (IK-in-the-loop DataCollection): the end effector follows its Fig8 target."""
+    import torch
+    from lerobot_mujoco_sim2real_amd import workloads as W
+    from lerobot_mujoco_sim2real_amd.sim import BatchSim
+    cm = W.model("rollout")
+    n, T = 256, 120
+    ids = np.arange(n)
+    S = BatchSim(cm, n)
+    q0 = W.initial_qpos(cm, ids)
+    obs = S.reset(init_qpos=q0[:, :5])
+    phase = torch.as_tensor(W.ik_phase(ids), dtype=torch.float32, device=S.device)
+    qstar = S.qpos.clone()
+    err = []
+    for t in range(T):
+        tgt = W.fig8_targets(float(t), phase, lib=torch)
+        qstar, ok, _ = S.ik(tgt, q=qstar)
+        a = W.ik_action(qstar[:5].T, obs[:, 3:8], lib=torch)
+        obs = S.step(a)
+        err.append(torch.linalg.norm(obs[:, :3] - tgt, dim=1).median().item())
+    assert err[-1] < 0.02 and err[-1] < 0.5 * err[0], err[::20]
+
+
 def test_cube_rests_gpu(gpu_lib, cube_model):
     cm = cube_model
     n = 256
