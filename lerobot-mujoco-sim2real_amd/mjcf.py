@@ -40,6 +40,9 @@ from . import abi
 ASSET_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "assets", "so101")
 SCENE_XML = os.path.join(ASSET_DIR, "scene_with_table_v.xml")
 CUBE_SCENE_XML = os.path.join(ASSET_DIR, "scene_with_table_cube_v.xml")
+# position-servo scenes (kp = 50 class default, forcerange +-33.5) of the viewer / sim2real scripts
+POSITION_SCENE_XML = os.path.join(ASSET_DIR, "scene_with_table.xml")
+FLOOR_SCENE_XML = os.path.join(ASSET_DIR, "scene.xml")
 
 # MuJoCo defaults (mjmodel.h / user_objects docs)
 DEF_SOLREF = (0.02, 1.0)

@@ -95,3 +95,20 @@ def test_hull_graph_consistency(arm_model):
         nb = cm.hull_adj[adr[0]: adr[-1]]
         assert nb.min() >= 0 and nb.max() < n
         assert np.all(np.diff(adr) >= 3)  # every hull vertex has >= 3 neighbours
+
+
+def test_position_servo_scenes():
+    """the position-servo scenes of the viewer / sim2real scripts
+    (scene_with_table.xml: so101_new_calib.xml:167-172, <position> with the class default
+    kp = 50 and forcerange +-33.5; scene.xml: floor only)."""
+    from lerobot_mujoco_sim2real_amd import mjcf
+    cm = mjcf.compile_mjcf(mjcf.POSITION_SCENE_XML)
+    d = cm.desc
+    assert (d.nq, d.nv, d.nu) == (6, 6, 6) and d.npair == 71
+    for a in range(6):
+        assert d.actuator_gainprm[a] == 50.0
+        assert list(d.actuator_biasprm[a]) == [0.0, -50.0, 0.0]
+        assert list(d.actuator_forcerange[a]) == [-33.5, 33.5]
+    assert abs(d.actuator_ctrlrange[0][1] - 1.91986) < 1e-9
+    cf = mjcf.compile_mjcf(mjcf.FLOOR_SCENE_XML)
+    assert cf.desc.nu == 6 and cf.desc.npair == 58  # 45 self pairs + 13 floor pairs

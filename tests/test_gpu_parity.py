@@ -322,6 +322,26 @@ def test_ik_rollout_tracks_fig8(gpu_lib):
     assert err[-1] < 0.02 and err[-1] < 0.5 * err[0], err[::20]
 
 
+def test_position_servo_scene_substep(gpu_lib):
+    """The position-servo scene (kp = 50, force +-33.5), arm-table contacts on."""
+    from lerobot_mujoco_sim2real_amd import mjcf
+    cm = mjcf.compile_mjcf(mjcf.POSITION_SCENE_XML)
+    n = 256
+    orc = Oracle(cm)
+    st = orc.new_state(n)
+    orc.reset(st, init_qpos=RNG.uniform(-0.5, 0.5, (n, 5)))
+    for _ in range(3):
+        orc.step(st, RNG.uniform(-0.5, 0.5, (n, 5)))
+    st = f32(st)
+    S = make_sim(cm, n)
+    st["ncon"][:] = 0
+    load_state(S, st)
+    S.substeps(1)
+    orc.step(st, None, nsub=1)
+    np.testing.assert_allclose(to_np(S.qpos).T, st["qpos"], atol=2e-6)
+    np.testing.assert_allclose(to_np(S.qvel).T, st["qvel"], atol=1e-3)
+
+
 def test_cube_rests_gpu(gpu_lib, cube_model):
     cm = cube_model
     n = 256

@@ -27,7 +27,10 @@ from scipy.spatial import ConvexHull
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 OUT = os.path.join(HERE, "..", "lerobot-mujoco-sim2real_amd", "assets", "so101")
-XMLS = ["scene_with_table_v.xml", "so101_new_calib_v.xml"]
+# the hot path's scene (velocity servos) and, for the position-servo scenes the viewer /
+# sim2real scripts load, scene_with_table.xml + scene.xml
+XMLS = ["scene_with_table_v.xml", "so101_new_calib_v.xml", "scene_with_table.xml", "so101_new_calib.xml",
+        "scene.xml"]
 
 
 def read_stl(path):
@@ -69,11 +72,13 @@ def hull_with_graph(verts_f32):
     return pts[hv].astype(np.float32), np.asarray(adj, dtype=np.int32), adr
 
 
-def main(ref_root):
+def main(ref_root, xml_only=False):
     src = os.path.join(ref_root, "SOARM101", "SO101")
     os.makedirs(OUT, exist_ok=True)
     for x in XMLS:
         shutil.copyfile(os.path.join(src, x), os.path.join(OUT, x))
+    if xml_only:
+        return
     arrays = {}
     for f in sorted(os.listdir(os.path.join(src, "assets"))):
         if not f.endswith(".stl"):
@@ -90,4 +95,5 @@ def main(ref_root):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "/root/reference")
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    main(args[0] if args else "/root/reference", xml_only="--xml-only" in sys.argv)
