@@ -342,6 +342,37 @@ def test_position_servo_scene_substep(gpu_lib):
     np.testing.assert_allclose(to_np(S.qvel).T, st["qvel"], atol=1e-3)
 
 
+def test_generate_and_save_data_cache(gpu_lib, tmp_path):
+    """SOARM101_DataCollection.py:138-181: .npy cache names / shapes / dtype, resume from
+    the cache, and the Collater split the Koopman trainer consumes (x = [5:13], u = [0:5])."""
+    import os
+    from lerobot_mujoco_sim2real_amd.args import Args
+    from lerobot_mujoco_sim2real_amd.SOARM101.SOARM101_DataCollection import SOARM101DataGenerator
+    a = Args(["--data_root", str(tmp_path), "--train_samples", "96", "--train_steps", "5",
+              "--test_samples", "32", "--test_steps", "7", "--batch_size", "16", "--eval_batch_size", "8"])
+    g = SOARM101DataGenerator(a)
+    g.generate_and_save_data()
+    d = os.path.join(str(tmp_path), "SOARM101", "data")
+    names = sorted(os.listdir(d))
+    assert names == sorted(["train_data_96_5.npy", "val_data_32_7.npy", "test_data_random_32_7.npy",
+                            "test_data_sin_32_7.npy", "test_data_chirp_32_7.npy"]), names
+    assert g.train_data.shape == (96, 6, 13) and g.train_data.dtype == np.float64
+    assert g.val_data.shape == (32, 8, 13)
+    for t in ("random", "sin", "chirp"):
+        assert g.test_data_dict[t].shape == (32, 8, 13)
+    assert np.abs(g.train_data[:, :, :5]).max() <= 0.5 + 1e-6
+    mt = {n: os.path.getmtime(os.path.join(d, n)) for n in names}
+    g2 = SOARM101DataGenerator(a)
+    g2.generate_and_save_data()  # resumes from the cache
+    assert {n: os.path.getmtime(os.path.join(d, n)) for n in names} == mt
+    np.testing.assert_array_equal(g2.train_data, g.train_data)
+    tr, va = g2.get_train_loader()
+    b = next(iter(tr))
+    assert tuple(b["x"].shape) == (16, 6, 8) and tuple(b["u"].shape) == (16, 6, 5)
+    tb = next(iter(g2.get_test_loader("chirp")))
+    assert tuple(tb["x"].shape) == (8, 8, 8)
+
+
 def test_cube_rests_gpu(gpu_lib, cube_model):
     cm = cube_model
     n = 256
