@@ -104,7 +104,7 @@ def main():
     from lerobot_mujoco_sim2real_amd import build, workloads as W
     from lerobot_mujoco_sim2real_amd.sim import BatchSim
 
-    build.build()
+    build.ensure_built(local)
     gpu = local % max(torch.cuda.device_count(), 1)  # > 1 rank per GPU only in gloo rehearsals
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)

@@ -27,8 +27,28 @@ def build(force=False, verbose=False):
     """Build csrc/libsoarm_sim.so if missing or older than its sources."""
     if not force and not _stale():
         return LIB_PATH
-    cmd = [HIPCC] + FLAGS + ["-o", LIB_PATH] + [os.path.join(SRC_DIR, s) for s in SOURCES]
+    tmp = f"{LIB_PATH}.{os.getpid()}.tmp"
+    cmd = [HIPCC] + FLAGS + ["-o", tmp] + [os.path.join(SRC_DIR, s) for s in SOURCES]
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd, cwd=SRC_DIR)
+    os.replace(tmp, LIB_PATH)  # atomic: concurrent loaders never see a partial file
+    return LIB_PATH
+
+
+def ensure_built(local_rank=0, timeout_s=600):
+    """Multi-process entry (bench under torch.distributed.run): never rebuild a library
+    that exists (file times may not survive a copy to another box); if it is missing,
+    local rank 0 builds it and the other ranks wait for it."""
+    import time
+
+    if os.path.exists(LIB_PATH):
+        return LIB_PATH
+    if local_rank == 0:
+        return build(force=True)
+    t0 = time.time()
+    while not os.path.exists(LIB_PATH):
+        if time.time() - t0 > timeout_s:
+            raise RuntimeError(f"{LIB_PATH} did not appear (built by local rank 0)")
+        time.sleep(1.0)
     return LIB_PATH
