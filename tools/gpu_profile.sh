@@ -28,7 +28,7 @@ step bench_nocontact 300 python bench.py --config nocontact --steps 200 --warmup
 step bench_dr 600 python bench.py --config dr --steps 50 --warmup 5 --cpu-seconds 8 > $O/bench_dr.json 2> $O/bench_dr.err
 step bench_rollout 600 python bench.py --config rollout --steps 100 --warmup 5 --cpu-seconds 8 > $O/bench_rollout.json 2> $O/bench_rollout.err
 cd /tmp
-step kernel_trace 600 rocprofv3 --kernel-trace --stats -f csv -d $O/prof_$TAG -o trace -- python3 $R/bench.py --steps 30 --warmup 5 --no-cpu-baseline > $O/bench_contact_traced.json
+step kernel_trace 600 rocprofv3 --kernel-trace --stats -f csv -d $O/prof_$TAG -o trace -- python3 $R/bench.py --no-cpu-baseline > $O/bench_contact_traced.json
 step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_substep|k_collide|k_step|k_geom" -f csv -d $O/prof_$TAG -o pmc_fetch -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-profile
 step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_substep|k_collide|k_step|k_geom" -f csv -d $O/prof_$TAG -o pmc_write -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-profile
 step pmc_sq 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY --kernel-include-regex "k_substep|k_collide|k_step|k_geom" -f csv -d $O/prof_$TAG -o pmc_sq -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-profile
