@@ -86,9 +86,30 @@ def cpu_baseline(cfg_name, seconds, seed):
             done += n
         chunk += 1
     dt = time.perf_counter() - t0
+    # the same oracle on ONE core (SURVEY 8d asks for both), a shorter sample of chunk 0's envs
+    st = orc.new_state(64)
+    q = W.initial_qpos(cm, np.arange(64), seed)
+    orc.reset(st, init_qpos=q[:, :5], extra_qpos=q)
+    tab = W.chirp_tables(np.arange(64), seed)
+    d1, t1 = 0, time.perf_counter()
+    while time.perf_counter() - t1 < max(1.0, seconds / 4):
+        a = W.chirp_action(tab, d1 // 64) if cfg["action"] == "chirp" else np.zeros((64, 5))
+        orc.step(st, a, nthreads=1)
+        d1 += 64
+    t1 = time.perf_counter() - t1
+    cpu_name = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu_name = next(ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name"))
+    except (OSError, StopIteration):
+        pass
+    import importlib.util
+    mj = "available (not used)" if importlib.util.find_spec("mujoco") else "MuJoCo unavailable"
     return {"value": done / dt, "unit": "env-steps/s", "cores": cores, "kind": "port",
             "sample": f"{done} env-steps ({chunk} chunks of {n} envs x {T} steps, {cfg_name} workload) "
-                      f"of the float64 C oracle, OpenMP over envs, {dt:.1f} s"}
+                      f"of the float64 C oracle, OpenMP over envs, {dt:.1f} s",
+            "single_core": {"value": d1 / t1, "sample": f"{d1} env-steps of 64 envs on 1 thread, {t1:.1f} s"},
+            "cpu_model": cpu_name, "nproc": os.cpu_count(), "mujoco": mj}
 
 
 def main():
