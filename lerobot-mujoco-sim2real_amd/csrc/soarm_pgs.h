@@ -35,6 +35,12 @@ namespace soarm {
 #ifdef SOARM_PHASE_PROF
 // diagnostic build only: per-env PGS start/end clock, sweep count, fast-path flag (env < 65536)
 __device__ long long g_pgs_prof[65536 * 8];
+// fine-grained per-env clock stamps of one k_substep (diagnostic build): see k_substep
+__device__ long long g_stamp[65536 * 16];
+#define PSTAMP(k) \
+  if (e < 65536) g_stamp[16 * e + (k)] = clock64()
+#else
+#define PSTAMP(k)
 #endif
 
 constexpr int LDS_CON = 7;  // contacts whose rows stay in LDS
@@ -233,6 +239,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   S.solve_m(S.qacc_s, S.fsmooth);
   MInv<NA, NF> Mi;
   Mi.build(S);
+  PSTAMP(6);
 
   // ---- dof frictionloss rows (MuJoCo row order: all of them first)
   float ff[NA], fa[NA], fR[NA], fhD[NA], fiD[NA];
@@ -267,6 +274,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
     }
   }
 
+  PSTAMP(7);
   // ---- contact rows, straight from the collide output in pair order
   int ncon = 0;
   if constexpr (CON) {
@@ -408,6 +416,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   const int nl = ncon < LDS_CON ? ncon : LDS_CON;
 #ifdef SOARM_PHASE_PROF
   if (e < 65536) g_pgs_prof[8 * e + 6] = clock64();  // rows built
+  PSTAMP(8);
 #endif
 
   // ---- warm start from qacc_warmstart (forces implied by the primal), keep if it beats f = 0
@@ -549,6 +558,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   }
 #ifdef SOARM_PHASE_PROF
   if (e < 65536) g_pgs_prof[8 * e] = clock64();
+  PSTAMP(9);
   int nsweep = m.iterations;
 #endif
   // dof-frictionloss rows (J = e_i): one pass.  Branch-free: a dof with frictionloss 0
@@ -580,6 +590,43 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       improvement -= df * (res + 0.5f * L.lm(l, L_ARD) * df);
     }
   };
+  // arm-only contact c: NA-dof dots, the 4-edge chain, one arm-block M^-1 product
+  auto arm_v = [&](int c, float mu, float Rp, const float* cf, float* fo, const float* ar, const float* ia,
+                   const float* hd, float& improvement) {
+    float jn[NA], j1[NA], j2[NA];
+#pragma unroll
+    for (int i = 0; i < NA; i++) jn[i] = L.at(c, i), j1[i] = L.at(c, 12 + i), j2[i] = L.at(c, 24 + i);
+    float a = 0.f, b = 0.f, cc = 0.f;
+#pragma unroll
+    for (int i = 0; i < NA; i++) a += jn[i] * v[i], b += j1[i] * v[i], cc += j2[i] * v[i];
+    float df[4];
+#pragma unroll
+    for (int ed = 0; ed < 4; ed++) {
+      const float s = (ed & 1) ? -mu : mu;
+      const float res = (a + s * ((ed >> 1) ? cc : b)) - ar[ed] + Rp * fo[ed];
+      const float fnew = fmaxf(fo[ed] - res * ia[ed], 0.f);
+      df[ed] = fnew - fo[ed];
+      a += cf[3 * ed] * df[ed];
+      b += cf[3 * ed + 1] * df[ed];
+      cc += cf[3 * ed + 2] * df[ed];
+      improvement -= df[ed] * (res + hd[ed] * df[ed]);
+      fo[ed] = fnew;
+    }
+    const float Dn = (df[0] + df[1]) + (df[2] + df[3]);
+    const float D1 = mu * (df[0] - df[1]), D2 = mu * (df[2] - df[3]);
+    float u[NA];
+#pragma unroll
+    for (int i = 0; i < NA; i++) u[i] = jn[i] * Dn + j1[i] * D1 + j2[i] * D2;
+#pragma unroll
+    for (int i = 0; i < NA; i++) {
+      float w = 0.f;
+#pragma unroll
+      for (int k = 0; k < NA; k++) w += Mi.a(i, k) * u[k];
+      v[i] += w;
+    }
+#pragma unroll
+    for (int ed = 0; ed < 4; ed++) L.at(c, F_FRC + ed) = fo[ed];
+  };
   // contact c from its LDS record, in Gram form: a 6-dof free-body update when
   // (wave-uniformly) it touches only the free body, otherwise full-width dots and one
   // M^-1 product per sweep for the velocity update
@@ -609,39 +656,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
     if (__all(!((int)L.at(c, F_FLAGS) & TOUCH_FREE))) {
       // arm-only contact (link vs table / floor / link): NA-dof dots, one arm-block
       // M^-1 product per sweep
-      float jn[NA], j1[NA], j2[NA];
-#pragma unroll
-      for (int i = 0; i < NA; i++) jn[i] = L.at(c, i), j1[i] = L.at(c, 12 + i), j2[i] = L.at(c, 24 + i);
-      float a = 0.f, b = 0.f, cc = 0.f;
-#pragma unroll
-      for (int i = 0; i < NA; i++) a += jn[i] * v[i], b += j1[i] * v[i], cc += j2[i] * v[i];
-      float df[4];
-#pragma unroll
-      for (int ed = 0; ed < 4; ed++) {
-        const float s = (ed & 1) ? -mu : mu;
-        const float res = (a + s * ((ed >> 1) ? cc : b)) - ar[ed] + Rp * fo[ed];
-        const float fnew = fmaxf(fo[ed] - res * ia[ed], 0.f);
-        df[ed] = fnew - fo[ed];
-        a += cf[3 * ed] * df[ed];
-        b += cf[3 * ed + 1] * df[ed];
-        cc += cf[3 * ed + 2] * df[ed];
-        improvement -= df[ed] * (res + hd[ed] * df[ed]);
-        fo[ed] = fnew;
-      }
-      const float Dn = (df[0] + df[1]) + (df[2] + df[3]);
-      const float D1 = mu * (df[0] - df[1]), D2 = mu * (df[2] - df[3]);
-      float u[NA];
-#pragma unroll
-      for (int i = 0; i < NA; i++) u[i] = jn[i] * Dn + j1[i] * D1 + j2[i] * D2;
-#pragma unroll
-      for (int i = 0; i < NA; i++) {
-        float w = 0.f;
-#pragma unroll
-        for (int k = 0; k < NA; k++) w += Mi.a(i, k) * u[k];
-        v[i] += w;
-      }
-#pragma unroll
-      for (int ed = 0; ed < 4; ed++) L.at(c, F_FRC + ed) = fo[ed];
+      arm_v(c, mu, Rp, cf, fo, ar, ia, hd, improvement);
       return;
     }
     // the record holds zeros in the halves the contact does not touch: full-width,
@@ -742,6 +757,11 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   for (int c = 0; c < c0; c++)
     if ((int)L.at(c, F_FLAGS) & TOUCH_FREE) npre = c0;
   const int npost = (c0 - npre) + (nl - c1);
+#ifdef SOARM_PHASE_PROF
+  bool npost_free = false;  // a non-block contact touches the free body
+  for (int c = 0; c < nl; c++)
+    if ((c < c0 || c >= c1) && ((int)L.at(c, F_FLAGS) & TOUCH_FREE)) npost_free = true;
+#endif
   // the block's sweep (straight-line: one basic block with the friction rows)
   auto block_rows = [&](float& improvement) {
     if constexpr (NF == 1 && CON) {
@@ -773,6 +793,207 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   bool arm_ok = nlim == 0 && nl == ncon && npost <= 1;
   if (npost == 1) arm_ok = arm_ok && (int)L.at(ca, F_FLAGS) == TOUCH_ARM;
   const bool arm_slot = CON && block_first && __all(arm_ok) && __any(npost == 1);
+  // ---- contact-space ("y") sweep of the register block, used when nothing else in the
+  // wave touches the free body (every lane: no limits, no overflow rows, no non-block
+  // contact other than at most one arm-only one).  Each block contact k keeps
+  // y_k = (J_n v, J_t1 v, J_t2 v) of the free body's velocity, shifted by its reference
+  // acceleration: a pyramid edge's aref is affine in the same directions,
+  // aref_e = alpha + s_e beta_k (s_e = +-mu), so res_e = (a - alpha) + s_e (t_k - beta_k)
+  // + R f_e.  A force step on contact j moves every other y_k by the 3x3 cross-Gram
+  // block J_k M^-1 J_j' (the free block of M is diagonal, host-validated) — 27 FMAs per
+  // contact instead of the three 6-dof dots and the 6-dof velocity update of the v form;
+  // the velocity is rebuilt once from the force change after the sweeps.  Same
+  // Gauss-Seidel sequence (MuJoCo's mj_solPGS row order) in exact arithmetic.
+  constexpr int NX = FC * (FC - 1) / 2;
+  float yb[FC][3], xg[NX > 0 ? NX : 1][9];
+  auto ypair = [](int j, int k) { return j * FC - j * (j + 1) / 2 + (k - j - 1); };  // j < k
+  auto yblock_setup = [&]() {
+    if constexpr (NF == 1 && CON) {
+#pragma unroll
+      for (int k = 0; k < FC; k++) {
+        const int c = cslot[k];
+        float ar[4];
+#pragma unroll
+        for (int ed = 0; ed < 4; ed++) ar[ed] = L.at(c, F_AREF + ed);
+        const float mu = L.at(c, F_MU);
+        const float sh[3] = {0.5f * (ar[0] + ar[1]), mu > 0.f ? 0.5f * (ar[0] - ar[1]) / mu : 0.f,
+                             mu > 0.f ? 0.5f * (ar[2] - ar[3]) / mu : 0.f};
+#pragma unroll
+        for (int q = 0; q < 3; q++) {
+          float s = 0.f;
+#pragma unroll
+          for (int i = 0; i < 6; i++) s = fmaf(L.at(c, 12 * q + NA + i), v[NA + i], s);
+          yb[k][q] = s - sh[q];
+        }
+      }
+      // cross-Gram blocks, one pair at a time (rows re-read from LDS: setup only)
+#pragma unroll
+      for (int j = 0; j < FC; j++)
+#pragma unroll
+        for (int k = j + 1; k < FC; k++) {
+          float wk[3][6];
+#pragma unroll
+          for (int q = 0; q < 3; q++)
+#pragma unroll
+            for (int i = 0; i < 6; i++) wk[q][i] = Mi.Fd[0][i] * L.at(cslot[k], 12 * q + NA + i);
+#pragma unroll
+          for (int r = 0; r < 3; r++) {
+            float jj[6];
+#pragma unroll
+            for (int i = 0; i < 6; i++) jj[i] = L.at(cslot[j], 12 * r + NA + i);
+#pragma unroll
+            for (int cc = 0; cc < 3; cc++) {
+              float s = 0.f;
+#pragma unroll
+              for (int i = 0; i < 6; i++) s = fmaf(jj[i], wk[cc][i], s);
+              xg[ypair(j, k)][3 * r + cc] = s;  // J_j[r] M^-1 J_k[cc]'
+            }
+          }
+        }
+    }
+  };
+  // per-sweep constants of the block in registers: 1/ARdiag, ARdiag/2, mu, R, the
+  // off-diagonal edge-Gram entries A_ed = J_e M^-1 J_d' (d < e) and the 3x3 Gram block
+  float yia[FC][4], yhd[FC][4], ymu[FC], yRp[FC], yA[FC][6], yG[FC][6];
+  auto yblock_consts = [&]() {
+    if constexpr (NF == 1 && CON) {
+#pragma unroll
+      for (int k = 0; k < FC; k++) {
+        const int c = cslot[k];
+#pragma unroll
+        for (int ed = 0; ed < 4; ed++) yia[k][ed] = L.at(c, F_IARD + ed), yhd[k][ed] = L.at(c, F_HARD + ed);
+        ymu[k] = L.at(c, F_MU), yRp[k] = L.at(c, F_R);
+#pragma unroll
+        for (int i = 0; i < 6; i++) yG[k][i] = L.at(c, F_GRAM + i);
+        // edge e = J_n + s_e J_t(e): s = +mu, -mu, +mu, -mu; t = 1, 1, 2, 2
+        const float* G = yG[k];
+        const float mu = ymu[k];
+        auto gt = [&](int e) { return (e >> 1) ? G[2] : G[1]; };                  // G_n,t(e)
+        auto gtt = [&](int e, int d) {                                          // G_t(e),t(d)
+          const int te = e >> 1, td = d >> 1;
+          return te == td ? (te ? G[5] : G[3]) : G[4];
+        };
+        auto sg = [&](int e) { return (e & 1) ? -mu : mu; };
+        int q = 0;
+#pragma unroll
+        for (int ed = 1; ed < 4; ed++)
+#pragma unroll
+          for (int d = 0; d < ed; d++)
+            yA[k][q++] = G[0] + sg(ed) * gt(ed) + sg(d) * gt(d) + sg(ed) * sg(d) * gtt(ed, d);
+      }
+    }
+  };
+  // One sweep over the block.  Per contact the 4 edges are a 4x4 Gauss-Seidel on the
+  // edge Gram matrix: every residual starts from the contact's y, and each force step
+  // adds A_ed df_d to the later edges' residuals, so the dependent chain per edge is
+  // mul -> max -> fma (df = max(-res/ARdiag, -f) is the projected step f' - f).
+  auto yblock_rows = [&](float& improvement) {
+    if constexpr (NF == 1 && CON) {
+#pragma unroll
+      for (int j = 0; j < FC; j++) {
+        const float a = yb[j][0], b = yb[j][1], cc = yb[j][2];
+        const float mu = ymu[j], Rp = yRp[j];
+        float r[4], df[4];
+        r[0] = fmaf(Rp, cfo[j][0], fmaf(mu, b, a));
+        r[1] = fmaf(Rp, cfo[j][1], fmaf(-mu, b, a));
+        r[2] = fmaf(Rp, cfo[j][2], fmaf(mu, cc, a));
+        r[3] = fmaf(Rp, cfo[j][3], fmaf(-mu, cc, a));
+        int q = 0;
+#pragma unroll
+        for (int ed = 0; ed < 4; ed++) {
+#pragma unroll
+          for (int d = 0; d < ed; d++) r[ed] = fmaf(yA[j][q++], df[d], r[ed]);
+          df[ed] = fmaxf(r[ed] * -yia[j][ed], -cfo[j][ed]);
+        }
+#pragma unroll
+        for (int ed = 0; ed < 4; ed++) {
+          cfo[j][ed] += df[ed];
+          improvement = fmaf(-df[ed], fmaf(yhd[j][ed], df[ed], r[ed]), improvement);
+        }
+        const float D[3] = {(df[0] + df[1]) + (df[2] + df[3]), mu * (df[0] - df[1]), mu * (df[2] - df[3])};
+        const float* G = yG[j];
+        yb[j][0] = fmaf(G[0], D[0], fmaf(G[1], D[1], fmaf(G[2], D[2], a)));
+        yb[j][1] = fmaf(G[1], D[0], fmaf(G[3], D[1], fmaf(G[4], D[2], b)));
+        yb[j][2] = fmaf(G[2], D[0], fmaf(G[4], D[1], fmaf(G[5], D[2], cc)));
+#pragma unroll
+        for (int k = 0; k < FC; k++) {
+          if (k == j) continue;
+#pragma unroll
+          for (int rr = 0; rr < 3; rr++) {
+            float s = yb[k][rr];
+#pragma unroll
+            for (int qq = 0; qq < 3; qq++)
+              s = fmaf(k < j ? xg[ypair(k, j)][3 * rr + qq] : xg[ypair(j, k)][3 * qq + rr], D[qq], s);
+            yb[k][rr] = s;
+          }
+        }
+      }
+    }
+  };
+  // dof-frictionloss rows of the y variants, short-chain form: df = clamp(-res/ARdiag,
+  // -fl - f, fl - f) (the projected step), v_arm += M^-1 e_i df
+  auto fric_rows_y = [&](float& improvement) {
+#pragma unroll
+    for (int i = 0; i < NA; i++) {
+      const float fl = m.dof_frictionloss[i];
+      const float res = fmaf(fR[i], ff[i], v[i] - fa[i]);
+      const float df = fminf(fmaxf(res * -fiD[i], -fl - ff[i]), fl - ff[i]);
+#pragma unroll
+      for (int k = 0; k < NA; k++) v[k] = fmaf(Mi.a(i, k), df, v[k]);
+      ff[i] += df;
+      improvement = fmaf(-df, fmaf(fhD[i], df, res), improvement);
+    }
+  };
+  // after the sweeps: the free body's velocity from the block's force change
+  auto yblock_finish = [&]() {
+    if constexpr (NF == 1 && CON) {
+#pragma unroll
+      for (int k = 0; k < FC; k++) {
+        const int c = cslot[k];
+        float d[4];
+#pragma unroll
+        for (int ed = 0; ed < 4; ed++) d[ed] = cfo[k][ed] - L.at(c, F_FRC + ed);
+        const float mu = ymu[k];
+        const float Dn = (d[0] + d[1]) + (d[2] + d[3]), D1 = mu * (d[0] - d[1]), D2 = mu * (d[2] - d[3]);
+#pragma unroll
+        for (int i = 0; i < 6; i++)
+          v[NA + i] = fmaf(Mi.Fd[0][i],
+                           fmaf(L.at(c, NA + i), Dn, fmaf(L.at(c, 12 + NA + i), D1, L.at(c, 24 + NA + i) * D2)),
+                           v[NA + i]);
+      }
+    }
+  };
+  // the single arm-only contact of the arm-slot variant (or the zero record)
+  auto arm_contact = [&](int c, float& improvement) {
+    float G[6], cf[12], fo[4], ar[4], ia[4], hd[4];
+#pragma unroll
+    for (int ed = 0; ed < 4; ed++)
+      fo[ed] = L.at(c, F_FRC + ed), ar[ed] = L.at(c, F_AREF + ed), ia[ed] = L.at(c, F_IARD + ed),
+      hd[ed] = L.at(c, F_HARD + ed);
+#pragma unroll
+    for (int k = 0; k < 6; k++) G[k] = L.at(c, F_GRAM + k);
+    const float mu = L.at(c, F_MU), Rp = L.at(c, F_R);
+    gram_coefs(G, mu, cf);
+    arm_v(c, mu, Rp, cf, fo, ar, ia, hd, improvement);
+  };
+  auto ysweeps = [&](auto arm) {
+    yblock_setup();
+    yblock_consts();
+    for (int it = 0; it < m.iterations; it++) {
+      float improvement = 0.f;
+      fric_rows_y(improvement);  // arm chain and cube block: independent, one straight-line region
+      yblock_rows(improvement);
+      if constexpr (decltype(arm)::value) arm_contact(ca, improvement);
+      if (improvement * scale < m.tolerance) {
+#ifdef SOARM_PHASE_PROF
+        nsweep = it + 1;
+#endif
+        break;
+      }
+    }
+    yblock_finish();
+  };
+  const bool ypure = CON && NF == 1 && block_first && __all(nlim == 0 && nl == ncon && npost == 0);
   auto sweeps = [&](auto first, auto arm) {
     for (int it = 0; it < m.iterations; it++) {
       float improvement = 0.f;
@@ -803,8 +1024,10 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
     }
   };
   // wave-uniform choice: separate copies of the loop, no branch inside the sweep
-  if (arm_slot) {
-    sweeps(std::true_type{}, std::true_type{});
+  if (ypure) {
+    ysweeps(std::false_type{});
+  } else if (arm_slot) {
+    ysweeps(std::true_type{});
   } else if (block_first) {
     sweeps(std::true_type{}, std::false_type{});
   } else {
@@ -835,7 +1058,8 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
 #ifdef SOARM_PHASE_PROF
   if (e < 65536)
     g_pgs_prof[8 * e + 1] = clock64(), g_pgs_prof[8 * e + 2] = nsweep,
-    g_pgs_prof[8 * e + 3] = (nrun == ncon && nlim == 0), g_pgs_prof[8 * e + 4] = nlim, g_pgs_prof[8 * e + 5] = ncon;
+    g_pgs_prof[8 * e + 3] = (ypure ? 0 : arm_slot ? 1 : block_first ? 2 : 3) | (npost > 0 && npost_free ? 16 : 0),
+    g_pgs_prof[8 * e + 4] = nlim, g_pgs_prof[8 * e + 5] = ncon;
 #endif
 
   // ---- qacc and qfrc_constraint = J' f

@@ -162,7 +162,10 @@ DEVI void write_obs(const Sim<NA, NF>& S, float* obs, int e) {
 //   joint limit, [13] waves with a contact outside the register block, [14] waves
 //   with more than LDS_CON contacts, [15] max contacts of an env, [16] rows: up to
 //   the built contact rows, [17] rows: warm start + cost, [18] rows: block setup
-__device__ unsigned long long g_phase[19];
+//   [19..22] waves per sweep variant (y-pure, y+arm slot, block-first general, other),
+//   [23..26] max wave cycles per variant, [27] waves with a non-block contact on the free body
+//   [28..42] wave cycles between consecutive fine stamps (g_stamp, see PSTAMP sites)
+__device__ unsigned long long g_phase[43];
 #define PHASE_T(v) const long long v = clock64()
 #else
 #define PHASE_T(v)
@@ -313,11 +316,17 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
   const bool use = S.status == st0 && ccount != nullptr;
 #ifdef SOARM_PHASE_PROF
   PHASE_T(t1);
+  PSTAMP(0);
   S.kinematics();
+  PSTAMP(1);
   S.com_crb();
+  PSTAMP(2);
   S.factor();
+  PSTAMP(3);
   S.smooth_forces();
+  PSTAMP(4);
   PHASE_T(t2);
+  PSTAMP(5);
   int ncon = solve_constraints<NA, NF, true>(S, use ? cbuf : nullptr, use ? ccount : nullptr, pmask, n, e, L, cr);
 #else
   int ncon = forward<NA, NF, true>(S, use ? cbuf : nullptr, use ? ccount : nullptr, pmask, n, e, L, cr);
@@ -327,6 +336,7 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
     store_state(S, st, n, e);
     ncon = forward<NA, NF, true>(S, nullptr, nullptr, nullptr, n, e, L, cr);
   }
+  PSTAMP(10);
   if constexpr (NF == 1) {  // reload (laundered pointers: not CSE'd with the first load)
     const float* qp = st.qpos;
     const float* qv = st.qvel;
@@ -339,23 +349,28 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
   if (pmask)  // consumed: clear for the next collide
     for (int w = 0; w < (m.npair + 31) >> 5; w++) pmask[(size_t)w * n + e] = 0u;
   const float ee[3] = {S.ee[0], S.ee[1], S.ee[2]};
+  PSTAMP(11);
   S.integrate();
+  PSTAMP(12);
   store_state(S, st, n, e);
   if (st.ncon) st.ncon[e] += (float)ncon;
   if (obs) {
     S.ee[0] = ee[0], S.ee[1] = ee[1], S.ee[2] = ee[2];
     write_obs(S, obs, e);
   }
+  PSTAMP(13);
   if (gpose) {
     S.kinematics();
+    PSTAMP(14);
     write_geom_poses(S, gpose, n, e);
   }
 #ifdef SOARM_PHASE_PROF
   PHASE_T(t5);
+  PSTAMP(15);
   const long long p0 = g_pgs_prof[8 * e], p1 = g_pgs_prof[8 * e + 1];
   const int nsw = (int)g_pgs_prof[8 * e + 2];
   const bool anylim = __any(g_pgs_prof[8 * e + 4] > 0), anyslow = __any(g_pgs_prof[8 * e + 3] == 0),
-             anyovf = __any(g_pgs_prof[8 * e + 5] > LDS_CON);
+             anyovf = __any(g_pgs_prof[8 * e + 5] > LDS_CON), anyfree = __any(g_pgs_prof[8 * e + 3] & 16);
   atomicMax(&g_phase[15], (unsigned long long)g_pgs_prof[8 * e + 5]);
   atomicAdd(&g_phase[6], (unsigned long long)nsw);
   atomicAdd(&g_phase[7], 1ull);
@@ -369,7 +384,14 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
     atomicAdd(&g_phase[3], (unsigned long long)(p1 - p0));
     atomicAdd(&g_phase[4], (unsigned long long)(t5 - p1));
     atomicMax(&g_phase[8], (unsigned long long)(t5 - t0));
-    atomicAdd(&g_phase[9], (unsigned long long)g_pgs_prof[8 * e + 3]);
+    {
+      int var = (int)g_pgs_prof[8 * e + 3] & 15;
+      atomicAdd(&g_phase[9], (unsigned long long)(var == 0));
+      atomicAdd(&g_phase[19 + var], 1ull);
+      atomicMax(&g_phase[23 + var], (unsigned long long)(t5 - t0));
+    }
+    atomicAdd(&g_phase[27], (unsigned long long)anyfree);
+    for (int k = 0; k < 15; k++) atomicAdd(&g_phase[28 + k], (unsigned long long)(g_stamp[16 * e + k + 1] - g_stamp[16 * e + k]));
     atomicAdd(&g_phase[16], (unsigned long long)(g_pgs_prof[8 * e + 6] - t2));
     atomicAdd(&g_phase[17], (unsigned long long)(g_pgs_prof[8 * e + 7] - g_pgs_prof[8 * e + 6]));
     atomicAdd(&g_phase[18], (unsigned long long)(p0 - g_pgs_prof[8 * e + 7]));
@@ -1051,12 +1073,12 @@ int sim_collide_profile(sim_batch* b, const sim_state* s, double* cycles, void* 
 int sim_phase_profile(double* out, int reset) {
   if (!out) return fail(SIM_E_ARG, "null output");
 #ifdef SOARM_PHASE_PROF
-  unsigned long long h[19];
+  unsigned long long h[43];
   HIPCHECK(hipDeviceSynchronize());
   HIPCHECK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_phase), sizeof(h)));
-  for (int k = 0; k < 19; k++) out[k] = (double)h[k];
+  for (int k = 0; k < 43; k++) out[k] = (double)h[k];
   if (reset) {
-    const unsigned long long z[19] = {};
+    const unsigned long long z[43] = {};
     HIPCHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof(z)));
   }
   return SIM_OK;

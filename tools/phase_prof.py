@@ -44,7 +44,7 @@ q0 = W.initial_qpos(cm, ids, 0)
 sim.reset(init_qpos=q0[:, :5], extra_qpos=q0, seed=0)
 tab = {k: (torch.as_tensor(v, dtype=torch.float32, device="cuda") if isinstance(v, np.ndarray) else v)
        for k, v in W.chirp_tables(ids, 0).items()}
-out = (ctypes.c_double * 19)()
+out = (ctypes.c_double * 43)()
 res = {}
 for t in range(T):
     if t in (0, T // 2, T - 10):
@@ -69,6 +69,13 @@ for t in range(T):
         r["waves_with_lds_overflow"] = v[14] / max(v[5], 1)
         r["max_ncon"] = v[15]
         r["rows_split"] = {"contact_rows": v[16] / tot, "warm_cost": v[17] / tot, "block_setup": v[18] / tot}
+        r["variant_waves"] = {k: v[19 + i] / max(v[5], 1) for i, k in enumerate(["ypure", "yarm", "general", "other"])}
+        r["variant_max_cycles"] = {k: v[23 + i] for i, k in enumerate(["ypure", "yarm", "general", "other"])}
+        r["waves_with_free_nonblock"] = v[27] / max(v[5], 1)
+        stamps = ["kinematics", "com_crb", "factor", "smooth_forces", "(gap)", "solve_m+Minv", "fric+limit rows",
+                  "contact rows", "warm+cost", "pgs+qacc/fcon", "reload", "integrate", "store+obs",
+                  "kinematics2", "geom poses"]
+        r["stamps_per_wave"] = {nm: round(v[28 + i] / max(v[5], 1)) for i, nm in enumerate(stamps)}
         res[t] = r
         print(t, json.dumps(r), flush=True)
 json.dump(res, open(os.path.join(ROOT, "gpurun_out", "phase_prof.json"), "w"), indent=1)
