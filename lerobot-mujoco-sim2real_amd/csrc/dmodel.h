@@ -49,6 +49,8 @@ struct DModel {
   float pair_solimp[MAXP][5], pair_KB[MAXP][2], pair_margin[MAXP], pair_tran[MAXP];
   float pair_friction[MAXP];
   int pair_slot[MAXP];  // first contact slot of the pair in the collide output
+  int pair_body1[MAXP], pair_body2[MAXP];  // geom_bodyid of the pair's geoms
+  int pair_cap[MAXP];                      // contact slots of the pair (1 or PAIR_MAXCON)
   int nslot;            // total contact slots (sum of per-pair capacities)
   int free_diag;        // every free body has ipos = 0 and iquat = 1: its 6x6 M block is diagonal
 

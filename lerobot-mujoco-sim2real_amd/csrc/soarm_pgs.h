@@ -285,17 +285,33 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
         while (bits) {
           const int p = 32 * w + __builtin_ctz(bits);
           bits &= bits - 1;
+          // everything this pair needs, loaded once and all in flight together: the count,
+          // the pair's constants and every slot it may fill (cap <= PAIR_MAXCON; a set mask
+          // bit means at least one contact, and slots past the count are never used)
           const int cnt = ccount[(size_t)p * n + e];
-          const int s0 = m.pair_slot[p];
-          for (int k = 0; k < cnt; k++) {
+          const int s0 = m.pair_slot[p], cap = m.pair_cap[p];
+          const int b1 = m.pair_body1[p], b2 = m.pair_body2[p];
+          const float mu = S.fric >= 0.f ? S.fric : m.pair_friction[p];
+          const float tran = m.pair_tran[p], margin = m.pair_margin[p];
+          const float KB0 = m.pair_KB[p][0], KB1 = m.pair_KB[p][1];
+          float si[5];
+#pragma unroll
+          for (int q = 0; q < 5; q++) si[q] = m.pair_solimp[p][q];
+          float raw[PAIR_MAXCON][7];
+#pragma unroll
+          for (int k = 0; k < PAIR_MAXCON; k++)
+#pragma unroll
+            for (int f = 0; f < 7; f++) raw[k][f] = k < cap ? cbuf[((size_t)(s0 + k) * 7 + f) * n + e] : 0.f;
+#pragma unroll
+          for (int k = 0; k < PAIR_MAXCON; k++) {
+            if (k >= cnt) break;
             if (ncon >= SIM_MAXCON) {
               S.status |= SIM_ST_CONOVERFLOW;
               break;
             }
-            const size_t base = (size_t)(s0 + k) * 7;
-            const float cdist = cbuf[base * n + e];
-            const float cpos[3] = {cbuf[(base + 1) * n + e], cbuf[(base + 2) * n + e], cbuf[(base + 3) * n + e]};
-            float fr[9] = {cbuf[(base + 4) * n + e], cbuf[(base + 5) * n + e], cbuf[(base + 6) * n + e], 0, 0, 0, 0, 0, 0};
+            const float cdist = raw[k][0];
+            const float cpos[3] = {raw[k][1], raw[k][2], raw[k][3]};
+            float fr[9] = {raw[k][4], raw[k][5], raw[k][6], 0, 0, 0, 0, 0, 0};
             {  // contact frame (mju_makeFrame)
               float y[3];
               if (fabsf(fr[1]) < 0.5f)
@@ -308,7 +324,6 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
               fr[3] = y[0] * inv, fr[4] = y[1] * inv, fr[5] = y[2] * inv;
               cross(fr + 6, fr, fr + 3);
             }
-            const int b1 = m.geom_bodyid[m.pair_geom1[p]], b2 = m.geom_bodyid[m.pair_geom2[p]];
             // relative translational Jacobian (body2 - body1) at the contact point, contact frame
             float jd[3][NV];
 #pragma unroll
@@ -346,11 +361,8 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
                 }
               }
             }
-            const bool ta = flags & TOUCH_ARM, tf = flags & TOUCH_FREE;
-            const float mu = S.fric >= 0.f ? S.fric : m.pair_friction[p];
-            const float tran = m.pair_tran[p];
-            const float margin = m.pair_margin[p];
-            const float imp = impedance(m.pair_solimp[p], cdist, margin);
+            const bool ta = flags & TOUCH_ARM;
+            const float imp = impedance(si, cdist, margin);
             const float diag = tran + mu * mu * tran;
             const float R0 = fmaxf(MINVALF, (1.f - imp) * diag / imp);
             const float Rpy = 2.f * mu * mu * R0 / m.impratio;
@@ -365,23 +377,25 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
               L.at(ncon, F_FLAGS) = (float)flags;
             }
             // Gram matrix G = [Jn; Jt1; Jt2] M^-1 [Jn; Jt1; Jt2]' and the three velocities:
-            // every pyramid edge J_e = J_n + s J_tk (s = +-mu) follows from them
-            // (full width: jd is zero on the halves the contact does not touch, and
-            // branch-free code avoids running both sides of a divergent flag test)
+            // every pyramid edge J_e = J_n + s J_tk (s = +-mu) follows from them.  Full
+            // width (jd is zero on the halves the contact does not touch; branch-free code
+            // avoids running both sides of a divergent flag test) unless no lane's contact
+            // touches the arm: then the free-body half alone (diagonal M^-1).
             float W0[NV], W1[NV], W2[NV], G[6];
-            Mi.mul(jd[0], W0, true, true);
-            Mi.mul(jd[1], W1, true, true);
-            Mi.mul(jd[2], W2, true, true);
-            G[0] = dotv<NA, NF>(jd[0], W0, true, true), G[1] = dotv<NA, NF>(jd[0], W1, true, true);
-            G[2] = dotv<NA, NF>(jd[0], W2, true, true), G[3] = dotv<NA, NF>(jd[1], W1, true, true);
-            G[4] = dotv<NA, NF>(jd[1], W2, true, true), G[5] = dotv<NA, NF>(jd[2], W2, true, true);
+            const bool arm_any = NF == 0 || !__all(!ta);
+            Mi.mul(jd[0], W0, arm_any, true);
+            Mi.mul(jd[1], W1, arm_any, true);
+            Mi.mul(jd[2], W2, arm_any, true);
+            G[0] = dotv<NA, NF>(jd[0], W0, arm_any, true), G[1] = dotv<NA, NF>(jd[0], W1, arm_any, true);
+            G[2] = dotv<NA, NF>(jd[0], W2, arm_any, true), G[3] = dotv<NA, NF>(jd[1], W1, arm_any, true);
+            G[4] = dotv<NA, NF>(jd[1], W2, arm_any, true), G[5] = dotv<NA, NF>(jd[2], W2, arm_any, true);
             float vq[3] = {0.f, 0.f, 0.f};
 #pragma unroll
             for (int i = 0; i < NV; i++)
               vq[0] += jd[0][i] * S.qvel[i], vq[1] += jd[1][i] * S.qvel[i], vq[2] += jd[2][i] * S.qvel[i];
             if (lds) {
 #pragma unroll
-              for (int k = 0; k < 6; k++) L.at(ncon, F_GRAM + k) = G[k];
+              for (int k2 = 0; k2 < 6; k2++) L.at(ncon, F_GRAM + k2) = G[k2];
             }
 #pragma unroll
             for (int ed = 0; ed < 4; ed++) {
@@ -390,7 +404,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
               const float vel = vq[0] + s * (k2 ? vq[2] : vq[1]);
               // J_e M^-1 J_e' = G_nn + 2 s G_nk + s^2 G_kk
               const float ard = G[0] + s * (2.f * (k2 ? G[2] : G[1]) + s * (k2 ? G[5] : G[3])) + Rpy;
-              const float ar = -m.pair_KB[p][1] * vel - m.pair_KB[p][0] * imp * (cdist - margin);
+              const float ar = -KB1 * vel - KB0 * imp * (cdist - margin);
               if (lds) {
                 L.at(ncon, F_AREF + ed) = ar;
                 L.at(ncon, F_HARD + ed) = 0.5f * ard;
@@ -785,14 +799,10 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   // arm row before it: run it beside the friction rows so the two independent chains
   // share one straight-line region, then limits and the remaining contacts.
   const bool block_first = __all(npre == 0);
-  // Arm slot: when every lane's only non-block row is (at most) one arm-only contact
-  // (a link touching the table) and no limit is active, the sweep runs it right after
-  // the block with no loop around it (lanes without one run the zero record): it
-  // commutes with the cube block and follows the friction rows, as in MuJoCo's order.
+  // The single non-block contact of a lane (when it has one): an arm-only contact before
+  // the block commutes with it (disjoint dofs), so it runs after the block, right where
+  // the post-block ones run (lanes without one use the zero record).
   const int ca = npost == 1 ? (c0 - npre > 0 ? npre : c1) : LDS_CON;
-  bool arm_ok = nlim == 0 && nl == ncon && npost <= 1;
-  if (npost == 1) arm_ok = arm_ok && (int)L.at(ca, F_FLAGS) == TOUCH_ARM;
-  const bool arm_slot = CON && block_first && __all(arm_ok) && __any(npost == 1);
   // ---- contact-space ("y") sweep of the register block, used when nothing else in the
   // wave touches the free body (every lane: no limits, no overflow rows, no non-block
   // contact other than at most one arm-only one).  Each block contact k keeps
@@ -804,6 +814,16 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   // contact instead of the three 6-dof dots and the 6-dof velocity update of the v form;
   // the velocity is rebuilt once from the force change after the sweeps.  Same
   // Gauss-Seidel sequence (MuJoCo's mj_solPGS row order) in exact arithmetic.
+  // Extra contact slot E of the y variants (every lane: at most one non-block contact,
+  // no limits, no overflow, at most 5 contacts): an arm-only contact, or one that touches
+  // the arm and the free body ("coupled"), or the zero record.  Its y_E lives in registers;
+  // its coefficients live in the LDS of records 5-6 (unused when no lane has more than 5
+  // contacts): W_E = M_arm^-1 J_E,arm' (how a force step on E moves v_arm, and how a
+  // frictionloss row moves y_E), the free-body cross-Gram blocks X_kE = J_k M^-1 J_E' with
+  // the block contacts, the off-diagonal edge Gram, the 3x3 Gram, 1/ARdiag, ARdiag/2, mu, R.
+  enum { E_W = 0, E_X = 18, E_A = 54, E_G = 60, E_IA = 66, E_HD = 70, E_MU = 74, E_RP = 75 };
+  auto EX = [&](int k) -> float& { return L.a[5 * CF + k][L.lane]; };
+  float yE[3] = {0.f, 0.f, 0.f}, fE[4] = {0.f, 0.f, 0.f, 0.f};
   constexpr int NX = FC * (FC - 1) / 2;
   float yb[FC][3], xg[NX > 0 ? NX : 1][9];
   auto ypair = [](int j, int k) { return j * FC - j * (j + 1) / 2 + (k - j - 1); };  // j < k
@@ -887,7 +907,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   // edge Gram matrix: every residual starts from the contact's y, and each force step
   // adds A_ed df_d to the later edges' residuals, so the dependent chain per edge is
   // mul -> max -> fma (df = max(-res/ARdiag, -f) is the projected step f' - f).
-  auto yblock_rows = [&](float& improvement) {
+  auto yblock_rows = [&](float& improvement, auto coupled) {
     if constexpr (NF == 1 && CON) {
 #pragma unroll
       for (int j = 0; j < FC; j++) {
@@ -927,12 +947,21 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
             yb[k][rr] = s;
           }
         }
+        if constexpr (decltype(coupled)::value) {  // the extra contact shares the free body
+#pragma unroll
+          for (int q = 0; q < 3; q++) {
+            float s = yE[q];
+#pragma unroll
+            for (int rr = 0; rr < 3; rr++) s = fmaf(EX(E_X + 9 * j + 3 * rr + q), D[rr], s);
+            yE[q] = s;
+          }
+        }
       }
     }
   };
   // dof-frictionloss rows of the y variants, short-chain form: df = clamp(-res/ARdiag,
   // -fl - f, fl - f) (the projected step), v_arm += M^-1 e_i df
-  auto fric_rows_y = [&](float& improvement) {
+  auto fric_rows_y = [&](float& improvement, auto ext) {
 #pragma unroll
     for (int i = 0; i < NA; i++) {
       const float fl = m.dof_frictionloss[i];
@@ -940,6 +969,10 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       const float df = fminf(fmaxf(res * -fiD[i], -fl - ff[i]), fl - ff[i]);
 #pragma unroll
       for (int k = 0; k < NA; k++) v[k] = fmaf(Mi.a(i, k), df, v[k]);
+      if constexpr (decltype(ext)::value) {  // the extra contact's y: J_E M^-1 e_i = W_E[i]
+#pragma unroll
+        for (int q = 0; q < 3; q++) yE[q] = fmaf(EX(E_W + 6 * q + i), df, yE[q]);
+      }
       ff[i] += df;
       improvement = fmaf(-df, fmaf(fhD[i], df, res), improvement);
     }
@@ -963,27 +996,145 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       }
     }
   };
-  // the single arm-only contact of the arm-slot variant (or the zero record)
-  auto arm_contact = [&](int c, float& improvement) {
-    float G[6], cf[12], fo[4], ar[4], ia[4], hd[4];
+  auto yext_setup = [&](int c) {
+    if constexpr (NF == 1 && CON) {
+      float jf[3][6];
 #pragma unroll
-    for (int ed = 0; ed < 4; ed++)
-      fo[ed] = L.at(c, F_FRC + ed), ar[ed] = L.at(c, F_AREF + ed), ia[ed] = L.at(c, F_IARD + ed),
-      hd[ed] = L.at(c, F_HARD + ed);
+      for (int q = 0; q < 3; q++) {
+        float ja[NA];
 #pragma unroll
-    for (int k = 0; k < 6; k++) G[k] = L.at(c, F_GRAM + k);
-    const float mu = L.at(c, F_MU), Rp = L.at(c, F_R);
-    gram_coefs(G, mu, cf);
-    arm_v(c, mu, Rp, cf, fo, ar, ia, hd, improvement);
+        for (int i = 0; i < NA; i++) ja[i] = L.at(c, 12 * q + i);
+#pragma unroll
+        for (int i = 0; i < 6; i++) jf[q][i] = L.at(c, 12 * q + NA + i);
+        float y = 0.f;
+#pragma unroll
+        for (int i = 0; i < NA; i++) {
+          float w = 0.f;
+#pragma unroll
+          for (int k = 0; k < NA; k++) w = fmaf(Mi.a(i, k), ja[k], w);
+          EX(E_W + 6 * q + i) = w;
+          y = fmaf(ja[i], v[i], y);
+        }
+#pragma unroll
+        for (int i = 0; i < 6; i++) y = fmaf(jf[q][i], v[NA + i], y);
+        yE[q] = y;
+      }
+#pragma unroll
+      for (int k = 0; k < FC; k++)
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+          float jk[6];
+#pragma unroll
+          for (int i = 0; i < 6; i++) jk[i] = L.at(cslot[k], 12 * r + NA + i) * Mi.Fd[0][i];
+#pragma unroll
+          for (int q = 0; q < 3; q++) {
+            float x = 0.f;
+#pragma unroll
+            for (int i = 0; i < 6; i++) x = fmaf(jk[i], jf[q][i], x);
+            EX(E_X + 9 * k + 3 * r + q) = x;
+          }
+        }
+      float ar[4], G[6];
+#pragma unroll
+      for (int ed = 0; ed < 4; ed++) {
+        ar[ed] = L.at(c, F_AREF + ed);
+        fE[ed] = L.at(c, F_FRC + ed);
+        EX(E_IA + ed) = L.at(c, F_IARD + ed);
+        EX(E_HD + ed) = L.at(c, F_HARD + ed);
+      }
+      const float mu = L.at(c, F_MU);
+      EX(E_MU) = mu;
+      EX(E_RP) = L.at(c, F_R);
+      yE[0] -= 0.5f * (ar[0] + ar[1]);
+      yE[1] -= mu > 0.f ? 0.5f * (ar[0] - ar[1]) / mu : 0.f;
+      yE[2] -= mu > 0.f ? 0.5f * (ar[2] - ar[3]) / mu : 0.f;
+#pragma unroll
+      for (int i = 0; i < 6; i++) G[i] = EX(E_G + i) = L.at(c, F_GRAM + i);
+      auto gt = [&](int e) { return (e >> 1) ? G[2] : G[1]; };
+      auto gtt = [&](int e, int d) {
+        const int te = e >> 1, td = d >> 1;
+        return te == td ? (te ? G[5] : G[3]) : G[4];
+      };
+      auto sg = [&](int e) { return (e & 1) ? -mu : mu; };
+      int q = 0;
+#pragma unroll
+      for (int ed = 1; ed < 4; ed++)
+#pragma unroll
+        for (int d = 0; d < ed; d++) EX(E_A + q++) = G[0] + sg(ed) * gt(ed) + sg(d) * gt(d) + sg(ed) * sg(d) * gtt(ed, d);
+    }
   };
-  auto ysweeps = [&](auto arm) {
+  // one sweep step of the extra contact (after the friction rows and the block)
+  auto yext_row = [&](float& improvement, auto coupled) {
+    if constexpr (NF == 1 && CON) {
+      const float mu = EX(E_MU), Rp = EX(E_RP);
+      float r[4], df[4];
+      r[0] = fmaf(Rp, fE[0], fmaf(mu, yE[1], yE[0]));
+      r[1] = fmaf(Rp, fE[1], fmaf(-mu, yE[1], yE[0]));
+      r[2] = fmaf(Rp, fE[2], fmaf(mu, yE[2], yE[0]));
+      r[3] = fmaf(Rp, fE[3], fmaf(-mu, yE[2], yE[0]));
+      int q = 0;
+#pragma unroll
+      for (int ed = 0; ed < 4; ed++) {
+#pragma unroll
+        for (int d = 0; d < ed; d++) r[ed] = fmaf(EX(E_A + q++), df[d], r[ed]);
+        df[ed] = fmaxf(r[ed] * -EX(E_IA + ed), -fE[ed]);
+      }
+#pragma unroll
+      for (int ed = 0; ed < 4; ed++) {
+        fE[ed] += df[ed];
+        improvement = fmaf(-df[ed], fmaf(EX(E_HD + ed), df[ed], r[ed]), improvement);
+      }
+      const float D[3] = {(df[0] + df[1]) + (df[2] + df[3]), mu * (df[0] - df[1]), mu * (df[2] - df[3])};
+#pragma unroll
+      for (int i = 0; i < NA; i++)
+        v[i] = fmaf(EX(E_W + i), D[0], fmaf(EX(E_W + 6 + i), D[1], fmaf(EX(E_W + 12 + i), D[2], v[i])));
+      if constexpr (decltype(coupled)::value) {
+#pragma unroll
+        for (int k = 0; k < FC; k++)
+#pragma unroll
+          for (int rr = 0; rr < 3; rr++) {
+            float s = yb[k][rr];
+#pragma unroll
+            for (int qq = 0; qq < 3; qq++) s = fmaf(EX(E_X + 9 * k + 3 * rr + qq), D[qq], s);
+            yb[k][rr] = s;
+          }
+      }
+      const float y0 = yE[0], y1 = yE[1], y2 = yE[2];
+      yE[0] = fmaf(EX(E_G + 0), D[0], fmaf(EX(E_G + 1), D[1], fmaf(EX(E_G + 2), D[2], y0)));
+      yE[1] = fmaf(EX(E_G + 1), D[0], fmaf(EX(E_G + 3), D[1], fmaf(EX(E_G + 4), D[2], y1)));
+      yE[2] = fmaf(EX(E_G + 2), D[0], fmaf(EX(E_G + 4), D[1], fmaf(EX(E_G + 5), D[2], y2)));
+    }
+  };
+  // after the sweeps: E's forces back to its record; its free-body part moves v6
+  auto yext_finish = [&](int c, auto coupled) {
+    if constexpr (NF == 1 && CON) {
+      float d[4];
+#pragma unroll
+      for (int ed = 0; ed < 4; ed++) d[ed] = fE[ed] - L.at(c, F_FRC + ed);
+      if constexpr (decltype(coupled)::value) {
+        const float mu = L.at(c, F_MU);
+        const float Dn = (d[0] + d[1]) + (d[2] + d[3]), D1 = mu * (d[0] - d[1]), D2 = mu * (d[2] - d[3]);
+#pragma unroll
+        for (int i = 0; i < 6; i++)
+          v[NA + i] = fmaf(Mi.Fd[0][i],
+                           fmaf(L.at(c, NA + i), Dn, fmaf(L.at(c, 12 + NA + i), D1, L.at(c, 24 + NA + i) * D2)),
+                           v[NA + i]);
+      }
+      if (c < LDS_CON) {
+#pragma unroll
+        for (int ed = 0; ed < 4; ed++) L.at(c, F_FRC + ed) = fE[ed];
+      }
+    }
+  };
+  auto ysweeps = [&](auto ext, auto coupled) {
     yblock_setup();
     yblock_consts();
+    if constexpr (decltype(ext)::value) yext_setup(ca);
     for (int it = 0; it < m.iterations; it++) {
       float improvement = 0.f;
-      fric_rows_y(improvement);  // arm chain and cube block: independent, one straight-line region
-      yblock_rows(improvement);
-      if constexpr (decltype(arm)::value) arm_contact(ca, improvement);
+      fric_rows_y(improvement, ext);  // arm chain and cube block: independent, one straight-line region
+      yblock_rows(improvement, coupled);
+      if constexpr (decltype(ext)::value) yext_row(improvement, coupled);
       if (improvement * scale < m.tolerance) {
 #ifdef SOARM_PHASE_PROF
         nsweep = it + 1;
@@ -992,16 +1143,16 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       }
     }
     yblock_finish();
+    if constexpr (decltype(ext)::value) yext_finish(ca, coupled);
   };
   const bool ypure = CON && NF == 1 && block_first && __all(nlim == 0 && nl == ncon && npost == 0);
-  auto sweeps = [&](auto first, auto arm) {
+  const bool yext = CON && NF == 1 && !ypure && block_first &&
+                    __all(nlim == 0 && nl == ncon && npost <= 1 && nl <= 5);
+  const bool ycoupled = yext && __any(npost == 1 && ((int)L.at(ca, F_FLAGS) & TOUCH_FREE));
+  auto sweeps = [&](auto first) {
     for (int it = 0; it < m.iterations; it++) {
       float improvement = 0.f;
-      if constexpr (decltype(arm)::value) {
-        fric_rows(improvement);  // friction and cube block, then the single arm contact
-        block_rows(improvement);
-        lds_contact(ca, improvement);
-      } else if constexpr (decltype(first)::value) {
+      if constexpr (decltype(first)::value) {
         fric_rows(improvement);  // same basic block as the register block: they interleave
         block_rows(improvement);
         limit_rows(improvement);
@@ -1025,13 +1176,15 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   };
   // wave-uniform choice: separate copies of the loop, no branch inside the sweep
   if (ypure) {
-    ysweeps(std::false_type{});
-  } else if (arm_slot) {
-    ysweeps(std::true_type{});
+    ysweeps(std::false_type{}, std::false_type{});
+  } else if (yext && ycoupled) {
+    ysweeps(std::true_type{}, std::true_type{});
+  } else if (yext) {
+    ysweeps(std::true_type{}, std::false_type{});
   } else if (block_first) {
-    sweeps(std::true_type{}, std::false_type{});
+    sweeps(std::true_type{});
   } else {
-    sweeps(std::false_type{}, std::false_type{});
+    sweeps(std::false_type{});
   }
   if constexpr (NF == 1 && CON) {  // the block's forces back to their records (for J' f)
 #pragma unroll
@@ -1058,7 +1211,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
 #ifdef SOARM_PHASE_PROF
   if (e < 65536)
     g_pgs_prof[8 * e + 1] = clock64(), g_pgs_prof[8 * e + 2] = nsweep,
-    g_pgs_prof[8 * e + 3] = (ypure ? 0 : arm_slot ? 1 : block_first ? 2 : 3) | (npost > 0 && npost_free ? 16 : 0),
+    g_pgs_prof[8 * e + 3] = (ypure ? 0 : yext ? 1 : block_first ? 2 : 3) | (npost > 0 && npost_free ? 16 : 0),
     g_pgs_prof[8 * e + 4] = nlim, g_pgs_prof[8 * e + 5] = ncon;
 #endif
 

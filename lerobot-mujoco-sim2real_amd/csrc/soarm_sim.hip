@@ -307,6 +307,7 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
   __shared__ float s_keep[keep_floats<NA, NF>()][64];
   const RowLds L{s_rows, s_lim, NF == 1 ? s_keep : nullptr, (int)threadIdx.x};
   const ContactRows<NA, NF> cr{scratch + e, n};
+  const float ncon_prev = st.ncon ? st.ncon[e] : 0.f;  // issued early: consumed at the end
   const int st0 = S.status;
   S.check_state();
   // positions / velocities are re-read from HBM after the solve instead of being held in
@@ -353,7 +354,7 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
   S.integrate();
   PSTAMP(12);
   store_state(S, st, n, e);
-  if (st.ncon) st.ncon[e] += (float)ncon;
+  if (st.ncon) st.ncon[e] = ncon_prev + (float)ncon;
   if (obs) {
     S.ee[0] = ee[0], S.ee[1] = ee[1], S.ee[2] = ee[2];
     write_obs(S, obs, e);
@@ -737,6 +738,8 @@ static int validate_and_build(const sim_model_desc& d, sim_model* M) {
     const int t1 = d.geom_type[g1], t2 = d.geom_type[g2];
     const int cap = (t2 == SIM_GEOM_BOX && (t1 == SIM_GEOM_BOX || t1 == SIM_GEOM_PLANE)) ? 4 : 1;
     m.pair_slot[p] = m.nslot;
+    m.pair_cap[p] = cap;
+    m.pair_body1[p] = d.geom_bodyid[g1], m.pair_body2[p] = d.geom_bodyid[g2];
     m.nslot += cap;
   }
   // free bodies: the kernels use a diagonal 6x6 mass block, which needs the inertia frame at
