@@ -43,7 +43,7 @@ __device__ long long g_stamp[65536 * 16];
 #define PSTAMP(k)
 #endif
 
-constexpr int LDS_CON = 7;  // contacts whose rows stay in LDS
+constexpr int LDS_CON = 6;  // contacts whose rows stay in LDS
 constexpr int CF = 61;      // LDS floats per contact record
 // record fields: [0, 3*12) J_n | J_t1 | J_t2 (12 slots each), 36..39 aref_e,
 // 40..43 ARdiag_e / 2, 44..47 force_e, 48..51 1/ARdiag_e, 52 mu, 53 R (pyramid),
@@ -59,12 +59,14 @@ template <int NA, int NF>
 constexpr int keep_floats() { return NA * (NA + 1) / 2 + 6 * NF + (NA + 6 * NF) + 3; }
 // joint-limit rows (rare): compact list, one record per active limit
 constexpr int LF = 7;  // dof, sign, aref, R, ARdiag, 1/ARdiag, force
+constexpr int XS_EXT = 98;  // floats per lane of extra-slot scratch beyond the limit list
 enum { L_DOF = 0, L_SGN = 1, L_AREF = 2, L_R = 3, L_ARD = 4, L_IARD = 5, L_FRC = 6 };
 
 struct RowLds {
   float (*a)[64];    // [(LDS_CON + 1) * CF][64] contact records + a zero record (null: contact-free kernel)
   float (*lim)[64];  // [NA * LF][64] active joint-limit records
   float (*keep)[64]; // [KEEP][64] state held in LDS across the PGS sweeps (null: kept in registers)
+  float (*ext)[64];  // [XS_EXT][64] scratch of the y sweep's extra contact slots
   int lane;
   DEVI float& at(int c, int f) const { return a[c * CF + f][lane]; }
   DEVI float& lm(int l, int f) const { return lim[l * LF + f][lane]; }
@@ -773,8 +775,9 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   const int npost = (c0 - npre) + (nl - c1);
 #ifdef SOARM_PHASE_PROF
   bool npost_free = false;  // a non-block contact touches the free body
+  int nfree_x = 0;
   for (int c = 0; c < nl; c++)
-    if ((c < c0 || c >= c1) && ((int)L.at(c, F_FLAGS) & TOUCH_FREE)) npost_free = true;
+    if ((c < c0 || c >= c1) && ((int)L.at(c, F_FLAGS) & TOUCH_FREE)) npost_free = true, nfree_x++;
 #endif
   // the block's sweep (straight-line: one basic block with the friction rows)
   auto block_rows = [&](float& improvement) {
@@ -803,6 +806,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   // the block commutes with it (disjoint dofs), so it runs after the block, right where
   // the post-block ones run (lanes without one use the zero record).
   const int ca = npost == 1 ? (c0 - npre > 0 ? npre : c1) : LDS_CON;
+  auto xidx = [&](int j) { return j < c0 - npre ? npre + j : c1 + j - (c0 - npre); };  // j-th non-block contact
   // ---- contact-space ("y") sweep of the register block, used when nothing else in the
   // wave touches the free body (every lane: no limits, no overflow rows, no non-block
   // contact other than at most one arm-only one).  Each block contact k keeps
@@ -821,9 +825,16 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   // contacts): W_E = M_arm^-1 J_E,arm' (how a force step on E moves v_arm, and how a
   // frictionloss row moves y_E), the free-body cross-Gram blocks X_kE = J_k M^-1 J_E' with
   // the block contacts, the off-diagonal edge Gram, the 3x3 Gram, 1/ARdiag, ARdiag/2, mu, R.
+  // Scratch of the extra slots (compile-time indices): the joint-limit list (no limit is
+  // active in the y variants) and an array of its own.
   enum { E_W = 0, E_X = 18, E_A = 54, E_G = 60, E_IA = 66, E_HD = 70, E_MU = 74, E_RP = 75 };
-  auto EX = [&](int k) -> float& { return L.a[5 * CF + k][L.lane]; };
-  float yE[3] = {0.f, 0.f, 0.f}, fE[4] = {0.f, 0.f, 0.f, 0.f};
+  // second extra slot F (an arm-only contact before E in row order), v-form on the arm:
+  // J_arm rows, W_F = M_arm^-1 J_F', edge Gram, 1/ARd, ARd/2, mu, R, aref shift, X_EF = J_E M^-1 J_F'
+  enum { F_J = 76, F_W = 94, F_A = 112, F_IA = 118, F_HD = 122, F_MUX = 126, F_RPX = 127, F_SH = 128, F_XE = 131,
+         XS_END = 140 };
+  static_assert(XS_END <= NA * LF + XS_EXT, "extra-slot scratch fits");
+  auto EX = [&](int k) -> float& { return k < NA * LF ? L.lim[k][L.lane] : L.ext[k - NA * LF][L.lane]; };
+  float yE[3] = {0.f, 0.f, 0.f}, fE[4] = {0.f, 0.f, 0.f, 0.f}, fF[4] = {0.f, 0.f, 0.f, 0.f};
   constexpr int NX = FC * (FC - 1) / 2;
   float yb[FC][3], xg[NX > 0 ? NX : 1][9];
   auto ypair = [](int j, int k) { return j * FC - j * (j + 1) / 2 + (k - j - 1); };  // j < k
@@ -985,7 +996,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
         const int c = cslot[k];
         float d[4];
 #pragma unroll
-        for (int ed = 0; ed < 4; ed++) d[ed] = cfo[k][ed] - L.at(c, F_FRC + ed);
+        for (int ed = 0; ed < 4; ed++) d[ed] = k < nrun ? cfo[k][ed] - L.at(c, F_FRC + ed) : 0.f;
         const float mu = ymu[k];
         const float Dn = (d[0] + d[1]) + (d[2] + d[3]), D1 = mu * (d[0] - d[1]), D2 = mu * (d[2] - d[3]);
 #pragma unroll
@@ -996,17 +1007,30 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       }
     }
   };
-  auto yext_setup = [&](int c) {
+  // edge Gram off-diagonals A_ed (d < e) of a contact from its 3x3 Gram block and mu
+  auto edge_gram = [](const float G[6], float mu, float A[6]) {
+    auto gt = [&](int e) { return (e >> 1) ? G[2] : G[1]; };
+    auto gtt = [&](int e, int d) {
+      const int te = e >> 1, td = d >> 1;
+      return te == td ? (te ? G[5] : G[3]) : G[4];
+    };
+    auto sg = [&](int e) { return (e & 1) ? -mu : mu; };
+    int q = 0;
+#pragma unroll
+    for (int ed = 1; ed < 4; ed++)
+#pragma unroll
+      for (int d = 0; d < ed; d++) A[q++] = G[0] + sg(ed) * gt(ed) + sg(d) * gt(d) + sg(ed) * sg(d) * gtt(ed, d);
+  };
+  // Set up E (record cE) and F (record cF); an absent slot is the zero record: 1/ARdiag = 0
+  // and f = 0, so its steps are exact no-ops.
+  auto yext_setup = [&](int cE, int cF) {
     if constexpr (NF == 1 && CON) {
-      float jf[3][6];
+      // ---- E: W_E, y_E, cross-Gram with the block, chain constants
 #pragma unroll
       for (int q = 0; q < 3; q++) {
-        float ja[NA];
+        float ja[NA], y = 0.f;
 #pragma unroll
-        for (int i = 0; i < NA; i++) ja[i] = L.at(c, 12 * q + i);
-#pragma unroll
-        for (int i = 0; i < 6; i++) jf[q][i] = L.at(c, 12 * q + NA + i);
-        float y = 0.f;
+        for (int i = 0; i < NA; i++) ja[i] = L.at(cE, 12 * q + i);
 #pragma unroll
         for (int i = 0; i < NA; i++) {
           float w = 0.f;
@@ -1016,7 +1040,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
           y = fmaf(ja[i], v[i], y);
         }
 #pragma unroll
-        for (int i = 0; i < 6; i++) y = fmaf(jf[q][i], v[NA + i], y);
+        for (int i = 0; i < 6; i++) y = fmaf(L.at(cE, 12 * q + NA + i), v[NA + i], y);
         yE[q] = y;
       }
 #pragma unroll
@@ -1030,37 +1054,112 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
           for (int q = 0; q < 3; q++) {
             float x = 0.f;
 #pragma unroll
-            for (int i = 0; i < 6; i++) x = fmaf(jk[i], jf[q][i], x);
+            for (int i = 0; i < 6; i++) x = fmaf(jk[i], L.at(cE, 12 * q + NA + i), x);
             EX(E_X + 9 * k + 3 * r + q) = x;
           }
         }
-      float ar[4], G[6];
+      {
+        float ar[4], G[6], A[6];
 #pragma unroll
-      for (int ed = 0; ed < 4; ed++) {
-        ar[ed] = L.at(c, F_AREF + ed);
-        fE[ed] = L.at(c, F_FRC + ed);
-        EX(E_IA + ed) = L.at(c, F_IARD + ed);
-        EX(E_HD + ed) = L.at(c, F_HARD + ed);
+        for (int ed = 0; ed < 4; ed++) {
+          ar[ed] = L.at(cE, F_AREF + ed);
+          fE[ed] = L.at(cE, F_FRC + ed);
+          EX(E_IA + ed) = L.at(cE, F_IARD + ed);
+          EX(E_HD + ed) = L.at(cE, F_HARD + ed);
+        }
+        const float mu = L.at(cE, F_MU);
+        EX(E_MU) = mu;
+        EX(E_RP) = L.at(cE, F_R);
+        yE[0] -= 0.5f * (ar[0] + ar[1]);
+        yE[1] -= mu > 0.f ? 0.5f * (ar[0] - ar[1]) / mu : 0.f;
+        yE[2] -= mu > 0.f ? 0.5f * (ar[2] - ar[3]) / mu : 0.f;
+#pragma unroll
+        for (int i = 0; i < 6; i++) G[i] = EX(E_G + i) = L.at(cE, F_GRAM + i);
+        edge_gram(G, mu, A);
+#pragma unroll
+        for (int i = 0; i < 6; i++) EX(E_A + i) = A[i];
       }
-      const float mu = L.at(c, F_MU);
-      EX(E_MU) = mu;
-      EX(E_RP) = L.at(c, F_R);
-      yE[0] -= 0.5f * (ar[0] + ar[1]);
-      yE[1] -= mu > 0.f ? 0.5f * (ar[0] - ar[1]) / mu : 0.f;
-      yE[2] -= mu > 0.f ? 0.5f * (ar[2] - ar[3]) / mu : 0.f;
+      // ---- F: J_arm, W_F, X_EF = J_E,arm W_F', chain constants, aref shift
 #pragma unroll
-      for (int i = 0; i < 6; i++) G[i] = EX(E_G + i) = L.at(c, F_GRAM + i);
-      auto gt = [&](int e) { return (e >> 1) ? G[2] : G[1]; };
-      auto gtt = [&](int e, int d) {
-        const int te = e >> 1, td = d >> 1;
-        return te == td ? (te ? G[5] : G[3]) : G[4];
-      };
-      auto sg = [&](int e) { return (e & 1) ? -mu : mu; };
+      for (int r = 0; r < 3; r++) {
+        float jf[NA], w[NA];
+#pragma unroll
+        for (int i = 0; i < NA; i++) jf[i] = EX(F_J + 6 * r + i) = L.at(cF, 12 * r + i);
+#pragma unroll
+        for (int i = 0; i < NA; i++) {
+          float t = 0.f;
+#pragma unroll
+          for (int k = 0; k < NA; k++) t = fmaf(Mi.a(i, k), jf[k], t);
+          w[i] = EX(F_W + 6 * r + i) = t;
+        }
+#pragma unroll
+        for (int q = 0; q < 3; q++) {
+          float x = 0.f;
+#pragma unroll
+          for (int i = 0; i < NA; i++) x = fmaf(L.at(cE, 12 * q + i), w[i], x);
+          EX(F_XE + 3 * q + r) = x;
+        }
+      }
+      {
+        float ar[4], G[6], A[6];
+#pragma unroll
+        for (int ed = 0; ed < 4; ed++) {
+          ar[ed] = L.at(cF, F_AREF + ed);
+          fF[ed] = L.at(cF, F_FRC + ed);
+          EX(F_IA + ed) = L.at(cF, F_IARD + ed);
+          EX(F_HD + ed) = L.at(cF, F_HARD + ed);
+        }
+        const float mu = L.at(cF, F_MU);
+        EX(F_MUX) = mu;
+        EX(F_RPX) = L.at(cF, F_R);
+        EX(F_SH + 0) = 0.5f * (ar[0] + ar[1]);
+        EX(F_SH + 1) = mu > 0.f ? 0.5f * (ar[0] - ar[1]) / mu : 0.f;
+        EX(F_SH + 2) = mu > 0.f ? 0.5f * (ar[2] - ar[3]) / mu : 0.f;
+#pragma unroll
+        for (int i = 0; i < 6; i++) G[i] = L.at(cF, F_GRAM + i);
+        edge_gram(G, mu, A);
+#pragma unroll
+        for (int i = 0; i < 6; i++) EX(F_A + i) = A[i];
+      }
+    }
+  };
+  // one sweep step of F (arm-only, before E in row order): v-form on the arm (its y from
+  // three NA-dof dots), the edge chain, v_arm += W_F D, and E's y by X_EF D
+  auto yf_row = [&](float& improvement) {
+    if constexpr (NF == 1 && CON) {
+      const float mu = EX(F_MUX), Rp = EX(F_RPX);
+      float y[3];
+#pragma unroll
+      for (int q = 0; q < 3; q++) {
+        float t = -EX(F_SH + q);
+#pragma unroll
+        for (int i = 0; i < NA; i++) t = fmaf(EX(F_J + 6 * q + i), v[i], t);
+        y[q] = t;
+      }
+      float r[4], df[4];
+      r[0] = fmaf(Rp, fF[0], fmaf(mu, y[1], y[0]));
+      r[1] = fmaf(Rp, fF[1], fmaf(-mu, y[1], y[0]));
+      r[2] = fmaf(Rp, fF[2], fmaf(mu, y[2], y[0]));
+      r[3] = fmaf(Rp, fF[3], fmaf(-mu, y[2], y[0]));
       int q = 0;
 #pragma unroll
-      for (int ed = 1; ed < 4; ed++)
+      for (int ed = 0; ed < 4; ed++) {
 #pragma unroll
-        for (int d = 0; d < ed; d++) EX(E_A + q++) = G[0] + sg(ed) * gt(ed) + sg(d) * gt(d) + sg(ed) * sg(d) * gtt(ed, d);
+        for (int d = 0; d < ed; d++) r[ed] = fmaf(EX(F_A + q++), df[d], r[ed]);
+        df[ed] = fmaxf(r[ed] * -EX(F_IA + ed), -fF[ed]);
+      }
+#pragma unroll
+      for (int ed = 0; ed < 4; ed++) {
+        fF[ed] += df[ed];
+        improvement = fmaf(-df[ed], fmaf(EX(F_HD + ed), df[ed], r[ed]), improvement);
+      }
+      const float D[3] = {(df[0] + df[1]) + (df[2] + df[3]), mu * (df[0] - df[1]), mu * (df[2] - df[3])};
+#pragma unroll
+      for (int i = 0; i < NA; i++)
+        v[i] = fmaf(EX(F_W + i), D[0], fmaf(EX(F_W + 6 + i), D[1], fmaf(EX(F_W + 12 + i), D[2], v[i])));
+#pragma unroll
+      for (int qq = 0; qq < 3; qq++)
+        yE[qq] = fmaf(EX(F_XE + 3 * qq), D[0], fmaf(EX(F_XE + 3 * qq + 1), D[1], fmaf(EX(F_XE + 3 * qq + 2), D[2], yE[qq])));
     }
   };
   // one sweep step of the extra contact (after the friction rows and the block)
@@ -1106,11 +1205,15 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
     }
   };
   // after the sweeps: E's forces back to its record; its free-body part moves v6
-  auto yext_finish = [&](int c, auto coupled) {
+  auto yext_finish = [&](int c, bool hasE, int cF, bool hasF, auto coupled) {
     if constexpr (NF == 1 && CON) {
+      if (hasF) {
+#pragma unroll
+        for (int ed = 0; ed < 4; ed++) L.at(cF, F_FRC + ed) = fF[ed];
+      }
       float d[4];
 #pragma unroll
-      for (int ed = 0; ed < 4; ed++) d[ed] = fE[ed] - L.at(c, F_FRC + ed);
+      for (int ed = 0; ed < 4; ed++) d[ed] = hasE ? fE[ed] - L.at(c, F_FRC + ed) : 0.f;
       if constexpr (decltype(coupled)::value) {
         const float mu = L.at(c, F_MU);
         const float Dn = (d[0] + d[1]) + (d[2] + d[3]), D1 = mu * (d[0] - d[1]), D2 = mu * (d[2] - d[3]);
@@ -1120,20 +1223,24 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
                            fmaf(L.at(c, NA + i), Dn, fmaf(L.at(c, 12 + NA + i), D1, L.at(c, 24 + NA + i) * D2)),
                            v[NA + i]);
       }
-      if (c < LDS_CON) {
+      if (hasE) {
 #pragma unroll
         for (int ed = 0; ed < 4; ed++) L.at(c, F_FRC + ed) = fE[ed];
       }
     }
   };
-  auto ysweeps = [&](auto ext, auto coupled) {
+  // extras in row order: F = the first of two (arm-only), E = the last one
+  const int cE = npost >= 1 ? xidx(npost - 1) : LDS_CON, cF = npost == 2 ? xidx(0) : LDS_CON;
+  const bool hasE = npost >= 1, hasF = npost == 2;
+  auto ysweeps = [&](auto ext, auto coupled, auto ext2) {
     yblock_setup();
     yblock_consts();
-    if constexpr (decltype(ext)::value) yext_setup(ca);
+    if constexpr (decltype(ext)::value) yext_setup(cE, cF);
     for (int it = 0; it < m.iterations; it++) {
       float improvement = 0.f;
       fric_rows_y(improvement, ext);  // arm chain and cube block: independent, one straight-line region
       yblock_rows(improvement, coupled);
+      if constexpr (decltype(ext2)::value) yf_row(improvement);
       if constexpr (decltype(ext)::value) yext_row(improvement, coupled);
       if (improvement * scale < m.tolerance) {
 #ifdef SOARM_PHASE_PROF
@@ -1143,12 +1250,16 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       }
     }
     yblock_finish();
-    if constexpr (decltype(ext)::value) yext_finish(ca, coupled);
+    if constexpr (decltype(ext)::value) yext_finish(cE, hasE, cF, hasF, coupled);
   };
   const bool ypure = CON && NF == 1 && block_first && __all(nlim == 0 && nl == ncon && npost == 0);
+  // up to two extras: the first of two must be arm-only (arm-only pairs precede the cube's
+  // in pair order, so that is the common case), the last may touch the cube
   const bool yext = CON && NF == 1 && !ypure && block_first &&
-                    __all(nlim == 0 && nl == ncon && npost <= 1 && nl <= 5);
-  const bool ycoupled = yext && __any(npost == 1 && ((int)L.at(ca, F_FLAGS) & TOUCH_FREE));
+                    __all(nlim == 0 && nl == ncon && npost <= 2 &&
+                          (npost < 2 || (int)L.at(xidx(0), F_FLAGS) == TOUCH_ARM));
+  const bool ycoupled = yext && __any(npost >= 1 && ((int)L.at(cE, F_FLAGS) & TOUCH_FREE));
+  const bool yext2 = yext && __any(npost == 2);
   auto sweeps = [&](auto first) {
     for (int it = 0; it < m.iterations; it++) {
       float improvement = 0.f;
@@ -1176,11 +1287,15 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   };
   // wave-uniform choice: separate copies of the loop, no branch inside the sweep
   if (ypure) {
-    ysweeps(std::false_type{}, std::false_type{});
+    ysweeps(std::false_type{}, std::false_type{}, std::false_type{});
+  } else if (yext && yext2 && ycoupled) {
+    ysweeps(std::true_type{}, std::true_type{}, std::true_type{});
+  } else if (yext && yext2) {
+    ysweeps(std::true_type{}, std::false_type{}, std::true_type{});
   } else if (yext && ycoupled) {
-    ysweeps(std::true_type{}, std::true_type{});
+    ysweeps(std::true_type{}, std::true_type{}, std::false_type{});
   } else if (yext) {
-    ysweeps(std::true_type{}, std::false_type{});
+    ysweeps(std::true_type{}, std::false_type{}, std::false_type{});
   } else if (block_first) {
     sweeps(std::true_type{});
   } else {
@@ -1211,7 +1326,9 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
 #ifdef SOARM_PHASE_PROF
   if (e < 65536)
     g_pgs_prof[8 * e + 1] = clock64(), g_pgs_prof[8 * e + 2] = nsweep,
-    g_pgs_prof[8 * e + 3] = (ypure ? 0 : yext ? 1 : block_first ? 2 : 3) | (npost > 0 && npost_free ? 16 : 0),
+    g_pgs_prof[8 * e + 3] = (ypure ? 0 : yext ? 1 : block_first ? 2 : 3) | (npost > 0 && npost_free ? 16 : 0) |
+                            (min(npost, 3) << 8) | (min(nfree_x, 3) << 12) | ((nl > 5) << 16) | ((nlim > 0) << 17) |
+                            ((nl != ncon) << 18),
     g_pgs_prof[8 * e + 4] = nlim, g_pgs_prof[8 * e + 5] = ncon;
 #endif
 

@@ -165,7 +165,7 @@ DEVI void write_obs(const Sim<NA, NF>& S, float* obs, int e) {
 //   [19..22] waves per sweep variant (y-pure, y+arm slot, block-first general, other),
 //   [23..26] max wave cycles per variant, [27] waves with a non-block contact on the free body
 //   [28..42] wave cycles between consecutive fine stamps (g_stamp, see PSTAMP sites)
-__device__ unsigned long long g_phase[43];
+__device__ unsigned long long g_phase[53];
 #define PHASE_T(v) const long long v = clock64()
 #else
 #define PHASE_T(v)
@@ -200,7 +200,7 @@ __global__ __launch_bounds__(64) void k_step(const DModel* __restrict__ dm, int 
       if (k < m.nact) S.ctrl[k] = action[(size_t)e * m.nact + k];
   }
   __shared__ float s_lim[NA * LF][64];
-  const RowLds L{nullptr, s_lim, nullptr, (int)threadIdx.x};
+  const RowLds L{nullptr, s_lim, nullptr, nullptr, (int)threadIdx.x};
   const ContactRows<NA, NF> cr{nullptr, n};
   for (int s = 0; s < nsub; s++) {
     S.relaunder();
@@ -305,7 +305,8 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
   __shared__ float s_rows[(LDS_CON + 1) * CF][64];  // + one all-zero record
   __shared__ float s_lim[NA * LF][64];
   __shared__ float s_keep[keep_floats<NA, NF>()][64];
-  const RowLds L{s_rows, s_lim, NF == 1 ? s_keep : nullptr, (int)threadIdx.x};
+  __shared__ float s_ext[NF == 1 ? XS_EXT : 1][64];  // y sweep: extra-contact slot coefficients
+  const RowLds L{s_rows, s_lim, NF == 1 ? s_keep : nullptr, s_ext, (int)threadIdx.x};
   const ContactRows<NA, NF> cr{scratch + e, n};
   const float ncon_prev = st.ncon ? st.ncon[e] : 0.f;  // issued early: consumed at the end
   const int st0 = S.status;
@@ -378,6 +379,17 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
   int wmax = nsw;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, __shfl_xor(wmax, o));
+  {  // per-lane census of lanes in waves on a non-y sweep: [43..46] npost 0..3+, [47..49] extras
+     // on the free body 0/1/2+, [50] > 5 contacts, [51] active limit, [52] overflow rows
+    const long long v = g_pgs_prof[8 * e + 3];
+    if ((v & 15) >= 2) {
+      atomicAdd(&g_phase[43 + ((v >> 8) & 3)], 1ull);
+      atomicAdd(&g_phase[47 + min((int)((v >> 12) & 3), 2)], 1ull);
+      atomicAdd(&g_phase[50], (unsigned long long)((v >> 16) & 1));
+      atomicAdd(&g_phase[51], (unsigned long long)((v >> 17) & 1));
+      atomicAdd(&g_phase[52], (unsigned long long)((v >> 18) & 1));
+    }
+  }
   if ((threadIdx.x & 63) == 0) {
     atomicAdd(&g_phase[0], (unsigned long long)(t1 - t0));
     atomicAdd(&g_phase[1], (unsigned long long)(t2 - t1));
@@ -1076,12 +1088,12 @@ int sim_collide_profile(sim_batch* b, const sim_state* s, double* cycles, void* 
 int sim_phase_profile(double* out, int reset) {
   if (!out) return fail(SIM_E_ARG, "null output");
 #ifdef SOARM_PHASE_PROF
-  unsigned long long h[43];
+  unsigned long long h[53];
   HIPCHECK(hipDeviceSynchronize());
   HIPCHECK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_phase), sizeof(h)));
-  for (int k = 0; k < 43; k++) out[k] = (double)h[k];
+  for (int k = 0; k < 53; k++) out[k] = (double)h[k];
   if (reset) {
-    const unsigned long long z[43] = {};
+    const unsigned long long z[53] = {};
     HIPCHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof(z)));
   }
   return SIM_OK;

@@ -44,14 +44,16 @@ q0 = W.initial_qpos(cm, ids, 0)
 sim.reset(init_qpos=q0[:, :5], extra_qpos=q0, seed=0)
 tab = {k: (torch.as_tensor(v, dtype=torch.float32, device="cuda") if isinstance(v, np.ndarray) else v)
        for k, v in W.chirp_tables(ids, 0).items()}
-out = (ctypes.c_double * 43)()
+out = (ctypes.c_double * 53)()
 res = {}
+every = int(os.environ.get("EVERY", 0))
+starts = set(range(0, T, every)) if every else {0, T // 2, T - 10}
 for t in range(T):
-    if t in (0, T // 2, T - 10):
+    if t in starts:
         torch.cuda.synchronize()
         lib.sim_phase_profile(ctypes.cast(out, ctypes.c_void_p), 1)
     sim.step(W.chirp_action(tab, float(t), lib=torch))
-    if t in (9, T // 2 + 9, T - 1):
+    if t - 9 in starts:
         torch.cuda.synchronize()
         lib.sim_phase_profile(ctypes.cast(out, ctypes.c_void_p), 1)
         v = list(out)
@@ -76,6 +78,7 @@ for t in range(T):
                   "contact rows", "warm+cost", "pgs+qacc/fcon", "reload", "integrate", "store+obs",
                   "kinematics2", "geom poses"]
         r["stamps_per_wave"] = {nm: round(v[28 + i] / max(v[5], 1)) for i, nm in enumerate(stamps)}
+        r["nony_lanes"] = {"npost": v[43:47], "free_extras": v[47:50], "nl>5": v[50], "limit": v[51], "overflow": v[52]}
         res[t] = r
         print(t, json.dumps(r), flush=True)
 json.dump(res, open(os.path.join(ROOT, "gpurun_out", "phase_prof.json"), "w"), indent=1)
