@@ -39,8 +39,22 @@ __device__ long long g_pgs_prof[65536 * 8];
 __device__ long long g_stamp[65536 * 16];
 #define PSTAMP(k) \
   if (e < 65536) g_stamp[16 * e + (k)] = clock64()
+// contact-row build split: [0] loads + frame, [1] Jacobian, [2] Gram / M^-1 / velocities, [3] edges + LDS writes
+__device__ long long g_rowprof[65536 * 4];
+#define RP_INIT long long rp_acc[4] = {0, 0, 0, 0}, rp_t = clock64()
+#define RP_MARK(k)                  \
+  {                                 \
+    const long long t_ = clock64(); \
+    rp_acc[k] += t_ - rp_t;         \
+    rp_t = t_;                      \
+  }
+#define RP_STORE \
+  if (e < 65536) g_rowprof[4 * e] = rp_acc[0], g_rowprof[4 * e + 1] = rp_acc[1], g_rowprof[4 * e + 2] = rp_acc[2], g_rowprof[4 * e + 3] = rp_acc[3]
 #else
 #define PSTAMP(k)
+#define RP_INIT
+#define RP_MARK(k)
+#define RP_STORE
 #endif
 
 constexpr int LDS_CON = 6;  // contacts whose rows stay in LDS
@@ -279,6 +293,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   PSTAMP(7);
   // ---- contact rows, straight from the collide output in pair order
   int ncon = 0;
+  RP_INIT;
   if constexpr (CON) {
     if (ccount != nullptr) {
       const int nw = (m.npair + 31) >> 5;
@@ -290,6 +305,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
           // everything this pair needs, loaded once and all in flight together: the count,
           // the pair's constants and every slot it may fill (cap <= PAIR_MAXCON; a set mask
           // bit means at least one contact, and slots past the count are never used)
+          RP_MARK(3);
           const int cnt = ccount[(size_t)p * n + e];
           const int s0 = m.pair_slot[p], cap = m.pair_cap[p];
           const int b1 = m.pair_body1[p], b2 = m.pair_body2[p];
@@ -326,6 +342,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
               fr[3] = y[0] * inv, fr[4] = y[1] * inv, fr[5] = y[2] * inv;
               cross(fr + 6, fr, fr + 3);
             }
+            RP_MARK(0);
             // relative translational Jacobian (body2 - body1) at the contact point, contact frame
             float jd[3][NV];
 #pragma unroll
@@ -364,6 +381,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
               }
             }
             const bool ta = flags & TOUCH_ARM;
+            RP_MARK(1);
             const float imp = impedance(si, cdist, margin);
             const float diag = tran + mu * mu * tran;
             const float R0 = fmaxf(MINVALF, (1.f - imp) * diag / imp);
@@ -399,6 +417,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
 #pragma unroll
               for (int k2 = 0; k2 < 6; k2++) L.at(ncon, F_GRAM + k2) = G[k2];
             }
+            RP_MARK(2);
 #pragma unroll
             for (int ed = 0; ed < 4; ed++) {
               const float s = (ed & 1) ? -mu : mu;
@@ -429,6 +448,8 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       }
     }
   }
+  RP_MARK(3);
+  RP_STORE;
   const int nl = ncon < LDS_CON ? ncon : LDS_CON;
 #ifdef SOARM_PHASE_PROF
   if (e < 65536) g_pgs_prof[8 * e + 6] = clock64();  // rows built

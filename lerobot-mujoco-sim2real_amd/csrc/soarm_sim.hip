@@ -165,7 +165,7 @@ DEVI void write_obs(const Sim<NA, NF>& S, float* obs, int e) {
 //   [19..22] waves per sweep variant (y-pure, y+arm slot, block-first general, other),
 //   [23..26] max wave cycles per variant, [27] waves with a non-block contact on the free body
 //   [28..42] wave cycles between consecutive fine stamps (g_stamp, see PSTAMP sites)
-__device__ unsigned long long g_phase[53];
+__device__ unsigned long long g_phase[57];  // [53..56] contact-row build split (g_rowprof)
 #define PHASE_T(v) const long long v = clock64()
 #else
 #define PHASE_T(v)
@@ -405,6 +405,7 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
     }
     atomicAdd(&g_phase[27], (unsigned long long)anyfree);
     for (int k = 0; k < 15; k++) atomicAdd(&g_phase[28 + k], (unsigned long long)(g_stamp[16 * e + k + 1] - g_stamp[16 * e + k]));
+    for (int k = 0; k < 4; k++) atomicAdd(&g_phase[53 + k], (unsigned long long)g_rowprof[4 * e + k]);
     atomicAdd(&g_phase[16], (unsigned long long)(g_pgs_prof[8 * e + 6] - t2));
     atomicAdd(&g_phase[17], (unsigned long long)(g_pgs_prof[8 * e + 7] - g_pgs_prof[8 * e + 6]));
     atomicAdd(&g_phase[18], (unsigned long long)(p0 - g_pgs_prof[8 * e + 7]));
@@ -1088,12 +1089,12 @@ int sim_collide_profile(sim_batch* b, const sim_state* s, double* cycles, void* 
 int sim_phase_profile(double* out, int reset) {
   if (!out) return fail(SIM_E_ARG, "null output");
 #ifdef SOARM_PHASE_PROF
-  unsigned long long h[53];
+  unsigned long long h[57];
   HIPCHECK(hipDeviceSynchronize());
   HIPCHECK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_phase), sizeof(h)));
-  for (int k = 0; k < 53; k++) out[k] = (double)h[k];
+  for (int k = 0; k < 57; k++) out[k] = (double)h[k];
   if (reset) {
-    const unsigned long long z[53] = {};
+    const unsigned long long z[57] = {};
     HIPCHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof(z)));
   }
   return SIM_OK;

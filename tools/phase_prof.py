@@ -44,7 +44,7 @@ q0 = W.initial_qpos(cm, ids, 0)
 sim.reset(init_qpos=q0[:, :5], extra_qpos=q0, seed=0)
 tab = {k: (torch.as_tensor(v, dtype=torch.float32, device="cuda") if isinstance(v, np.ndarray) else v)
        for k, v in W.chirp_tables(ids, 0).items()}
-out = (ctypes.c_double * 53)()
+out = (ctypes.c_double * 57)()
 res = {}
 every = int(os.environ.get("EVERY", 0))
 starts = set(range(0, T, every)) if every else {0, T // 2, T - 10}
@@ -79,6 +79,8 @@ for t in range(T):
                   "kinematics2", "geom poses"]
         r["stamps_per_wave"] = {nm: round(v[28 + i] / max(v[5], 1)) for i, nm in enumerate(stamps)}
         r["nony_lanes"] = {"npost": v[43:47], "free_extras": v[47:50], "nl>5": v[50], "limit": v[51], "overflow": v[52]}
+        r["row_split_per_wave"] = {nm: round(v[53 + i] / max(v[5], 1)) for i, nm in
+                                   enumerate(["loads+frame", "jacobian", "gram", "edges+writes"])}
         res[t] = r
         print(t, json.dumps(r), flush=True)
 json.dump(res, open(os.path.join(ROOT, "gpurun_out", "phase_prof.json"), "w"), indent=1)
