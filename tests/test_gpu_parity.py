@@ -231,7 +231,7 @@ def test_one_substep_with_contacts(gpu_lib, cube_model):
     assert to_np(S.ncon).sum() == st["ncon"].sum()
 
 
-def _bench_states(name, n, steps, seed=0):
+def _bench_states(name, n, steps, seed=0, nthreads=8):
     """Oracle states of a bench workload after `steps` env-steps (chirp inputs), fp32-rounded."""
     from lerobot_mujoco_sim2real_amd import workloads as W
     cm = W.model(name)
@@ -246,7 +246,7 @@ def _bench_states(name, n, steps, seed=0):
         p = W.dr_params(ids, seed)
         prm = np.stack([p["mass_scale"], p["friction"], p["damping_scale"]], 1).astype(np.float32).astype(np.float64)
     for t in range(steps):
-        orc.step(st, W.chirp_action(tab, t), params=prm, nthreads=8)
+        orc.step(st, W.chirp_action(tab, t), params=prm, nthreads=nthreads)
     return cm, orc, f32(st), prm
 
 
@@ -264,6 +264,52 @@ def test_one_substep_bench_state_mixed_contacts(gpu_lib):
     np.testing.assert_allclose(to_np(S.qpos).T, st["qpos"], atol=5e-6)
     np.testing.assert_allclose(to_np(S.qvel).T, st["qvel"], atol=5e-3)
     assert to_np(S.ncon).sum() == st["ncon"].sum()
+
+
+def test_one_substep_extra_contact_sweeps(gpu_lib):
+    """The contact-space PGS variants (soarm_pgs.h ysweeps): waves whose lanes carry the
+    cube's block plus one arm-only extra contact, one arm-cube extra, or both (the two-slot
+    variant), assembled from late bench states (oracle census of each env's contacts) so
+    that every variant runs; one substep against the oracle."""
+    from lerobot_mujoco_sim2real_amd import workloads as W
+    nb = 4096  # arm-cube contacts are rare (~0.5% of envs at t = 100)
+    cm, orc, st, _ = _bench_states("contact", nb, 100, nthreads=16)
+    names = cm.geom_names
+    table, cube = names.index("table"), names.index("cube")
+    cats = {k: [] for k in ("block", "arm", "coupled", "both")}
+    for i in range(nb):
+        fw = orc.forward(st["qpos"][i], st["qvel"][i], st["ctrl"][i], st["warm"][i])
+        g = [(int(c[7]), int(c[8])) for c in fw["contacts"]]
+        blk = [x for x in g if set(x) == {table, cube}]
+        ext = [x for x in g if set(x) != {table, cube}]
+        if len(blk) == 0 or len(blk) > 4:
+            continue
+        onc = [cube in x for x in ext]
+        if not ext:
+            cats["block"].append(i)
+        elif len(ext) == 1:
+            cats["coupled" if onc[0] else "arm"].append(i)
+        elif len(ext) == 2 and not onc[0]:
+            cats["both"].append(i)
+    counts = {k: len(v) for k, v in cats.items()}
+    assert counts["arm"] > 0 and counts["coupled"] + counts["both"] > 0, counts
+    # one wave per category (lanes filled with block-only envs), then a mixed wave
+    pick = []
+    for k in ("arm", "coupled", "both"):
+        ids = (cats[k] * 64)[:64] if cats[k] else []
+        pick += ids + cats["block"][: 64 - len(ids)] if ids else []
+    pick += (cats["arm"] + cats["coupled"] + cats["both"] + cats["block"]) [:64]
+    pick = np.array(pick[: (len(pick) // 64) * 64])
+    sub = {k: v[pick].copy() for k, v in st.items()}
+    n = len(pick)
+    S = make_sim(cm, n)
+    sub["ncon"][:] = 0
+    load_state(S, sub)
+    S.substeps(1)
+    orc.step(sub, None, nsub=1)
+    np.testing.assert_allclose(to_np(S.qpos).T, sub["qpos"], atol=5e-6)
+    np.testing.assert_allclose(to_np(S.qvel).T, sub["qvel"], atol=5e-3)
+    assert to_np(S.ncon).sum() == sub["ncon"].sum()
 
 
 def test_one_substep_domain_randomised(gpu_lib):
