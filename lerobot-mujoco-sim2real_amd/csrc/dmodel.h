@@ -69,6 +69,14 @@ struct DModel {
   const int32_t* hull_adj;   // local neighbour ids
   const uint16_t* hull_lut;  // per mesh geom: HULL_LUT_CELLS start vertices (cube-map of directions)
   int geom_lutadr[MAXG];     // first LUT entry of each mesh geom (-1: not a mesh)
+  // hill-climbing records, 32 B per vertex (two uint4): [0] x, y, z (float bits), degree |
+  // overflow offset << 8; [1] the first 8 neighbour ids (local, uint16, padded with the
+  // vertex itself).  Neighbours past 8 live in hull_ovf.  hull_lutrec holds, per LUT cell,
+  // a copy of its start vertex's record, so a query opens with one load and each climbing
+  // step is one round trip (coordinates and neighbour ids of all candidates together).
+  const uint4* hull_rec;
+  const uint4* hull_lutrec;
+  const uint16_t* hull_ovf;
 };
 
 // Support-point start table: a cube map of HULL_LUT_K x HULL_LUT_K cells per

@@ -62,40 +62,59 @@ struct PairOut {
   float c[PAIR_MAXCON][7];  // dist, pos(3), normal(3) geom1 -> geom2
 };
 
-// hill-climbing support on a mesh hull; returns the local vertex
+// hill-climbing support on a mesh hull; returns the local vertex.  Opens at the cube-map
+// cell's start record (coordinates + neighbour ids in one load) and climbs to the best
+// neighbour while one improves; each step loads all candidates' records together (their
+// coordinates to compare, their neighbour ids for the next step), so a step is one
+// dependent round trip.  Same comparisons, order and result as a CSR walk.
 DEVI float3 hull_support(const DModel& m, int g, const float l[3]) {
-  const float4* v = m.hull_vert + m.geom_hulladr[g];
+  const uint4* rec = m.hull_rec + 2 * m.geom_hulladr[g];
+  const uint4* lr = m.hull_lutrec + 2 * (m.geom_lutadr[g] + lut_cell(l[0], l[1], l[2]));
+  uint4 r0 = lr[0], r1 = lr[1];
   const int nvert = m.geom_hullnum[g];
-  // start at the cube-map cell's vertex (the table is shared by the whole wave: one
-  // pair per block, so these loads hit the same few cache lines)
-  int cur = m.hull_lut[m.geom_lutadr[g] + lut_cell(l[0], l[1], l[2])];
-  float4 cv = v[cur];
-  float cd = l[0] * cv.x + l[1] * cv.y + l[2] * cv.z;
+  auto dotr = [&](const uint4& r) {
+    return l[0] * __uint_as_float(r.x) + l[1] * __uint_as_float(r.y) + l[2] * __uint_as_float(r.z);
+  };
+  float cd = dotr(r0);
   for (int guard = 0; guard < nvert; guard++) {
-    // the vertex record carries its adjacency range: one dependent round trip for the
-    // neighbour ids, one for their coordinates (8 at a time, loads issued together)
-    const uint32_t w = __float_as_uint(cv.w);
-    const int a0 = (int)(w >> 8), a1 = a0 + (int)(w & 255u);
-    int nxt = cur;
+    const uint32_t ids[4] = {r1.x, r1.y, r1.z, r1.w};
+    uint4 c0[8], c1[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const uint32_t u = (ids[k >> 1] >> (16 * (k & 1))) & 0xffffu;
+      c0[k] = rec[2 * u], c1[k] = rec[2 * u + 1];
+    }
     float nd = cd;
-    float4 nv = cv;
-    for (int a = a0; a < a1; a += 8) {
-      int u[8];
+    int best = -1;
 #pragma unroll
-      for (int k = 0; k < 8; k++) u[k] = (a + k < a1) ? m.hull_adj[a + k] : cur;
-      float4 wv[8];
+    for (int k = 0; k < 8; k++) {
+      const float s = dotr(c0[k]);
+      if (s > nd) nd = s, best = k;
+    }
+    uint4 b0 = r0, b1 = r1;
 #pragma unroll
-      for (int k = 0; k < 8; k++) wv[k] = v[u[k]];
+    for (int k = 0; k < 8; k++)
+      if (k == best) b0 = c0[k], b1 = c1[k];
+    const int deg = (int)(r0.w & 255u);
+    if (deg > 8) {  // hub vertex (~2%): the rest of its neighbours, 8 per round trip
+      const uint16_t* ov = m.hull_ovf + (r0.w >> 8);
+      for (int a = 8; a < deg; a += 8) {
 #pragma unroll
-      for (int k = 0; k < 8; k++) {
-        const float s = l[0] * wv[k].x + l[1] * wv[k].y + l[2] * wv[k].z;
-        if (s > nd) nd = s, nxt = u[k], nv = wv[k];
+        for (int k = 0; k < 8; k++) {
+          const uint32_t u = (a + k < deg) ? ov[a - 8 + k] : ov[a - 8];
+          c0[k] = rec[2 * u], c1[k] = rec[2 * u + 1];
+        }
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+          const float s = dotr(c0[k]);
+          if (s > nd) nd = s, b0 = c0[k], b1 = c1[k], best = 8;
+        }
       }
     }
-    if (nxt == cur) break;
-    cur = nxt, cd = nd, cv = nv;
+    if (best < 0) break;
+    r0 = b0, r1 = b1, cd = nd;
   }
-  return make_float3(cv.x, cv.y, cv.z);
+  return make_float3(__uint_as_float(r0.x), __uint_as_float(r0.y), __uint_as_float(r0.z));
 }
 
 // world support point of geom g (type uniform across the wave)

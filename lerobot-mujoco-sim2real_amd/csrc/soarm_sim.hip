@@ -39,6 +39,8 @@ struct sim_model {
   std::vector<float4> hull_vert;
   std::vector<int32_t> hull_adr, hull_adj;
   std::vector<uint16_t> hull_lut;
+  std::vector<uint4> hull_rec, hull_lutrec;  // climbing records (dmodel.h)
+  std::vector<uint16_t> hull_ovf;
   int lutadr[SIM_MAXGEOM];
   int na = 0, nf = 0;
 };
@@ -50,6 +52,8 @@ struct sim_batch {
   float4* d_hv = nullptr;
   int32_t *d_hadr = nullptr, *d_hadj = nullptr;
   uint16_t* d_hlut = nullptr;
+  uint4 *d_hrec = nullptr, *d_hlutrec = nullptr;
+  uint16_t* d_hovf = nullptr;
   float* d_scratch = nullptr;  // contact rows, [slot][env]
   size_t scratch_floats = 0;
   float* d_gpose = nullptr;    // geom world poses [geom*12+k][env]
@@ -847,6 +851,39 @@ int sim_model_create(const sim_model_desc* desc, const float* hull_vert, const i
     }
     k++;
   }
+  // climbing records: coordinates, degree and the first 8 neighbours in 32 B per vertex
+  M->hull_rec.assign((size_t)2 * std::max(desc->nhullvert, 1), make_uint4(0, 0, 0, 0));
+  M->hull_ovf.assign(1, 0);
+  for (int g = 0; g < desc->ngeom; g++) {
+    if (desc->geom_type[g] != SIM_GEOM_MESH) continue;
+    const int base = desc->geom_hulladr[g];
+    for (int li = 0; li < desc->geom_hullnum[g]; li++) {
+      const int i = base + li;
+      const int32_t a0 = M->hull_adr[i], deg = M->hull_adr[i + 1] - a0;
+      const size_t ovf = M->hull_ovf.size();
+      for (int a = 8; a < deg; a++) M->hull_ovf.push_back((uint16_t)M->hull_adj[a0 + a]);
+      if (ovf >= (1u << 24)) {
+        delete M;
+        return fail(SIM_E_MODEL, "hull adjacency overflow table too large");
+      }
+      uint32_t xb, yb, zb;
+      memcpy(&xb, &hull_vert[3 * i], 4), memcpy(&yb, &hull_vert[3 * i + 1], 4), memcpy(&zb, &hull_vert[3 * i + 2], 4);
+      M->hull_rec[2 * i] = make_uint4(xb, yb, zb, (uint32_t)deg | (deg > 8 ? (uint32_t)ovf << 8 : 0u));
+      uint32_t id[8];
+      for (int a = 0; a < 8; a++) id[a] = a < deg ? (uint32_t)M->hull_adj[a0 + a] : (uint32_t)li;
+      M->hull_rec[2 * i + 1] = make_uint4(id[0] | id[1] << 16, id[2] | id[3] << 16, id[4] | id[5] << 16, id[6] | id[7] << 16);
+    }
+  }
+  M->hull_lutrec.assign((size_t)2 * M->hull_lut.size(), make_uint4(0, 0, 0, 0));
+  for (int g = 0; g < desc->ngeom; g++) {
+    if (M->lutadr[g] < 0) continue;
+    for (int c = 0; c < HULL_LUT_CELLS; c++) {
+      const size_t cell = (size_t)M->lutadr[g] + c;
+      const size_t v = (size_t)desc->geom_hulladr[g] + M->hull_lut[cell];
+      M->hull_lutrec[2 * cell] = M->hull_rec[2 * v];
+      M->hull_lutrec[2 * cell + 1] = M->hull_rec[2 * v + 1];
+    }
+  }
   *out = M;
   return SIM_OK;
 }
@@ -879,6 +916,18 @@ int sim_batch_create(const sim_model* m, int n_envs, int device, sim_batch** out
   HIPCHECK(hipMalloc(&B->d_hlut, m->hull_lut.size() * sizeof(uint16_t)));
   HIPCHECK(hipMemcpy(B->d_hlut, m->hull_lut.data(), m->hull_lut.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
   dm.hull_lut = B->d_hlut;
+  auto up = [&](auto& dst, const auto& src) {
+    using T = typename std::remove_reference<decltype(src)>::type::value_type;
+    HIPCHECK(hipMalloc(&dst, src.size() * sizeof(T)));
+    HIPCHECK(hipMemcpy(dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice));
+    return 0;
+  };
+  if (int rc = up(B->d_hrec, m->hull_rec)) return rc;
+  if (int rc = up(B->d_hlutrec, m->hull_lutrec)) return rc;
+  if (int rc = up(B->d_hovf, m->hull_ovf)) return rc;
+  dm.hull_rec = B->d_hrec;
+  dm.hull_lutrec = B->d_hlutrec;
+  dm.hull_ovf = B->d_hovf;
   for (int g = 0; g < MAXG; g++) dm.geom_lutadr[g] = g < m->desc.ngeom ? m->lutadr[g] : -1;
   HIPCHECK(hipMalloc(&B->d_model, sizeof(DModel)));
   HIPCHECK(hipMemcpy(B->d_model, &dm, sizeof(DModel), hipMemcpyHostToDevice));
@@ -905,6 +954,9 @@ void sim_batch_free(sim_batch* b) {
   (void)hipFree(b->d_hadr);
   (void)hipFree(b->d_hadj);
   (void)hipFree(b->d_hlut);
+  (void)hipFree(b->d_hrec);
+  (void)hipFree(b->d_hlutrec);
+  (void)hipFree(b->d_hovf);
   (void)hipFree(b->d_scratch);
   (void)hipFree(b->d_gpose);
   (void)hipFree(b->d_cbuf);
