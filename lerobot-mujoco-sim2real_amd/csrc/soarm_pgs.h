@@ -58,6 +58,25 @@ __device__ long long g_rowprof[65536 * 4];
 #endif
 
 constexpr int LDS_CON = 6;  // contacts whose rows stay in LDS
+// Lanes per env of the contact substep kernel for scenes with a free body: 4 lanes run the
+// same per-env code (identical values, so identical stores), and the contact-space sweep
+// of the cube block gives lane k ownership of block contact k's y (its cross-Gram row),
+// broadcasting y within the quad (DPP) on that contact's turn.
+#ifndef SOARM_LPE
+#define SOARM_LPE 4
+#endif
+template <int NF>
+constexpr int lpe() { return NF == 1 ? SOARM_LPE : 1; }
+// value of lane J of each quad (DPP quad_perm broadcast); J is a compile-time 0..3
+DEVI float qbcast(float x, int j) {
+  const int b = __float_as_int(x);
+  switch (j) {
+    case 0: return __int_as_float(__builtin_amdgcn_mov_dpp(b, 0x00, 0xF, 0xF, false));
+    case 1: return __int_as_float(__builtin_amdgcn_mov_dpp(b, 0x55, 0xF, 0xF, false));
+    case 2: return __int_as_float(__builtin_amdgcn_mov_dpp(b, 0xAA, 0xF, 0xF, false));
+    default: return __int_as_float(__builtin_amdgcn_mov_dpp(b, 0xFF, 0xF, 0xF, false));
+  }
+}
 constexpr int CF = 61;      // LDS floats per contact record
 // record fields: [0, 3*12) J_n | J_t1 | J_t2 (12 slots each), 36..39 aref_e,
 // 40..43 ARdiag_e / 2, 44..47 force_e, 48..51 1/ARdiag_e, 52 mu, 53 R (pyramid),
@@ -858,6 +877,11 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   float yE[3] = {0.f, 0.f, 0.f}, fE[4] = {0.f, 0.f, 0.f, 0.f}, fF[4] = {0.f, 0.f, 0.f, 0.f};
   constexpr int NX = FC * (FC - 1) / 2;
   float yb[FC][3], xg[NX > 0 ? NX : 1][9];
+  constexpr bool QUAD = lpe<NF>() == 4 && NF == 1 && CON && FC == 4;
+  const int sub = QUAD ? (L.lane & 3) : 0;
+  // quad mode: this lane's block contact (sub) — its y and its cross-Gram row X_sub,j
+  // (j = sub: the contact's own 3x3 Gram block), full 3x3 per j
+  float yo[3] = {0.f, 0.f, 0.f}, xr[QUAD ? FC : 1][9];
   auto ypair = [](int j, int k) { return j * FC - j * (j + 1) / 2 + (k - j - 1); };  // j < k
   auto yblock_setup = [&]() {
     if constexpr (NF == 1 && CON) {
@@ -902,6 +926,29 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
             }
           }
         }
+      if constexpr (QUAD) {
+#pragma unroll
+        for (int q = 0; q < 3; q++) yo[q] = sub == 0 ? yb[0][q] : sub == 1 ? yb[1][q] : sub == 2 ? yb[2][q] : yb[3][q];
+#pragma unroll
+        for (int j = 0; j < FC; j++)
+#pragma unroll
+          for (int r = 0; r < 3; r++)
+#pragma unroll
+            for (int q = 0; q < 3; q++) {
+              float cand[FC];
+#pragma unroll
+              for (int k = 0; k < FC; k++) {
+                if (k == j) {  // own Gram block, symmetric packed (nn, n1, n2, 11, 12, 22)
+                  const int lo = r < q ? r : q, hi = r < q ? q : r;
+                  const int gi = lo == 0 ? hi : (lo == 1 ? 2 + hi : 5);
+                  cand[k] = L.at(cslot[k], F_GRAM + gi);
+                } else {
+                  cand[k] = k < j ? xg[ypair(k, j)][3 * r + q] : xg[ypair(j, k)][3 * q + r];
+                }
+              }
+              xr[j][3 * r + q] = sub == 0 ? cand[0] : sub == 1 ? cand[1] : sub == 2 ? cand[2] : cand[3];
+            }
+      }
     }
   };
   // per-sweep constants of the block in registers: 1/ARdiag, ARdiag/2, mu, R, the
@@ -915,10 +962,13 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
 #pragma unroll
         for (int ed = 0; ed < 4; ed++) yia[k][ed] = L.at(c, F_IARD + ed), yhd[k][ed] = L.at(c, F_HARD + ed);
         ymu[k] = L.at(c, F_MU), yRp[k] = L.at(c, F_R);
+        float G[6];
 #pragma unroll
-        for (int i = 0; i < 6; i++) yG[k][i] = L.at(c, F_GRAM + i);
+        for (int i = 0; i < 6; i++) {
+          G[i] = L.at(c, F_GRAM + i);
+          if constexpr (!QUAD) yG[k][i] = G[i];  // quad mode: the own block sits in xr
+        }
         // edge e = J_n + s_e J_t(e): s = +mu, -mu, +mu, -mu; t = 1, 1, 2, 2
-        const float* G = yG[k];
         const float mu = ymu[k];
         auto gt = [&](int e) { return (e >> 1) ? G[2] : G[1]; };                  // G_n,t(e)
         auto gtt = [&](int e, int d) {                                          // G_t(e),t(d)
@@ -943,7 +993,12 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
     if constexpr (NF == 1 && CON) {
 #pragma unroll
       for (int j = 0; j < FC; j++) {
-        const float a = yb[j][0], b = yb[j][1], cc = yb[j][2];
+        float a, b, cc;
+        if constexpr (QUAD) {  // contact j's y lives in lane j of the quad
+          a = qbcast(yo[0], j), b = qbcast(yo[1], j), cc = qbcast(yo[2], j);
+        } else {
+          a = yb[j][0], b = yb[j][1], cc = yb[j][2];
+        }
         const float mu = ymu[j], Rp = yRp[j];
         float r[4], df[4];
         r[0] = fmaf(Rp, cfo[j][0], fmaf(mu, b, a));
@@ -963,13 +1018,20 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
           improvement = fmaf(-df[ed], fmaf(yhd[j][ed], df[ed], r[ed]), improvement);
         }
         const float D[3] = {(df[0] + df[1]) + (df[2] + df[3]), mu * (df[0] - df[1]), mu * (df[2] - df[3])};
-        const float* G = yG[j];
-        yb[j][0] = fmaf(G[0], D[0], fmaf(G[1], D[1], fmaf(G[2], D[2], a)));
-        yb[j][1] = fmaf(G[1], D[0], fmaf(G[3], D[1], fmaf(G[4], D[2], b)));
-        yb[j][2] = fmaf(G[2], D[0], fmaf(G[4], D[1], fmaf(G[5], D[2], cc)));
+        if constexpr (QUAD) {  // this lane's contact moves by its row of the cross-Gram
+#pragma unroll
+          for (int rr = 0; rr < 3; rr++)
+            yo[rr] = fmaf(xr[j][3 * rr], D[0], fmaf(xr[j][3 * rr + 1], D[1], fmaf(xr[j][3 * rr + 2], D[2], yo[rr])));
+        }
+        if constexpr (!QUAD) {
+          const float* G = yG[j];
+          yb[j][0] = fmaf(G[0], D[0], fmaf(G[1], D[1], fmaf(G[2], D[2], a)));
+          yb[j][1] = fmaf(G[1], D[0], fmaf(G[3], D[1], fmaf(G[4], D[2], b)));
+          yb[j][2] = fmaf(G[2], D[0], fmaf(G[4], D[1], fmaf(G[5], D[2], cc)));
+        }
 #pragma unroll
         for (int k = 0; k < FC; k++) {
-          if (k == j) continue;
+          if (QUAD || k == j) continue;
 #pragma unroll
           for (int rr = 0; rr < 3; rr++) {
             float s = yb[k][rr];
@@ -1209,15 +1271,25 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       for (int i = 0; i < NA; i++)
         v[i] = fmaf(EX(E_W + i), D[0], fmaf(EX(E_W + 6 + i), D[1], fmaf(EX(E_W + 12 + i), D[2], v[i])));
       if constexpr (decltype(coupled)::value) {
-#pragma unroll
-        for (int k = 0; k < FC; k++)
+        if constexpr (QUAD) {
 #pragma unroll
           for (int rr = 0; rr < 3; rr++) {
-            float s = yb[k][rr];
+            float s = yo[rr];
 #pragma unroll
-            for (int qq = 0; qq < 3; qq++) s = fmaf(EX(E_X + 9 * k + 3 * rr + qq), D[qq], s);
-            yb[k][rr] = s;
+            for (int qq = 0; qq < 3; qq++) s = fmaf(EX(E_X + 9 * sub + 3 * rr + qq), D[qq], s);
+            yo[rr] = s;
           }
+        } else {
+#pragma unroll
+          for (int k = 0; k < FC; k++)
+#pragma unroll
+            for (int rr = 0; rr < 3; rr++) {
+              float s = yb[k][rr];
+#pragma unroll
+              for (int qq = 0; qq < 3; qq++) s = fmaf(EX(E_X + 9 * k + 3 * rr + qq), D[qq], s);
+              yb[k][rr] = s;
+            }
+        }
       }
       const float y0 = yE[0], y1 = yE[1], y2 = yE[2];
       yE[0] = fmaf(EX(E_G + 0), D[0], fmaf(EX(E_G + 1), D[1], fmaf(EX(E_G + 2), D[2], y0)));

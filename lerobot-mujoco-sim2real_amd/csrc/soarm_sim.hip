@@ -294,7 +294,8 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
                                                 const int* __restrict__ ccount,
                                                 uint32_t* __restrict__ pmask,
                                                 float* __restrict__ gpose) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  // lpe<NF>() lanes per env (soarm_pgs.h): they run the same per-env code
+  const int e = blockIdx.x * (64 / lpe<NF>()) + (int)threadIdx.x / lpe<NF>();
   if (e >= n) return;
   PHASE_T(t0);
   const DModel& m = *dm;
@@ -1033,7 +1034,8 @@ int sim_step(sim_batch* b, const sim_state* s, const float* action, int frame_sk
         }
         const bool last = sub == frame_skip - 1;
         prof_mark(b, 2, q);
-        hipLaunchKernelGGL((k_substep<NA, NF>), grid_for(b->n), dim3(64), 0, q, b->d_model, b->n, *s,
+        hipLaunchKernelGGL((k_substep<NA, NF>), dim3((b->n + 64 / lpe<NF>() - 1) / (64 / lpe<NF>())), dim3(64), 0, q,
+                           b->d_model, b->n, *s,
                            sub == 0 ? action : nullptr, last ? obs : nullptr, b->params, b->d_scratch,
                            b->d_cbuf, np > 0 ? b->d_ccount : nullptr, np > 0 ? b->d_pmask : nullptr,
                            last ? nullptr : b->d_gpose);
