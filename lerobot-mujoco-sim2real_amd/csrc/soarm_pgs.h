@@ -313,7 +313,180 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   // ---- contact rows, straight from the collide output in pair order
   int ncon = 0;
   RP_INIT;
-  if constexpr (CON) {
+  // Contact row c from its collide output rw (dist, pos, normal geom1 -> geom2) and its pair's
+  // constants: record c (LDS, c < LDS_CON) or the overflow slab.  split: lane-split build
+  // (quad mode), the building lane writes the record into all 4 columns of its quad.
+  auto wrec = [&](int c, int f, float x, bool split) {
+    if (split)
+      *reinterpret_cast<float4*>(&L.a[c * CF + f][L.lane & ~3]) = make_float4(x, x, x, x);
+    else
+      L.at(c, f) = x;
+  };
+  auto build_row = [&](int c, const float* rw, int b1, int b2, float mu, float tran, float margin, float KB0,
+                       float KB1, const float* si, bool split) {
+      const float cdist = rw[0];
+      const float cpos[3] = {rw[1], rw[2], rw[3]};
+      float fr[9] = {rw[4], rw[5], rw[6], 0, 0, 0, 0, 0, 0};
+      {  // contact frame (mju_makeFrame)
+        float y[3];
+        if (fabsf(fr[1]) < 0.5f)
+          y[0] = 0, y[1] = 1, y[2] = 0;
+        else
+          y[0] = 0, y[1] = 0, y[2] = 1;
+        const float dd = dot3(fr, y);
+        y[0] -= dd * fr[0], y[1] -= dd * fr[1], y[2] -= dd * fr[2];
+        const float inv = rsqrtf(dot3(y, y));
+        fr[3] = y[0] * inv, fr[4] = y[1] * inv, fr[5] = y[2] * inv;
+        cross(fr + 6, fr, fr + 3);
+      }
+      RP_MARK(0);
+      // relative translational Jacobian (body2 - body1) at the contact point, contact frame
+      float jd[3][NV];
+#pragma unroll
+      for (int i = 0; i < NV; i++) jd[0][i] = jd[1][i] = jd[2][i] = 0.f;
+      int flags = 0;
+#pragma unroll
+      for (int side = 0; side < 2; side++) {
+        const int b = side ? b2 : b1;
+        const float sg = side ? 1.f : -1.f;
+        if (b >= 2 && b < 2 + NA) flags |= TOUCH_ARM;
+#pragma unroll
+        for (int i = 0; i < NA; i++) {
+          if (b >= i + 2 && b < 2 + NA) {  // hinge i moves chain bodies i+2.. (reference point: origin)
+            float l[3];
+            cross(l, S.cdof[i], cpos);
+            const float jp[3] = {S.cdof[i][3] + l[0], S.cdof[i][4] + l[1], S.cdof[i][5] + l[2]};
+#pragma unroll
+            for (int q = 0; q < 3; q++) jd[q][i] += sg * dot3(fr + 3 * q, jp);
+          }
+        }
+#pragma unroll
+        for (int ff2 = 0; ff2 < NF; ff2++) {
+          const int fb = 2 + NA + ff2, d0 = NA + 6 * ff2;
+          if (b == fb) {
+            flags |= TOUCH_FREE;
+            const float off[3] = {cpos[0] - S.xpos[fb][0], cpos[1] - S.xpos[fb][1], cpos[2] - S.xpos[fb][2]};
+#pragma unroll
+            for (int i = 0; i < 6; i++) {
+              float l[3];
+              cross(l, S.cdof[d0 + i], off);
+              const float jp[3] = {S.cdof[d0 + i][3] + l[0], S.cdof[d0 + i][4] + l[1], S.cdof[d0 + i][5] + l[2]};
+#pragma unroll
+              for (int q = 0; q < 3; q++) jd[q][d0 + i] += sg * dot3(fr + 3 * q, jp);
+            }
+          }
+        }
+      }
+      const bool ta = flags & TOUCH_ARM;
+      RP_MARK(1);
+      const float imp = impedance(si, cdist, margin);
+      const float diag = tran + mu * mu * tran;
+      const float R0 = fmaxf(MINVALF, (1.f - imp) * diag / imp);
+      const float Rpy = 2.f * mu * mu * R0 / m.impratio;
+      const bool lds = c < LDS_CON;
+      if (lds) {
+#pragma unroll
+        for (int q = 0; q < 3; q++)
+#pragma unroll
+          for (int i = 0; i < NV; i++) wrec(c, 12 * q + i, jd[q][i], split);
+        wrec(c, F_MU, mu, split);
+        wrec(c, F_R, Rpy, split);
+        wrec(c, F_FLAGS, (float)flags, split);
+      }
+      // Gram matrix G = [Jn; Jt1; Jt2] M^-1 [Jn; Jt1; Jt2]' and the three velocities:
+      // every pyramid edge J_e = J_n + s J_tk (s = +-mu) follows from them.  Full
+      // width (jd is zero on the halves the contact does not touch; branch-free code
+      // avoids running both sides of a divergent flag test) unless no lane's contact
+      // touches the arm: then the free-body half alone (diagonal M^-1).
+      float W0[NV], W1[NV], W2[NV], G[6];
+      const bool arm_any = NF == 0 || !__all(!ta);
+      Mi.mul(jd[0], W0, arm_any, true);
+      Mi.mul(jd[1], W1, arm_any, true);
+      Mi.mul(jd[2], W2, arm_any, true);
+      G[0] = dotv<NA, NF>(jd[0], W0, arm_any, true), G[1] = dotv<NA, NF>(jd[0], W1, arm_any, true);
+      G[2] = dotv<NA, NF>(jd[0], W2, arm_any, true), G[3] = dotv<NA, NF>(jd[1], W1, arm_any, true);
+      G[4] = dotv<NA, NF>(jd[1], W2, arm_any, true), G[5] = dotv<NA, NF>(jd[2], W2, arm_any, true);
+      float vq[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < NV; i++)
+        vq[0] += jd[0][i] * S.qvel[i], vq[1] += jd[1][i] * S.qvel[i], vq[2] += jd[2][i] * S.qvel[i];
+      if (lds) {
+#pragma unroll
+        for (int k2 = 0; k2 < 6; k2++) wrec(c, F_GRAM + k2, G[k2], split);
+      }
+      RP_MARK(2);
+#pragma unroll
+      for (int ed = 0; ed < 4; ed++) {
+        const float s = (ed & 1) ? -mu : mu;
+        const bool k2 = ed >> 1;
+        const float vel = vq[0] + s * (k2 ? vq[2] : vq[1]);
+        // J_e M^-1 J_e' = G_nn + 2 s G_nk + s^2 G_kk
+        const float ard = G[0] + s * (2.f * (k2 ? G[2] : G[1]) + s * (k2 ? G[5] : G[3])) + Rpy;
+        const float ar = -KB1 * vel - KB0 * imp * (cdist - margin);
+        if (lds) {
+          wrec(c, F_AREF + ed, ar, split);
+          wrec(c, F_HARD + ed, 0.5f * ard, split);
+          wrec(c, F_IARD + ed, 1.f / ard, split);
+        } else {
+          const int r = 4 * c + ed;
+#pragma unroll
+          for (int i = 0; i < NV; i++) {
+            cr.J(r, i) = jd[0][i] + s * (k2 ? jd[2][i] : jd[1][i]);
+            cr.W(r, i) = W0[i] + s * (k2 ? W2[i] : W1[i]);
+          }
+          cr.S(r, 0) = ar;
+          cr.S(r, 1) = Rpy;
+          cr.S(r, 2) = ard;
+        }
+      }
+  };
+
+  constexpr bool QUADR = lpe<NF>() == 4 && NF == 1;
+  if constexpr (CON && QUADR) {
+    if (ccount != nullptr) {
+      // lane-split build (quad mode): every lane lists the env's contacts (pair, slot) in
+      // pair order, then lane k of the quad builds contacts k, k+4, ... of the LDS records
+      // and writes each into the quad's 4 columns; overflow contacts (rare) are built by
+      // every lane (identical values in the env's slab)
+      const int nw = (m.npair + 31) >> 5;
+      for (int w = 0; w < nw; w++) {
+        uint32_t bits = pmask[(size_t)w * n + e];
+        while (bits) {
+          const int p = 32 * w + __builtin_ctz(bits);
+          bits &= bits - 1;
+          const int cnt = ccount[(size_t)p * n + e];
+          for (int k = 0; k < cnt; k++) {
+            if (ncon >= SIM_MAXCON) {
+              S.status |= SIM_ST_CONOVERFLOW;
+              break;
+            }
+            L.ext[ncon][L.lane] = __int_as_float(p << 3 | k);
+            ncon++;
+          }
+        }
+      }
+      auto build_listed = [&](int c, bool split) {
+        const int pk = __float_as_int(L.ext[c][L.lane]);
+        const int p = pk >> 3, k = pk & 7;
+        const int s0 = m.pair_slot[p];
+        float rw[7];
+#pragma unroll
+        for (int f = 0; f < 7; f++) rw[f] = cbuf[((size_t)(s0 + k) * 7 + f) * n + e];
+        float si[5];
+#pragma unroll
+        for (int q = 0; q < 5; q++) si[q] = m.pair_solimp[p][q];
+        build_row(c, rw, m.pair_body1[p], m.pair_body2[p], S.fric >= 0.f ? S.fric : m.pair_friction[p],
+                  m.pair_tran[p], m.pair_margin[p], m.pair_KB[p][0], m.pair_KB[p][1], si, split);
+      };
+      const int nlds = ncon < LDS_CON ? ncon : LDS_CON;
+      for (int c0 = 0; c0 < nlds; c0 += 4) {
+        const int c = c0 + (L.lane & 3);
+        if (c < nlds) build_listed(c, true);
+      }
+      __syncthreads();  // the quad's records, written by its 4 lanes
+      for (int c = LDS_CON; c < ncon; c++) build_listed(c, false);
+    }
+  } else if constexpr (CON) {
     if (ccount != nullptr) {
       const int nw = (m.npair + 31) >> 5;
       for (int w = 0; w < nw; w++) {
@@ -346,121 +519,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
               S.status |= SIM_ST_CONOVERFLOW;
               break;
             }
-            const float cdist = raw[k][0];
-            const float cpos[3] = {raw[k][1], raw[k][2], raw[k][3]};
-            float fr[9] = {raw[k][4], raw[k][5], raw[k][6], 0, 0, 0, 0, 0, 0};
-            {  // contact frame (mju_makeFrame)
-              float y[3];
-              if (fabsf(fr[1]) < 0.5f)
-                y[0] = 0, y[1] = 1, y[2] = 0;
-              else
-                y[0] = 0, y[1] = 0, y[2] = 1;
-              const float dd = dot3(fr, y);
-              y[0] -= dd * fr[0], y[1] -= dd * fr[1], y[2] -= dd * fr[2];
-              const float inv = rsqrtf(dot3(y, y));
-              fr[3] = y[0] * inv, fr[4] = y[1] * inv, fr[5] = y[2] * inv;
-              cross(fr + 6, fr, fr + 3);
-            }
-            RP_MARK(0);
-            // relative translational Jacobian (body2 - body1) at the contact point, contact frame
-            float jd[3][NV];
-#pragma unroll
-            for (int i = 0; i < NV; i++) jd[0][i] = jd[1][i] = jd[2][i] = 0.f;
-            int flags = 0;
-#pragma unroll
-            for (int side = 0; side < 2; side++) {
-              const int b = side ? b2 : b1;
-              const float sg = side ? 1.f : -1.f;
-              if (b >= 2 && b < 2 + NA) flags |= TOUCH_ARM;
-#pragma unroll
-              for (int i = 0; i < NA; i++) {
-                if (b >= i + 2 && b < 2 + NA) {  // hinge i moves chain bodies i+2.. (reference point: origin)
-                  float l[3];
-                  cross(l, S.cdof[i], cpos);
-                  const float jp[3] = {S.cdof[i][3] + l[0], S.cdof[i][4] + l[1], S.cdof[i][5] + l[2]};
-#pragma unroll
-                  for (int q = 0; q < 3; q++) jd[q][i] += sg * dot3(fr + 3 * q, jp);
-                }
-              }
-#pragma unroll
-              for (int ff2 = 0; ff2 < NF; ff2++) {
-                const int fb = 2 + NA + ff2, d0 = NA + 6 * ff2;
-                if (b == fb) {
-                  flags |= TOUCH_FREE;
-                  const float off[3] = {cpos[0] - S.xpos[fb][0], cpos[1] - S.xpos[fb][1], cpos[2] - S.xpos[fb][2]};
-#pragma unroll
-                  for (int i = 0; i < 6; i++) {
-                    float l[3];
-                    cross(l, S.cdof[d0 + i], off);
-                    const float jp[3] = {S.cdof[d0 + i][3] + l[0], S.cdof[d0 + i][4] + l[1], S.cdof[d0 + i][5] + l[2]};
-#pragma unroll
-                    for (int q = 0; q < 3; q++) jd[q][d0 + i] += sg * dot3(fr + 3 * q, jp);
-                  }
-                }
-              }
-            }
-            const bool ta = flags & TOUCH_ARM;
-            RP_MARK(1);
-            const float imp = impedance(si, cdist, margin);
-            const float diag = tran + mu * mu * tran;
-            const float R0 = fmaxf(MINVALF, (1.f - imp) * diag / imp);
-            const float Rpy = 2.f * mu * mu * R0 / m.impratio;
-            const bool lds = ncon < LDS_CON;
-            if (lds) {
-#pragma unroll
-              for (int q = 0; q < 3; q++)
-#pragma unroll
-                for (int i = 0; i < NV; i++) L.at(ncon, 12 * q + i) = jd[q][i];
-              L.at(ncon, F_MU) = mu;
-              L.at(ncon, F_R) = Rpy;
-              L.at(ncon, F_FLAGS) = (float)flags;
-            }
-            // Gram matrix G = [Jn; Jt1; Jt2] M^-1 [Jn; Jt1; Jt2]' and the three velocities:
-            // every pyramid edge J_e = J_n + s J_tk (s = +-mu) follows from them.  Full
-            // width (jd is zero on the halves the contact does not touch; branch-free code
-            // avoids running both sides of a divergent flag test) unless no lane's contact
-            // touches the arm: then the free-body half alone (diagonal M^-1).
-            float W0[NV], W1[NV], W2[NV], G[6];
-            const bool arm_any = NF == 0 || !__all(!ta);
-            Mi.mul(jd[0], W0, arm_any, true);
-            Mi.mul(jd[1], W1, arm_any, true);
-            Mi.mul(jd[2], W2, arm_any, true);
-            G[0] = dotv<NA, NF>(jd[0], W0, arm_any, true), G[1] = dotv<NA, NF>(jd[0], W1, arm_any, true);
-            G[2] = dotv<NA, NF>(jd[0], W2, arm_any, true), G[3] = dotv<NA, NF>(jd[1], W1, arm_any, true);
-            G[4] = dotv<NA, NF>(jd[1], W2, arm_any, true), G[5] = dotv<NA, NF>(jd[2], W2, arm_any, true);
-            float vq[3] = {0.f, 0.f, 0.f};
-#pragma unroll
-            for (int i = 0; i < NV; i++)
-              vq[0] += jd[0][i] * S.qvel[i], vq[1] += jd[1][i] * S.qvel[i], vq[2] += jd[2][i] * S.qvel[i];
-            if (lds) {
-#pragma unroll
-              for (int k2 = 0; k2 < 6; k2++) L.at(ncon, F_GRAM + k2) = G[k2];
-            }
-            RP_MARK(2);
-#pragma unroll
-            for (int ed = 0; ed < 4; ed++) {
-              const float s = (ed & 1) ? -mu : mu;
-              const bool k2 = ed >> 1;
-              const float vel = vq[0] + s * (k2 ? vq[2] : vq[1]);
-              // J_e M^-1 J_e' = G_nn + 2 s G_nk + s^2 G_kk
-              const float ard = G[0] + s * (2.f * (k2 ? G[2] : G[1]) + s * (k2 ? G[5] : G[3])) + Rpy;
-              const float ar = -KB1 * vel - KB0 * imp * (cdist - margin);
-              if (lds) {
-                L.at(ncon, F_AREF + ed) = ar;
-                L.at(ncon, F_HARD + ed) = 0.5f * ard;
-                L.at(ncon, F_IARD + ed) = 1.f / ard;
-              } else {
-                const int r = 4 * ncon + ed;
-#pragma unroll
-                for (int i = 0; i < NV; i++) {
-                  cr.J(r, i) = jd[0][i] + s * (k2 ? jd[2][i] : jd[1][i]);
-                  cr.W(r, i) = W0[i] + s * (k2 ? W2[i] : W1[i]);
-                }
-                cr.S(r, 0) = ar;
-                cr.S(r, 1) = Rpy;
-                cr.S(r, 2) = ard;
-              }
-            }
+            build_row(ncon, raw[k], b1, b2, mu, tran, margin, KB0, KB1, si, false);
             ncon++;
           }
         }
