@@ -77,6 +77,13 @@ DEVI float qbcast(float x, int j) {
     default: return __int_as_float(__builtin_amdgcn_mov_dpp(b, 0xFF, 0xF, 0xF, false));
   }
 }
+// LDS written by other lanes of the (single-wave) workgroup is read after this
+DEVI void wave_sync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
+// sum over the quad, bit-identical in its 4 lanes (butterfly of commutative adds)
+DEVI float qsum(float x) {
+  const float t = x + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xF, 0xF, false));
+  return t + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(t), 0x4E, 0xF, 0xF, false));
+}
 constexpr int CF = 61;      // LDS floats per contact record
 // record fields: [0, 3*12) J_n | J_t1 | J_t2 (12 slots each), 36..39 aref_e,
 // 40..43 ARdiag_e / 2, 44..47 force_e, 48..51 1/ARdiag_e, 52 mu, 53 R (pyramid),
@@ -441,7 +448,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       }
   };
 
-  constexpr bool QUADR = lpe<NF>() == 4 && NF == 1;
+  constexpr bool QUADR = lpe<NF>() == 4 && NF == 1 && CON;
   if constexpr (CON && QUADR) {
     if (ccount != nullptr) {
       // lane-split build (quad mode): every lane lists the env's contacts (pair, slot) in
@@ -483,7 +490,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
         const int c = c0 + (L.lane & 3);
         if (c < nlds) build_listed(c, true);
       }
-      __syncthreads();  // the quad's records, written by its 4 lanes
+      wave_sync();  // the quad's records, written by its 4 lanes
       for (int c = LDS_CON; c < ncon; c++) build_listed(c, false);
     }
   } else if constexpr (CON) {
@@ -556,8 +563,13 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
     L.lm(l, L_FRC) = fs;
     add_arm_col(Mi, v, oh, sg * fs);
   }
-  // contacts (Gram form: J_e x = J_n x + s J_tk x; one M^-1 product per contact)
-  for (int c = 0; c < nl; c++) {
+  // contacts (Gram form: J_e x = J_n x + s J_tk x; one M^-1 product per contact); quad mode:
+  // lane k takes contacts k, k+4, ... and the quad sums the velocity changes
+  float vw[NV];
+#pragma unroll
+  for (int i = 0; i < NV; i++) vw[i] = 0.f;
+  const int cstep = QUADR ? 4 : 1, cfirst = QUADR ? (L.lane & 3) : 0;
+  for (int c = cfirst; c < nl; c += cstep) {
     float jn[NV], jt1[NV], jt2[NV];
 #pragma unroll
     for (int i = 0; i < NV; i++) jn[i] = L.at(c, i), jt1[i] = L.at(c, 12 + i), jt2[i] = L.at(c, 24 + i);
@@ -571,7 +583,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       const float s = (ed & 1) ? -mu : mu;
       const float jar = jw[0] + s * jw[1 + (ed >> 1)] - L.at(c, F_AREF + ed);
       fs[ed] = jar < 0.f ? -jar / Rp : 0.f;
-      L.at(c, F_FRC + ed) = fs[ed];
+      wrec(c, F_FRC + ed, fs[ed], QUADR);
     }
     const float Dn = (fs[0] + fs[1]) + (fs[2] + fs[3]), D1 = mu * (fs[0] - fs[1]), D2 = mu * (fs[2] - fs[3]);
     float u[NV], w[NV];
@@ -579,8 +591,10 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
     for (int i = 0; i < NV; i++) u[i] = jn[i] * Dn + jt1[i] * D1 + jt2[i] * D2;
     Mi.mul(u, w, true, true);
 #pragma unroll
-    for (int i = 0; i < NV; i++) v[i] += w[i];
+    for (int i = 0; i < NV; i++) vw[i] += w[i];
   }
+#pragma unroll
+  for (int i = 0; i < NV; i++) v[i] += QUADR ? qsum(vw[i]) : vw[i];
   for (int c = nl; c < ncon; c++)
     for (int ed = 0; ed < 4; ed++) {
       const int r = 4 * c + ed;
@@ -603,7 +617,8 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
     const float sg = L.lm(l, L_SGN), f = L.lm(l, L_FRC), ar = L.lm(l, L_AREF);
     cost += 0.5f * f * (sg * pick<NA>(v, oh) - ar + L.lm(l, L_R) * f) + 0.5f * f * (sg * pick<NA>(S.qacc_s, oh) - ar);
   }
-  for (int c = 0; c < nl; c++) {
+  float ccost = 0.f;  // contacts' share (quad mode: lane k's contacts, summed over the quad)
+  for (int c = cfirst; c < nl; c += cstep) {
     float jn[NV], jt1[NV], jt2[NV];
 #pragma unroll
     for (int i = 0; i < NV; i++) jn[i] = L.at(c, i), jt1[i] = L.at(c, 12 + i), jt2[i] = L.at(c, 24 + i);
@@ -618,10 +633,12 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
     for (int ed = 0; ed < 4; ed++) {
       const float s = (ed & 1) ? -mu : mu;
       const float fr = L.at(c, F_FRC + ed), ar = L.at(c, F_AREF + ed);
-      cost += 0.5f * fr * (jv[0] + s * jv[1 + (ed >> 1)] - ar + Rp * fr) +
-              0.5f * fr * (jq[0] + s * jq[1 + (ed >> 1)] - ar);
+      ccost += 0.5f * fr * (jv[0] + s * jv[1 + (ed >> 1)] - ar + Rp * fr) +
+               0.5f * fr * (jq[0] + s * jq[1 + (ed >> 1)] - ar);
     }
   }
+  cost += QUADR ? qsum(ccost) : ccost;
+  if constexpr (QUADR) wave_sync();  // F_FRC of the quad's contacts, written by their lanes
   for (int c = nl; c < ncon; c++)
     for (int ed = 0; ed < 4; ed++) {
       const int r = 4 * c + ed;
