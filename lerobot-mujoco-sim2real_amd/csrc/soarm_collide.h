@@ -614,11 +614,13 @@ DEVI void box_box(const DModel& m, int g1, int g2, const GeomPose& P1, const Geo
 
 // world poses of every collidable geom of this env -> global SoA [geom*12+k][env]
 template <int NA, int NF>
-DEVI void write_geom_poses(const Sim<NA, NF>& S, float* __restrict__ gpose, int n, int e) {
+// geoms g0, g0 + gstep, ... (quad mode: lane k of the quad writes every 4th geom)
+DEVI void write_geom_poses(const Sim<NA, NF>& S, float* __restrict__ gpose, int n, int e, int g0 = 0,
+                           int gstep = 1) {
   const DModel& m = *S.mp;
   constexpr int NB = Sim<NA, NF>::NB;
-  for (int g = 0; g < m.ngeom; g++) {
-    const int b = m.geom_bodyid[g];  // wave-uniform
+  for (int g = g0; g < m.ngeom; g += gstep) {
+    const int b = m.geom_bodyid[g];  // wave-uniform unless gstep > 1
     float bp[3] = {0, 0, 0}, bR[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
 #pragma unroll
     for (int k = 1; k < NB; k++)

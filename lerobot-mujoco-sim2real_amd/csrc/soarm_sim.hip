@@ -369,7 +369,7 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
   if (gpose) {
     S.kinematics();
     PSTAMP(14);
-    write_geom_poses(S, gpose, n, e);
+    write_geom_poses(S, gpose, n, e, (int)threadIdx.x % lpe<NF>(), lpe<NF>());
   }
 #ifdef SOARM_PHASE_PROF
   PHASE_T(t5);
