@@ -99,17 +99,26 @@ template <int NA, int NF>
 constexpr int keep_floats() { return NA * (NA + 1) / 2 + 6 * NF + (NA + 6 * NF) + 3; }
 // joint-limit rows (rare): compact list, one record per active limit
 constexpr int LF = 7;  // dof, sign, aref, R, ARdiag, 1/ARdiag, force
-constexpr int XS_EXT = 98;  // floats per lane of extra-slot scratch beyond the limit list
+constexpr int XS_LIST = SIM_MAXCON;           // ext[0, XS_LIST): the env's contact list (quad build)
+constexpr int XS_EXT = XS_LIST + 98;           // + extra-slot scratch beyond the limit list
 enum { L_DOF = 0, L_SGN = 1, L_AREF = 2, L_R = 3, L_ARD = 4, L_IARD = 5, L_FRC = 6 };
 
+// Per-env LDS state, [field][column]: one column per env of the workgroup (64 / lanes per
+// env); the lanes of an env share its column (identical values, or records written by the
+// one lane that built them).
 struct RowLds {
-  float (*a)[64];    // [(LDS_CON + 1) * CF][64] contact records + a zero record (null: contact-free kernel)
-  float (*lim)[64];  // [NA * LF][64] active joint-limit records
-  float (*keep)[64]; // [KEEP][64] state held in LDS across the PGS sweeps (null: kept in registers)
-  float (*ext)[64];  // [XS_EXT][64] scratch of the y sweep's extra contact slots
-  int lane;
-  DEVI float& at(int c, int f) const { return a[c * CF + f][lane]; }
-  DEVI float& lm(int l, int f) const { return lim[l * LF + f][lane]; }
+  float* a;     // [(LDS_CON + 1) * CF][cols] contact records + a zero record (null: contact-free kernel)
+  float* lim;   // [NA * LF][cols] active joint-limit records
+  float* keep;  // [KEEP][cols] state held in LDS across the PGS sweeps (null: kept in registers)
+  float* ext;   // [XS_EXT][cols] scratch of the y sweep (contact list, extra contact slots)
+  int lane;     // thread in the workgroup
+  int col;      // this env's column
+  int cols;     // columns (envs per workgroup)
+  DEVI float& at(int c, int f) const { return a[(c * CF + f) * cols + col]; }
+  DEVI float& lm(int l, int f) const { return lim[(l * LF + f) * cols + col]; }
+  DEVI float& lraw(int k) const { return lim[k * cols + col]; }
+  DEVI float& kp(int k) const { return keep[k * cols + col]; }
+  DEVI float& ex(int k) const { return ext[k * cols + col]; }
 };
 
 template <int NA, int NF>
@@ -324,10 +333,8 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   // constants: record c (LDS, c < LDS_CON) or the overflow slab.  split: lane-split build
   // (quad mode), the building lane writes the record into all 4 columns of its quad.
   auto wrec = [&](int c, int f, float x, bool split) {
-    if (split)
-      *reinterpret_cast<float4*>(&L.a[c * CF + f][L.lane & ~3]) = make_float4(x, x, x, x);
-    else
-      L.at(c, f) = x;
+    (void)split;  // the env's column is shared by its lanes: one store serves the quad
+    L.at(c, f) = x;
   };
   auto build_row = [&](int c, const float* rw, int b1, int b2, float mu, float tran, float margin, float KB0,
                        float KB1, const float* si, bool split) {
@@ -467,13 +474,13 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
               S.status |= SIM_ST_CONOVERFLOW;
               break;
             }
-            L.ext[ncon][L.lane] = __int_as_float(p << 3 | k);
+            L.ex(ncon) = __int_as_float(p << 3 | k);
             ncon++;
           }
         }
       }
       auto build_listed = [&](int c, bool split) {
-        const int pk = __float_as_int(L.ext[c][L.lane]);
+        const int pk = __float_as_int(L.ex(c));
         const int p = pk >> 3, k = pk & 7;
         const int s0 = m.pair_slot[p];
         float rw[7];
@@ -678,15 +685,15 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   if (L.keep) {  // park what only the post-solve stages need (restored below)
     int k = 0;
 #pragma unroll
-    for (int i = 0; i < NA * (NA + 1) / 2; i++) L.keep[k++][L.lane] = S.MA[i];
+    for (int i = 0; i < NA * (NA + 1) / 2; i++) L.kp(k++) = S.MA[i];
 #pragma unroll
     for (int f2 = 0; f2 < NF; f2++)
 #pragma unroll
-      for (int i = 0; i < 6; i++) L.keep[k++][L.lane] = S.MF[f2][i * (i + 1) / 2 + i];
+      for (int i = 0; i < 6; i++) L.kp(k++) = S.MF[f2][i * (i + 1) / 2 + i];
 #pragma unroll
-    for (int i = 0; i < NV; i++) L.keep[k++][L.lane] = S.fsmooth[i];
+    for (int i = 0; i < NV; i++) L.kp(k++) = S.fsmooth[i];
 #pragma unroll
-    for (int i = 0; i < 3; i++) L.keep[k++][L.lane] = S.ee[i];
+    for (int i = 0; i < 3; i++) L.kp(k++) = S.ee[i];
   }
 #ifdef SOARM_PHASE_PROF
   if (e < 65536) g_pgs_prof[8 * e] = clock64();
@@ -948,8 +955,8 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   // J_arm rows, W_F = M_arm^-1 J_F', edge Gram, 1/ARd, ARd/2, mu, R, aref shift, X_EF = J_E M^-1 J_F'
   enum { F_J = 76, F_W = 94, F_A = 112, F_IA = 118, F_HD = 122, F_MUX = 126, F_RPX = 127, F_SH = 128, F_XE = 131,
          XS_END = 140 };
-  static_assert(XS_END <= NA * LF + XS_EXT, "extra-slot scratch fits");
-  auto EX = [&](int k) -> float& { return k < NA * LF ? L.lim[k][L.lane] : L.ext[k - NA * LF][L.lane]; };
+  static_assert(XS_END <= NA * LF + XS_EXT - XS_LIST, "extra-slot scratch fits");
+  auto EX = [&](int k) -> float& { return k < NA * LF ? L.lraw(k) : L.ex(XS_LIST + k - NA * LF); };
   float yE[3] = {0.f, 0.f, 0.f}, fE[4] = {0.f, 0.f, 0.f, 0.f}, fF[4] = {0.f, 0.f, 0.f, 0.f};
   constexpr int NX = FC * (FC - 1) / 2;
   float yb[FC][3], xg[NX > 0 ? NX : 1][9];
@@ -1480,17 +1487,17 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   if (L.keep) {
     int k = 0;
 #pragma unroll
-    for (int i = 0; i < NA * (NA + 1) / 2; i++) S.MA[i] = L.keep[k++][L.lane];
+    for (int i = 0; i < NA * (NA + 1) / 2; i++) S.MA[i] = L.kp(k++);
 #pragma unroll
     for (int f2 = 0; f2 < NF; f2++)
 #pragma unroll
       for (int i = 0; i < 6; i++)
 #pragma unroll
-        for (int j = 0; j <= i; j++) S.MF[f2][i * (i + 1) / 2 + j] = (i == j) ? L.keep[k++][L.lane] : 0.f;
+        for (int j = 0; j <= i; j++) S.MF[f2][i * (i + 1) / 2 + j] = (i == j) ? L.kp(k++) : 0.f;
 #pragma unroll
-    for (int i = 0; i < NV; i++) S.fsmooth[i] = L.keep[k++][L.lane];
+    for (int i = 0; i < NV; i++) S.fsmooth[i] = L.kp(k++);
 #pragma unroll
-    for (int i = 0; i < 3; i++) S.ee[i] = L.keep[k++][L.lane];
+    for (int i = 0; i < 3; i++) S.ee[i] = L.kp(k++);
   }
 #ifdef SOARM_PHASE_PROF
   if (e < 65536)

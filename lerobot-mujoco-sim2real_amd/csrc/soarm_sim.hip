@@ -204,7 +204,7 @@ __global__ __launch_bounds__(64) void k_step(const DModel* __restrict__ dm, int 
       if (k < m.nact) S.ctrl[k] = action[(size_t)e * m.nact + k];
   }
   __shared__ float s_lim[NA * LF][64];
-  const RowLds L{nullptr, s_lim, nullptr, nullptr, (int)threadIdx.x};
+  const RowLds L{nullptr, &s_lim[0][0], nullptr, nullptr, (int)threadIdx.x, (int)threadIdx.x, 64};
   const ContactRows<NA, NF> cr{nullptr, n};
   for (int s = 0; s < nsub; s++) {
     S.relaunder();
@@ -307,11 +307,13 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
     for (int k = 0; k < NA; k++)
       if (k < m.nact) S.ctrl[k] = action[(size_t)e * m.nact + k];
   }
-  __shared__ float s_rows[(LDS_CON + 1) * CF][64];  // + one all-zero record
-  __shared__ float s_lim[NA * LF][64];
-  __shared__ float s_keep[keep_floats<NA, NF>()][64];
-  __shared__ float s_ext[NF == 1 ? XS_EXT : 1][64];  // y sweep: extra-contact slot coefficients
-  const RowLds L{s_rows, s_lim, NF == 1 ? s_keep : nullptr, s_ext, (int)threadIdx.x};
+  constexpr int COLS = 64 / lpe<NF>();  // envs per workgroup: one LDS column each
+  __shared__ float s_rows[(LDS_CON + 1) * CF][COLS];  // + one all-zero record
+  __shared__ float s_lim[NA * LF][COLS];
+  __shared__ float s_keep[keep_floats<NA, NF>()][COLS];
+  __shared__ float s_ext[NF == 1 ? XS_EXT : 1][COLS];  // y sweep: contact list, extra-contact slots
+  const RowLds L{&s_rows[0][0], &s_lim[0][0], NF == 1 ? &s_keep[0][0] : nullptr, &s_ext[0][0], (int)threadIdx.x,
+                 (int)threadIdx.x / lpe<NF>(), COLS};
   const ContactRows<NA, NF> cr{scratch + e, n};
   const float ncon_prev = st.ncon ? st.ncon[e] : 0.f;  // issued early: consumed at the end
   const int st0 = S.status;
