@@ -254,13 +254,15 @@ def main():
         tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(tpath):
             traffic = json.load(open(tpath)).get(name, {}).get(kind)
-        # one lane per env, 64-lane waves: the kernel can occupy at most ceil(n/64) of the
+        # 64-lane waves, one lane per env (four per env in k_substep when the scene has a free
+        # body: quad mode, soarm_pgs.h lpe()): the kernel can occupy at most that many of the
         # chip's 1024 SIMDs; the VALU peak those SIMDs can issue bounds it first
-        waves = -(-n // 64)
+        lanes = 4 if kind == "substep" and cm.desc.nq - cm.desc.nv == 1 else 1
+        waves = -(-n * lanes // 64)
         capped = PEAK_FP32_TFLOPS * min(1.0, waves / 1024)
         roof = {"bound": "mfma", "achieved": achieved, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                 "frac": achieved / PEAK_FP32_TFLOPS, "traffic": traffic,
-                "waves_per_launch": waves, "occupancy_capped_peak": capped, "frac_of_capped": achieved / capped,
+                "lanes_per_env": lanes, "waves_per_launch": waves, "occupancy_capped_peak": capped, "frac_of_capped": achieved / capped,
                 "kernel": kind, "avg_launch_ms": avg_ms, "launches": cnt,
                 "flops_per_launch": per_launch,
                 "kernel_ms_per_step": {k: v[0] / kp for k, v in prof.items()},
