@@ -68,6 +68,23 @@ constexpr int LDS_CON = 6;  // contacts whose rows stay in LDS
 template <int NF>
 constexpr int lpe() { return NF == 1 ? SOARM_LPE : 1; }
 // value of lane J of each quad (DPP quad_perm broadcast); J is a compile-time 0..3
+// projected Gauss-Seidel step of a pyramid edge, max(x, -f): one VOP3 max with a
+// negated source.  fmaxf(x, -f) on a loop-carried f costs an extra canonicalising
+// v_max(-f, -f) per edge (IEEE mode: the compiler cannot prove -f canonical); every
+// operand here is a finite arithmetic result, so the plain instruction is exact.
+// Used only in loops without memory reads: an inline asm is not known to return, so
+// LICM keeps loads that follow it inside the loop.
+// packed FP32 (v_pk_fma_f32 / v_pk_add_f32): one wave per SIMD issues a VALU op every
+// ~4.7 cycles whether it is packed or not, so two independent FMAs on a register pair
+// cost one issue slot (tools/mb_chain.hip)
+typedef float f2 __attribute__((ext_vector_type(2)));
+DEVI f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+DEVI f2 splat2(float x) { return f2{x, x}; }
+DEVI float max_neg(float x, float f) {
+  float r;
+  asm("v_max_f32_e64 %0, %1, -%2" : "=v"(r) : "v"(x), "v"(f));
+  return r;
+}
 DEVI float qbcast(float x, int j) {
   const int b = __float_as_int(x);
   switch (j) {
@@ -958,6 +975,12 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   static_assert(XS_END <= NA * LF + XS_EXT - XS_LIST, "extra-slot scratch fits");
   auto EX = [&](int k) -> float& { return k < NA * LF ? L.lraw(k) : L.ex(XS_LIST + k - NA * LF); };
   float yE[3] = {0.f, 0.f, 0.f}, fE[4] = {0.f, 0.f, 0.f, 0.f}, fF[4] = {0.f, 0.f, 0.f, 0.f};
+  // quad mode: the E/F coefficients preloaded into registers before the sweeps, in the
+  // register pairs the packed loop consumes (no memory reads inside the sweep loop)
+  struct ExtQ {
+    float eW[18], eIA[4], fIA[4], muo, eA10, eA32, fA10, fA32, eMu, eRp, fMu, fRp, fJ2[6], fX2[3], eG2[3], xo[9], fSh2;
+    f2 eWp[9], eA2030, eA2131, fA2030, fA2131, eHD01, eHD23, fHD01, fHD23, fJp[6], fWp[9], fXp[3], eGp[3], xop[3], fSh01;
+  } xq;
   constexpr int NX = FC * (FC - 1) / 2;
   float yb[FC][3], xg[NX > 0 ? NX : 1][9];
   constexpr bool QUAD = lpe<NF>() == 4 && NF == 1 && CON && FC == 4;
@@ -965,6 +988,8 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   // quad mode: this lane's block contact (sub) — its y and its cross-Gram row X_sub,j
   // (j = sub: the contact's own 3x3 Gram block), full 3x3 per j
   float yo[3] = {0.f, 0.f, 0.f}, xr[QUAD ? FC : 1][9];
+  // rows of the arm block of M^-1 as dof pairs (packed v_arm updates of the friction rows)
+  f2 Mp[NA][NA / 2];
   auto ypair = [](int j, int k) { return j * FC - j * (j + 1) / 2 + (k - j - 1); };  // j < k
   auto yblock_setup = [&]() {
     if constexpr (NF == 1 && CON) {
@@ -1037,7 +1062,11 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   // per-sweep constants of the block in registers: 1/ARdiag, ARdiag/2, mu, R, the
   // off-diagonal edge-Gram entries A_ed = J_e M^-1 J_d' (d < e) and the 3x3 Gram block
   float yia[FC][4], yhd[FC][4], ymu[FC], yRp[FC], yA[FC][6], yG[FC][6];
-  auto yblock_consts = [&]() {
+  // quad mode, packed: (mu, -mu), edge-Gram pairs (A20, A30), (A21, A31), ARdiag/2 pairs, and
+  // the own row's update folded per edge, K_e = X_sub,j (1, s_e on t(e)): y_own += K_e df_e
+  f2 qmu2[FC], qA2030[FC], qA2131[FC], qhd01[FC], qhd23[FC], K01[QUAD ? FC : 1][4];
+  float K2[QUAD ? FC : 1][4];
+  auto yblock_consts = [&](auto pk) {
     if constexpr (NF == 1 && CON) {
 #pragma unroll
       for (int k = 0; k < FC; k++) {
@@ -1065,6 +1094,17 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
 #pragma unroll
           for (int d = 0; d < ed; d++)
             yA[k][q++] = G[0] + sg(ed) * gt(ed) + sg(d) * gt(d) + sg(ed) * sg(d) * gtt(ed, d);
+        if constexpr (QUAD && decltype(pk)::value) {
+          qmu2[k] = f2{mu, -mu};
+          qA2030[k] = f2{yA[k][1], yA[k][3]}, qA2131[k] = f2{yA[k][2], yA[k][4]};
+          qhd01[k] = f2{yhd[k][0], yhd[k][1]}, qhd23[k] = f2{yhd[k][2], yhd[k][3]};
+#pragma unroll
+          for (int ed = 0; ed < 4; ed++) {
+            const int t = 1 + (ed >> 1);
+            K01[k][ed] = f2{fmaf(sg(ed), xr[k][t], xr[k][0]), fmaf(sg(ed), xr[k][3 + t], xr[k][3])};
+            K2[k][ed] = fmaf(sg(ed), xr[k][6 + t], xr[k][6]);
+          }
+        }
       }
     }
   };
@@ -1072,10 +1112,39 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   // edge Gram matrix: every residual starts from the contact's y, and each force step
   // adds A_ed df_d to the later edges' residuals, so the dependent chain per edge is
   // mul -> max -> fma (df = max(-res/ARdiag, -f) is the projected step f' - f).
-  auto yblock_rows = [&](float& improvement, auto coupled) {
-    if constexpr (NF == 1 && CON) {
+  auto yblock_contact = [&](const int j, float& improvement, f2& impq, float (&dsel)[4], auto coupled, auto pk) {
+    if constexpr (QUAD && decltype(pk)::value) {  // packed form; contact j's y lives in lane j of the quad
+      const float a = qbcast(yo[0], j), b = qbcast(yo[1], j), cc = qbcast(yo[2], j);
+      const f2 c01 = f2{cfo[j][0], cfo[j][1]}, c23 = f2{cfo[j][2], cfo[j][3]};
+      f2 r01 = fma2(splat2(yRp[j]), c01, fma2(qmu2[j], splat2(b), splat2(a)));
+      f2 r23 = fma2(splat2(yRp[j]), c23, fma2(qmu2[j], splat2(cc), splat2(a)));
+      const float df0 = max_neg(r01.x * -yia[j][0], c01.x);
+      const float r1 = fmaf(yA[j][0], df0, r01.y);
+      r23 = fma2(qA2030[j], splat2(df0), r23);
+      const float df1 = max_neg(r1 * -yia[j][1], c01.y);
+      r23 = fma2(qA2131[j], splat2(df1), r23);
+      const float df2 = max_neg(r23.x * -yia[j][2], c23.x);
+      const float r3 = fmaf(yA[j][5], df2, r23.y);
+      const float df3 = max_neg(r3 * -yia[j][3], c23.y);
+      const f2 d01 = f2{df0, df1}, d23 = f2{df2, df3};
+      const f2 n01 = c01 + d01, n23 = c23 + d23;
+      cfo[j][0] = n01.x, cfo[j][1] = n01.y, cfo[j][2] = n23.x, cfo[j][3] = n23.y;
+      impq = fma2(-d01, fma2(qhd01[j], d01, f2{r01.x, r1}), impq);
+      impq = fma2(-d23, fma2(qhd23[j], d23, f2{r23.x, r3}), impq);
+      f2 y01 = f2{yo[0], yo[1]};
+      const float dfs[4] = {df0, df1, df2, df3};
 #pragma unroll
-      for (int j = 0; j < FC; j++) {
+      for (int ed = 0; ed < 4; ed++) {
+        y01 = fma2(K01[j][ed], splat2(dfs[ed]), y01);
+        yo[2] = fmaf(K2[j][ed], dfs[ed], yo[2]);
+      }
+      yo[0] = y01.x, yo[1] = y01.y;
+      if constexpr (decltype(coupled)::value) {  // y_E moves by X_jE D_j: lane j keeps its own
+#pragma unroll                                   // contact's steps, the quad sums them before E
+        for (int ed = 0; ed < 4; ed++) dsel[ed] = sub == j ? dfs[ed] : dsel[ed];
+      }
+    } else if constexpr (NF == 1 && CON) {
+      {
         float a, b, cc;
         if constexpr (QUAD) {  // contact j's y lives in lane j of the quad
           a = qbcast(yo[0], j), b = qbcast(yo[1], j), cc = qbcast(yo[2], j);
@@ -1138,19 +1207,28 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   };
   // dof-frictionloss rows of the y variants, short-chain form: df = clamp(-res/ARdiag,
   // -fl - f, fl - f) (the projected step), v_arm += M^-1 e_i df
-  auto fric_rows_y = [&](float& improvement, auto ext) {
-#pragma unroll
-    for (int i = 0; i < NA; i++) {
+  auto fric_row_y = [&](const int i, float& improvement, auto ext, auto pk) {
+    {
       const float fl = m.dof_frictionloss[i];
       const float res = fmaf(fR[i], ff[i], v[i] - fa[i]);
-      const float df = fminf(fmaxf(res * -fiD[i], -fl - ff[i]), fl - ff[i]);
+      const float fn = fminf(fmaxf(fmaf(res, -fiD[i], ff[i]), -fl), fl);
+      const float df = fn - ff[i];
+      if constexpr (decltype(pk)::value) {
 #pragma unroll
-      for (int k = 0; k < NA; k++) v[k] = fmaf(Mi.a(i, k), df, v[k]);
+        for (int k = 0; k + 1 < NA; k += 2) {  // v_arm += M^-1 e_i df, two dofs per packed FMA
+          const f2 t = fma2(Mp[i][k >> 1], splat2(df), f2{v[k], v[k + 1]});
+          v[k] = t.x, v[k + 1] = t.y;
+        }
+        if constexpr (NA & 1) v[NA - 1] = fmaf(Mi.a(i, NA - 1), df, v[NA - 1]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < NA; k++) v[k] = fmaf(Mi.a(i, k), df, v[k]);
+      }
       if constexpr (decltype(ext)::value) {  // the extra contact's y: J_E M^-1 e_i = W_E[i]
 #pragma unroll
-        for (int q = 0; q < 3; q++) yE[q] = fmaf(EX(E_W + 6 * q + i), df, yE[q]);
+        for (int q = 0; q < 3; q++) yE[q] = fmaf(decltype(pk)::value ? xq.eW[6 * q + i] : EX(E_W + 6 * q + i), df, yE[q]);
       }
-      ff[i] += df;
+      ff[i] = fn;
       improvement = fmaf(-df, fmaf(fhD[i], df, res), improvement);
     }
   };
@@ -1328,6 +1406,116 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
         yE[qq] = fmaf(EX(F_XE + 3 * qq), D[0], fmaf(EX(F_XE + 3 * qq + 1), D[1], fmaf(EX(F_XE + 3 * qq + 2), D[2], yE[qq])));
     }
   };
+  // quad mode, packed: the block's accumulated steps on y_E (lane-split X_kE D_k)
+  auto yblock_to_e = [&](const float (&dsel)[4]) {
+    const float mu = xq.muo;
+    const float D[3] = {(dsel[0] + dsel[1]) + (dsel[2] + dsel[3]), mu * (dsel[0] - dsel[1]), mu * (dsel[2] - dsel[3])};
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+      float p = 0.f;
+#pragma unroll
+      for (int rr = 0; rr < 3; rr++) p = fmaf(xq.xo[3 * rr + q], D[rr], p);
+      yE[q] += qsum(p);
+    }
+  };
+  // quad mode, packed: one edge chain (pyramid of 4 edges) from y = (a, b, c)
+  auto qchain = [&](float a, float b, float c, float (&f)[4], float mu, float Rp, const float (&ia)[4], float A10,
+                    f2 A2030, f2 A2131, float A32, f2 hd01, f2 hd23, f2& imp, float (&df)[4]) {
+    const f2 c01 = f2{f[0], f[1]}, c23 = f2{f[2], f[3]};
+    f2 r01 = fma2(splat2(Rp), c01, fma2(f2{mu, -mu}, splat2(b), splat2(a)));
+    f2 r23 = fma2(splat2(Rp), c23, fma2(f2{mu, -mu}, splat2(c), splat2(a)));
+    df[0] = max_neg(r01.x * -ia[0], c01.x);
+    const float r1 = fmaf(A10, df[0], r01.y);
+    r23 = fma2(A2030, splat2(df[0]), r23);
+    df[1] = max_neg(r1 * -ia[1], c01.y);
+    r23 = fma2(A2131, splat2(df[1]), r23);
+    df[2] = max_neg(r23.x * -ia[2], c23.x);
+    const float r3 = fmaf(A32, df[2], r23.y);
+    df[3] = max_neg(r3 * -ia[3], c23.y);
+    const f2 d01 = f2{df[0], df[1]}, d23 = f2{df[2], df[3]};
+    const f2 n01 = c01 + d01, n23 = c23 + d23;
+    f[0] = n01.x, f[1] = n01.y, f[2] = n23.x, f[3] = n23.y;
+    imp = fma2(-d01, fma2(hd01, d01, f2{r01.x, r1}), imp);
+    imp = fma2(-d23, fma2(hd23, d23, f2{r23.x, r3}), imp);
+  };
+  // v_arm += W D with W as dof pairs (W[q] row pairs)
+  auto qvarm = [&](const f2 (&Wp)[9], const float (&D)[3]) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      f2 t = f2{v[2 * k], v[2 * k + 1]};
+#pragma unroll
+      for (int q = 0; q < 3; q++) t = fma2(Wp[3 * q + k], splat2(D[q]), t);
+      v[2 * k] = t.x, v[2 * k + 1] = t.y;
+    }
+  };
+  auto yf_row_q = [&](f2& imp) {
+    f2 y01 = xq.fSh01;
+    float y2 = xq.fSh2;
+#pragma unroll
+    for (int i = 0; i < NA; i++) y01 = fma2(xq.fJp[i], splat2(v[i]), y01), y2 = fmaf(xq.fJ2[i], v[i], y2);
+    float df[4];
+    qchain(y01.x, y01.y, y2, fF, xq.fMu, xq.fRp, xq.fIA, xq.fA10, xq.fA2030, xq.fA2131, xq.fA32, xq.fHD01, xq.fHD23,
+           imp, df);
+    const float mu = xq.fMu;
+    const float D[3] = {(df[0] + df[1]) + (df[2] + df[3]), mu * (df[0] - df[1]), mu * (df[2] - df[3])};
+    qvarm(xq.fWp, D);
+    f2 e01 = f2{yE[0], yE[1]};
+#pragma unroll
+    for (int rr = 0; rr < 3; rr++) e01 = fma2(xq.fXp[rr], splat2(D[rr]), e01), yE[2] = fmaf(xq.fX2[rr], D[rr], yE[2]);
+    yE[0] = e01.x, yE[1] = e01.y;
+  };
+  auto yext_row_q = [&](f2& imp, auto coupled) {
+    float df[4];
+    qchain(yE[0], yE[1], yE[2], fE, xq.eMu, xq.eRp, xq.eIA, xq.eA10, xq.eA2030, xq.eA2131, xq.eA32, xq.eHD01, xq.eHD23,
+           imp, df);
+    const float mu = xq.eMu;
+    const float D[3] = {(df[0] + df[1]) + (df[2] + df[3]), mu * (df[0] - df[1]), mu * (df[2] - df[3])};
+    qvarm(xq.eWp, D);
+    if constexpr (decltype(coupled)::value) {  // this lane's block contact moves by X_own,E D
+      f2 o01 = f2{yo[0], yo[1]};
+#pragma unroll
+      for (int qq = 0; qq < 3; qq++) o01 = fma2(xq.xop[qq], splat2(D[qq]), o01), yo[2] = fmaf(xq.xo[6 + qq], D[qq], yo[2]);
+      yo[0] = o01.x, yo[1] = o01.y;
+    }
+    f2 e01 = f2{yE[0], yE[1]};
+    float e2 = yE[2];
+#pragma unroll
+    for (int qq = 0; qq < 3; qq++) e01 = fma2(xq.eGp[qq], splat2(D[qq]), e01), e2 = fmaf(xq.eG2[qq], D[qq], e2);
+    yE[0] = e01.x, yE[1] = e01.y, yE[2] = e2;
+  };
+  // quad mode: preload the E/F coefficients (after yext_setup wrote them to LDS)
+  auto yext_preload = [&]() {
+#pragma unroll
+    for (int k = 0; k < 18; k++) xq.eW[k] = EX(E_W + k);
+#pragma unroll
+    for (int q = 0; q < 3; q++)
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        xq.eWp[3 * q + k] = f2{EX(E_W + 6 * q + 2 * k), EX(E_W + 6 * q + 2 * k + 1)};
+        xq.fWp[3 * q + k] = f2{EX(F_W + 6 * q + 2 * k), EX(F_W + 6 * q + 2 * k + 1)};
+      }
+#pragma unroll
+    for (int ed = 0; ed < 4; ed++) xq.eIA[ed] = EX(E_IA + ed), xq.fIA[ed] = EX(F_IA + ed);
+    xq.eA10 = EX(E_A + 0), xq.eA2030 = f2{EX(E_A + 1), EX(E_A + 3)}, xq.eA2131 = f2{EX(E_A + 2), EX(E_A + 4)};
+    xq.eA32 = EX(E_A + 5);
+    xq.fA10 = EX(F_A + 0), xq.fA2030 = f2{EX(F_A + 1), EX(F_A + 3)}, xq.fA2131 = f2{EX(F_A + 2), EX(F_A + 4)};
+    xq.fA32 = EX(F_A + 5);
+    xq.eHD01 = f2{EX(E_HD + 0), EX(E_HD + 1)}, xq.eHD23 = f2{EX(E_HD + 2), EX(E_HD + 3)};
+    xq.fHD01 = f2{EX(F_HD + 0), EX(F_HD + 1)}, xq.fHD23 = f2{EX(F_HD + 2), EX(F_HD + 3)};
+    xq.eMu = EX(E_MU), xq.eRp = EX(E_RP), xq.fMu = EX(F_MUX), xq.fRp = EX(F_RPX);
+#pragma unroll
+    for (int i = 0; i < NA; i++) xq.fJp[i] = f2{EX(F_J + i), EX(F_J + 6 + i)}, xq.fJ2[i] = EX(F_J + 12 + i);
+#pragma unroll
+    for (int rr = 0; rr < 3; rr++) xq.fXp[rr] = f2{EX(F_XE + rr), EX(F_XE + 3 + rr)}, xq.fX2[rr] = EX(F_XE + 6 + rr);
+    xq.eGp[0] = f2{EX(E_G + 0), EX(E_G + 1)}, xq.eGp[1] = f2{EX(E_G + 1), EX(E_G + 3)}, xq.eGp[2] = f2{EX(E_G + 2), EX(E_G + 4)};
+    xq.eG2[0] = EX(E_G + 2), xq.eG2[1] = EX(E_G + 4), xq.eG2[2] = EX(E_G + 5);
+#pragma unroll
+    for (int t = 0; t < 9; t++) xq.xo[t] = EX(E_X + 9 * sub + t);
+    xq.muo = sub == 0 ? ymu[0] : sub == 1 ? ymu[1] : sub == 2 ? ymu[2] : ymu[3];
+#pragma unroll
+    for (int qq = 0; qq < 3; qq++) xq.xop[qq] = f2{xq.xo[qq], xq.xo[3 + qq]};
+    xq.fSh01 = f2{-EX(F_SH + 0), -EX(F_SH + 1)}, xq.fSh2 = -EX(F_SH + 2);
+  };
   // one sweep step of the extra contact (after the friction rows and the block)
   auto yext_row = [&](float& improvement, auto coupled) {
     if constexpr (NF == 1 && CON) {
@@ -1410,14 +1598,47 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   const bool hasE = npost >= 1, hasF = npost == 2;
   auto ysweeps = [&](auto ext, auto coupled, auto ext2) {
     yblock_setup();
-    yblock_consts();
-    if constexpr (decltype(ext)::value) yext_setup(cE, cF);
+    using PK = std::integral_constant<bool, QUAD>;
+    yblock_consts(PK{});
+    if constexpr (PK::value) {
+#pragma unroll
+      for (int i = 0; i < NA; i++)
+#pragma unroll
+        for (int k = 0; k + 1 < NA; k += 2) Mp[i][k >> 1] = f2{Mi.a(i, k), Mi.a(i, k + 1)};
+    }
+    if constexpr (decltype(ext)::value) {
+      yext_setup(cE, cF);
+      if constexpr (PK::value) yext_preload();
+    }
     for (int it = 0; it < m.iterations; it++) {
-      float improvement = 0.f;
-      fric_rows_y(improvement, ext);  // arm chain and cube block: independent, one straight-line region
-      yblock_rows(improvement, coupled);
-      if constexpr (decltype(ext2)::value) yf_row(improvement);
-      if constexpr (decltype(ext)::value) yext_row(improvement, coupled);
+      // the arm's frictionloss rows and the cube block touch disjoint dofs (M is block
+      // diagonal): the two Gauss-Seidel chains commute, so their rows are interleaved in
+      // program order to give the (latency-bound) issue stream independent work; the
+      // improvement terms go to one accumulator per chain
+      float improvement = 0.f, imp_b = 0.f;
+      f2 impq = f2{0.f, 0.f};
+      float dsel[4] = {0.f, 0.f, 0.f, 0.f};
+      // (NA = 6, FC = 4: rows {0,1} c0 {2} c1 {3,4} c2 {5} c3)
+#pragma unroll
+      for (int j = 0; j < FC; j++) {
+#pragma unroll
+        for (int i = (j * NA + FC - 1) / FC; i < ((j + 1) * NA + FC - 1) / FC; i++) fric_row_y(i, improvement, ext, PK{});
+        yblock_contact(j, imp_b, impq, dsel, coupled, PK{});
+      }
+      if constexpr (FC == 0) {
+#pragma unroll
+        for (int i = 0; i < NA; i++) fric_row_y(i, improvement, ext, PK{});
+      }
+      if constexpr (PK::value) {
+        if constexpr (decltype(ext)::value && decltype(coupled)::value) yblock_to_e(dsel);
+        if constexpr (decltype(ext2)::value) yf_row_q(impq);
+        if constexpr (decltype(ext)::value) yext_row_q(impq, coupled);
+        improvement += impq.x + impq.y;
+      } else {
+        improvement += imp_b;
+        if constexpr (decltype(ext2)::value) yf_row(improvement);
+        if constexpr (decltype(ext)::value) yext_row(improvement, coupled);
+      }
       if (improvement * scale < m.tolerance) {
 #ifdef SOARM_PHASE_PROF
         nsweep = it + 1;
