@@ -50,9 +50,9 @@ struct GeomPose {
 // geom world poses in global memory, SoA [geom*12 + k][env]
 DEVI void load_pose(const float* __restrict__ gpose, int n, int e, int g, GeomPose& o) {
 #pragma unroll
-  for (int k = 0; k < 3; k++) o.p[k] = gpose[(size_t)(g * 12 + k) * n + e];
+  for (int k = 0; k < 3; k++) o.p[k] = soa(gpose, g * 12 + k, n, e);
 #pragma unroll
-  for (int k = 0; k < 9; k++) o.R[k] = gpose[(size_t)(g * 12 + 3 + k) * n + e];
+  for (int k = 0; k < 9; k++) o.R[k] = soa(gpose, g * 12 + 3 + k, n, e);
 }
 
 // contacts of one candidate pair (<= 4: box-box / plane-box corners; 1 otherwise)
@@ -635,9 +635,9 @@ DEVI void write_geom_poses(const Sim<NA, NF>& S, float* __restrict__ gpose, int 
     mv(w, bR, gp);
     mm(R, bR, m.geom_mat[g]);
 #pragma unroll
-    for (int c = 0; c < 3; c++) gpose[(size_t)(g * 12 + c) * n + e] = bp[c] + w[c];
+    for (int c = 0; c < 3; c++) soa(gpose, g * 12 + c, n, e) = bp[c] + w[c];
 #pragma unroll
-    for (int c = 0; c < 9; c++) gpose[(size_t)(g * 12 + 3 + c) * n + e] = R[c];
+    for (int c = 0; c < 9; c++) soa(gpose, g * 12 + 3 + c, n, e) = R[c];
   }
 }
 

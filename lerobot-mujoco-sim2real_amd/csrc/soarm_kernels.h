@@ -23,6 +23,23 @@
 
 #define DEVI __device__ __forceinline__
 
+// element e of row r of a [row][env] array (4-byte T): the row pointer is wave-uniform
+// (SGPRs) and the lane's byte offset e*4 a 32-bit VGPR shared by every row, so the access
+// is a saddr global load/store.  A 64-bit per-lane address for every (row, env) element
+// costs two VGPRs each, which the compiler keeps live across the kernel and spills.
+// an opaque copy of a (wave-uniform) pointer: addresses derived from it are not CSE'd with
+// those of an earlier access, so no per-lane address stays live between the two
+template <class T>
+DEVI T* launder(T* p) {
+  asm volatile("" : "+s"(p));
+  return p;
+}
+template <class T>
+DEVI T& soa(T* p, int r, int n, int e) {
+  static_assert(sizeof(T) == 4, "4-byte elements");
+  return *(T*)((const char*)(p + (size_t)r * n) + ((uint32_t)e << 2));
+}
+
 namespace soarm {
 
 constexpr float MINVALF = 1e-15f;

@@ -481,11 +481,11 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       // every lane (identical values in the env's slab)
       const int nw = (m.npair + 31) >> 5;
       for (int w = 0; w < nw; w++) {
-        uint32_t bits = pmask[(size_t)w * n + e];
+        uint32_t bits = soa(pmask, w, n, e);
         while (bits) {
           const int p = 32 * w + __builtin_ctz(bits);
           bits &= bits - 1;
-          const int cnt = ccount[(size_t)p * n + e];
+          const int cnt = soa(ccount, p, n, e);
           for (int k = 0; k < cnt; k++) {
             if (ncon >= SIM_MAXCON) {
               S.status |= SIM_ST_CONOVERFLOW;
@@ -502,7 +502,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
         const int s0 = m.pair_slot[p];
         float rw[7];
 #pragma unroll
-        for (int f = 0; f < 7; f++) rw[f] = cbuf[((size_t)(s0 + k) * 7 + f) * n + e];
+        for (int f = 0; f < 7; f++) rw[f] = soa(cbuf, (s0 + k) * 7 + f, n, e);
         float si[5];
 #pragma unroll
         for (int q = 0; q < 5; q++) si[q] = m.pair_solimp[p][q];
@@ -521,7 +521,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
     if (ccount != nullptr) {
       const int nw = (m.npair + 31) >> 5;
       for (int w = 0; w < nw; w++) {
-        uint32_t bits = pmask[(size_t)w * n + e];
+        uint32_t bits = soa(pmask, w, n, e);
         while (bits) {
           const int p = 32 * w + __builtin_ctz(bits);
           bits &= bits - 1;
@@ -529,7 +529,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
           // the pair's constants and every slot it may fill (cap <= PAIR_MAXCON; a set mask
           // bit means at least one contact, and slots past the count are never used)
           RP_MARK(3);
-          const int cnt = ccount[(size_t)p * n + e];
+          const int cnt = soa(ccount, p, n, e);
           const int s0 = m.pair_slot[p], cap = m.pair_cap[p];
           const int b1 = m.pair_body1[p], b2 = m.pair_body2[p];
           const float mu = S.fric >= 0.f ? S.fric : m.pair_friction[p];
@@ -542,7 +542,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
 #pragma unroll
           for (int k = 0; k < PAIR_MAXCON; k++)
 #pragma unroll
-            for (int f = 0; f < 7; f++) raw[k][f] = k < cap ? cbuf[((size_t)(s0 + k) * 7 + f) * n + e] : 0.f;
+            for (int f = 0; f < 7; f++) raw[k][f] = k < cap ? soa(cbuf, (s0 + k) * 7 + f, n, e) : 0.f;
 #pragma unroll
           for (int k = 0; k < PAIR_MAXCON; k++) {
             if (k >= cnt) break;
@@ -978,7 +978,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   // quad mode: the E/F coefficients preloaded into registers before the sweeps, in the
   // register pairs the packed loop consumes (no memory reads inside the sweep loop)
   struct ExtQ {
-    float eW[18], eIA[4], fIA[4], muo, eA10, eA32, fA10, fA32, eMu, eRp, fMu, fRp, fJ2[6], fX2[3], eG2[3], xo[9], fSh2;
+    float eIA[4], fIA[4], muo, eA10, eA32, fA10, fA32, eMu, eRp, fMu, fRp, fJ2[6], fX2[3], eG2[3], xo[9], fSh2;
     f2 eWp[9], eA2030, eA2131, fA2030, fA2131, eHD01, eHD23, fHD01, fHD23, fJp[6], fWp[9], fXp[3], eGp[3], xop[3], fSh01;
   } xq;
   constexpr int NX = FC * (FC - 1) / 2;
@@ -1226,7 +1226,10 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       }
       if constexpr (decltype(ext)::value) {  // the extra contact's y: J_E M^-1 e_i = W_E[i]
 #pragma unroll
-        for (int q = 0; q < 3; q++) yE[q] = fmaf(decltype(pk)::value ? xq.eW[6 * q + i] : EX(E_W + 6 * q + i), df, yE[q]);
+        for (int q = 0; q < 3; q++)
+          yE[q] = fmaf(decltype(pk)::value ? ((i & 1) ? xq.eWp[3 * q + (i >> 1)].y : xq.eWp[3 * q + (i >> 1)].x)
+                                           : EX(E_W + 6 * q + i),
+                       df, yE[q]);
       }
       ff[i] = fn;
       improvement = fmaf(-df, fmaf(fhD[i], df, res), improvement);
@@ -1485,8 +1488,6 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   };
   // quad mode: preload the E/F coefficients (after yext_setup wrote them to LDS)
   auto yext_preload = [&]() {
-#pragma unroll
-    for (int k = 0; k < 18; k++) xq.eW[k] = EX(E_W + k);
 #pragma unroll
     for (int q = 0; q < 3; q++)
 #pragma unroll

@@ -115,29 +115,29 @@ template <int NA, int NF>
 DEVI void load_state(Sim<NA, NF>& S, const sim_state& st, int n, int e) {
   constexpr int NQ = Sim<NA, NF>::NQ, NV = Sim<NA, NF>::NV;
 #pragma unroll
-  for (int i = 0; i < NQ; i++) S.qpos[i] = st.qpos[(size_t)i * n + e];
+  for (int i = 0; i < NQ; i++) S.qpos[i] = soa(launder(st.qpos), i, n, e);
 #pragma unroll
   for (int i = 0; i < NV; i++) {
-    S.qvel[i] = st.qvel[(size_t)i * n + e];
-    S.warm[i] = st.qacc_warmstart[(size_t)i * n + e];
+    S.qvel[i] = soa(launder(st.qvel), i, n, e);
+    S.warm[i] = soa(launder(st.qacc_warmstart), i, n, e);
   }
 #pragma unroll
-  for (int i = 0; i < NA; i++) S.ctrl[i] = (i < S.mp->nu) ? st.ctrl[(size_t)i * n + e] : 0.f;
+  for (int i = 0; i < NA; i++) S.ctrl[i] = (i < S.mp->nu) ? soa(launder(st.ctrl), i, n, e) : 0.f;
   S.status = st.status[e];
 }
 template <int NA, int NF>
 DEVI void store_state(const Sim<NA, NF>& S, const sim_state& st, int n, int e) {
   constexpr int NQ = Sim<NA, NF>::NQ, NV = Sim<NA, NF>::NV;
 #pragma unroll
-  for (int i = 0; i < NQ; i++) st.qpos[(size_t)i * n + e] = S.qpos[i];
+  for (int i = 0; i < NQ; i++) soa(launder(st.qpos), i, n, e) = S.qpos[i];
 #pragma unroll
   for (int i = 0; i < NV; i++) {
-    st.qvel[(size_t)i * n + e] = S.qvel[i];
-    st.qacc_warmstart[(size_t)i * n + e] = S.warm[i];
+    soa(launder(st.qvel), i, n, e) = S.qvel[i];
+    soa(launder(st.qacc_warmstart), i, n, e) = S.warm[i];
   }
 #pragma unroll
   for (int i = 0; i < NA; i++)
-    if (i < S.mp->nu) st.ctrl[(size_t)i * n + e] = S.ctrl[i];
+    if (i < S.mp->nu) soa(launder(st.ctrl), i, n, e) = S.ctrl[i];
   st.status[e] = S.status;
 }
 template <int NA, int NF>
@@ -248,14 +248,14 @@ __global__ __launch_bounds__(256) void k_collide(const DModel* __restrict__ dm, 
   load_pose(gpose, n, e, m.pair_geom2[p], P2);
   PairOut o;
   collide_pair(m, p, P1, P2, o);
-  ccount[(size_t)p * n + e] = o.n;
+  soa(ccount, p, n, e) = o.n;
   if (o.n > 0) atomicOr(&pmask[(size_t)(p >> 5) * n + e], 1u << (p & 31));
   const int s0 = m.pair_slot[p];
 #pragma unroll
   for (int k = 0; k < PAIR_MAXCON; k++)
     if (k < o.n)
 #pragma unroll
-      for (int f = 0; f < 7; f++) cbuf[((size_t)(s0 + k) * 7 + f) * n + e] = o.c[k][f];
+      for (int f = 0; f < 7; f++) soa(cbuf, (s0 + k) * 7 + f, n, e) = o.c[k][f];
   if (pcyc && (threadIdx.x & 63) == 0) atomicAdd(&pcyc[p], (unsigned long long)(clock64() - t0));
 }
 
@@ -351,12 +351,12 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
     const float* qv = st.qvel;
     asm volatile("" : "+s"(qp), "+s"(qv));
 #pragma unroll
-    for (int i = 0; i < Sim<NA, NF>::NQ; i++) S.qpos[i] = qp[(size_t)i * n + e];
+    for (int i = 0; i < Sim<NA, NF>::NQ; i++) S.qpos[i] = soa(qp, i, n, e);
 #pragma unroll
-    for (int i = 0; i < Sim<NA, NF>::NV; i++) S.qvel[i] = qv[(size_t)i * n + e];
+    for (int i = 0; i < Sim<NA, NF>::NV; i++) S.qvel[i] = soa(qv, i, n, e);
   }
   if (pmask)  // consumed: clear for the next collide
-    for (int w = 0; w < (m.npair + 31) >> 5; w++) pmask[(size_t)w * n + e] = 0u;
+    for (int w = 0; w < (m.npair + 31) >> 5; w++) soa(pmask, w, n, e) = 0u;
   const float ee[3] = {S.ee[0], S.ee[1], S.ee[2]};
   PSTAMP(11);
   S.integrate();
@@ -433,7 +433,7 @@ __global__ __launch_bounds__(64) void k_gather(const DModel* __restrict__ dm, in
                                                float* __restrict__ out, int* __restrict__ nout) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
-  for (int w = 0; w < (dm->npair + 31) >> 5; w++) pmask[(size_t)w * n + e] = 0u;
+  for (int w = 0; w < (dm->npair + 31) >> 5; w++) soa(pmask, w, n, e) = 0u;
   __shared__ float s_con[SIM_MAXCON * 8][64];
   const ConLds C{s_con, (int)threadIdx.x};
   int status = 0;
