@@ -71,9 +71,10 @@ struct DModel {
   int geom_lutadr[MAXG];     // first LUT entry of each mesh geom (-1: not a mesh)
   // hill-climbing records, 32 B per vertex (two uint4): [0] x, y, z (float bits), degree |
   // overflow offset << 8; [1] the first 8 neighbour ids (local, uint16, padded with the
-  // vertex itself).  Neighbours past 8 live in hull_ovf.  hull_lutrec holds, per LUT cell,
-  // a copy of its start vertex's record, so a query opens with one load and each climbing
-  // step is one round trip (coordinates and neighbour ids of all candidates together).
+  // vertex itself).  Neighbours past 8 live in hull_ovf.  hull_lutrec holds, per LUT cell
+  // (HULL_LUTREC uint4), a copy of its start vertex's record and the coordinates of its
+  // first 8 neighbours, so a query whose start cell already holds the maximum (the usual
+  // case) finishes in one round trip; each further climbing step is one more.
   const uint4* hull_rec;
   const uint4* hull_lutrec;
   const uint16_t* hull_ovf;
@@ -84,6 +85,9 @@ struct DModel {
 // direction.  Hill climbing starts there, so a query walks ~1 edge (the
 // final step only verifies the local maximum).
 constexpr int HULL_LUT_K = 16;
+// uint4 per LUT cell in hull_lutrec: the start vertex's two record words, then its first 8
+// neighbours as (x, y, z, local id) -- the first climbing step needs no second round trip
+constexpr int HULL_LUTREC = 10;
 constexpr int HULL_LUT_CELLS = 6 * HULL_LUT_K * HULL_LUT_K;
 
 // cube-map cell of a (not necessarily unit) direction; same mapping on host and device

@@ -69,13 +69,30 @@ struct PairOut {
 // dependent round trip.  Same comparisons, order and result as a CSR walk.
 DEVI float3 hull_support(const DModel& m, int g, const float l[3]) {
   const uint4* rec = m.hull_rec + 2 * m.geom_hulladr[g];
-  const uint4* lr = m.hull_lutrec + 2 * (m.geom_lutadr[g] + lut_cell(l[0], l[1], l[2]));
-  uint4 r0 = lr[0], r1 = lr[1];
+  const uint4* lr = m.hull_lutrec + HULL_LUTREC * (m.geom_lutadr[g] + lut_cell(l[0], l[1], l[2]));
+  uint4 r0 = lr[0], r1 = lr[1], nb[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) nb[k] = lr[2 + k];
   const int nvert = m.geom_hullnum[g];
   auto dotr = [&](const uint4& r) {
     return l[0] * __uint_as_float(r.x) + l[1] * __uint_as_float(r.y) + l[2] * __uint_as_float(r.z);
   };
   float cd = dotr(r0);
+  if ((r0.w & 255u) <= 8) {  // first step from the cell's copy of the start's neighbours
+    float nd = cd;
+    int best = -1;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const float s = dotr(nb[k]);
+      if (s > nd) nd = s, best = k;
+    }
+    if (best < 0) return make_float3(__uint_as_float(r0.x), __uint_as_float(r0.y), __uint_as_float(r0.z));
+    uint32_t u = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      if (k == best) u = nb[k].w;
+    r0 = rec[2 * u], r1 = rec[2 * u + 1], cd = nd;
+  }
   for (int guard = 0; guard < nvert; guard++) {
     const uint32_t ids[4] = {r1.x, r1.y, r1.z, r1.w};
     uint4 c0[8], c1[8];

@@ -877,14 +877,23 @@ int sim_model_create(const sim_model_desc* desc, const float* hull_vert, const i
       M->hull_rec[2 * i + 1] = make_uint4(id[0] | id[1] << 16, id[2] | id[3] << 16, id[4] | id[5] << 16, id[6] | id[7] << 16);
     }
   }
-  M->hull_lutrec.assign((size_t)2 * M->hull_lut.size(), make_uint4(0, 0, 0, 0));
+  M->hull_lutrec.assign((size_t)HULL_LUTREC * M->hull_lut.size(), make_uint4(0, 0, 0, 0));
   for (int g = 0; g < desc->ngeom; g++) {
     if (M->lutadr[g] < 0) continue;
+    const size_t base = (size_t)desc->geom_hulladr[g];
     for (int c = 0; c < HULL_LUT_CELLS; c++) {
       const size_t cell = (size_t)M->lutadr[g] + c;
-      const size_t v = (size_t)desc->geom_hulladr[g] + M->hull_lut[cell];
-      M->hull_lutrec[2 * cell] = M->hull_rec[2 * v];
-      M->hull_lutrec[2 * cell + 1] = M->hull_rec[2 * v + 1];
+      const size_t v = base + M->hull_lut[cell];
+      uint4* out = &M->hull_lutrec[HULL_LUTREC * cell];
+      out[0] = M->hull_rec[2 * v];
+      out[1] = M->hull_rec[2 * v + 1];
+      const uint4 ids = out[1];
+      const uint32_t w[4] = {ids.x, ids.y, ids.z, ids.w};
+      for (int k = 0; k < 8; k++) {  // neighbour k in record order (padding = the vertex itself)
+        const uint32_t u = (w[k >> 1] >> (16 * (k & 1))) & 0xffffu;
+        const uint4 r = M->hull_rec[2 * (base + u)];
+        out[2 + k] = make_uint4(r.x, r.y, r.z, u);
+      }
     }
   }
   *out = M;
