@@ -631,30 +631,35 @@ DEVI void box_box(const DModel& m, int g1, int g2, const GeomPose& P1, const Geo
 
 // world poses of every collidable geom of this env -> global SoA [geom*12+k][env]
 template <int NA, int NF>
-// geoms g0, g0 + gstep, ... (quad mode: lane k of the quad writes every 4th geom)
+// geoms g0, g0 + gstep, ... of each body (quad mode: lane k of the quad writes every 4th)
 DEVI void write_geom_poses(const Sim<NA, NF>& S, float* __restrict__ gpose, int n, int e, int g0 = 0,
                            int gstep = 1) {
+  // bodies in compile-time order, each body's geoms from a wave-uniform list: the body frame
+  // is read with constant indices (a per-lane body id would select it with 12 v_cndmask per
+  // body); g0/gstep split a body's geoms over the lanes of an env
   const DModel& m = *S.mp;
   constexpr int NB = Sim<NA, NF>::NB;
-  for (int g = g0; g < m.ngeom; g += gstep) {
-    const int b = m.geom_bodyid[g];  // wave-uniform unless gstep > 1
+#pragma unroll
+  for (int b = 0; b < NB; b++) {
     float bp[3] = {0, 0, 0}, bR[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    if (b > 0) {
 #pragma unroll
-    for (int k = 1; k < NB; k++)
-      if (k == b) {
+      for (int c = 0; c < 3; c++) bp[c] = S.xpos[b][c];
 #pragma unroll
-        for (int c = 0; c < 3; c++) bp[c] = S.xpos[k][c];
+      for (int c = 0; c < 9; c++) bR[c] = S.xmat[b][c];
+    }
+    const int adr = m.body_gadr[b], num = m.body_gnum[b];
+    for (int t = g0; t < num; t += gstep) {
+      const int g = m.geom_bybody[adr + t];
+      const float gp[3] = {m.geom_pos[g][0], m.geom_pos[g][1], m.geom_pos[g][2]};
+      float w[3], R[9];
+      mv(w, bR, gp);
+      mm(R, bR, m.geom_mat[g]);
 #pragma unroll
-        for (int c = 0; c < 9; c++) bR[c] = S.xmat[k][c];
-      }
-    const float gp[3] = {m.geom_pos[g][0], m.geom_pos[g][1], m.geom_pos[g][2]};
-    float w[3], R[9];
-    mv(w, bR, gp);
-    mm(R, bR, m.geom_mat[g]);
+      for (int c = 0; c < 3; c++) soa(gpose, g * 12 + c, n, e) = bp[c] + w[c];
 #pragma unroll
-    for (int c = 0; c < 3; c++) soa(gpose, g * 12 + c, n, e) = bp[c] + w[c];
-#pragma unroll
-    for (int c = 0; c < 9; c++) soa(gpose, g * 12 + 3 + c, n, e) = R[c];
+      for (int c = 0; c < 9; c++) soa(gpose, g * 12 + 3 + c, n, e) = R[c];
+    }
   }
 }
 

@@ -728,6 +728,14 @@ static int validate_and_build(const sim_model_desc& d, sim_model* M) {
     host_KB(d.dof_solref[i], d.dof_solimp[i], d.timestep, KB);
     m.dof_fricB[i] = KB[1];
   }
+  {  // geoms grouped by body (write_geom_poses walks bodies with compile-time indices)
+    int k = 0;
+    for (int b = 0; b < SIM_MAXBODY; b++) {
+      m.body_gadr[b] = k, m.body_gnum[b] = 0;
+      for (int g = 0; g < d.ngeom; g++)
+        if (d.geom_bodyid[g] == b) m.geom_bybody[k++] = g, m.body_gnum[b]++;
+    }
+  }
   for (int g = 0; g < d.ngeom; g++) {
     m.geom_type[g] = d.geom_type[g], m.geom_bodyid[g] = d.geom_bodyid[g];
     m.geom_hulladr[g] = d.geom_hulladr[g], m.geom_hullnum[g] = d.geom_hullnum[g];
