@@ -84,9 +84,12 @@ struct DModel {
 
 // Support-point start table: a cube map of HULL_LUT_K x HULL_LUT_K cells per
 // face; each cell holds the hull's argmax vertex for the cell-centre
-// direction.  Hill climbing starts there, so a query walks ~1 edge (the
-// final step only verifies the local maximum).
-constexpr int HULL_LUT_K = 16;
+// direction.  Hill climbing starts there, so a query usually ends at the start
+// (verified from the neighbour coordinates the cell carries).  96 x 96: the
+// collide kernel is latency-bound on support round trips, and a finer map
+// (115 MB of cell records for the 13 arm hulls) lands the start on the answer
+// more often: collide 0.287 (16) -> 0.251 (48) -> 0.231 (96) ms per env-step.
+constexpr int HULL_LUT_K = 96;
 // uint4 per LUT cell in hull_lutrec: the start vertex's two record words, then its first 8
 // neighbours as (x, y, z, local id) -- the first climbing step needs no second round trip
 constexpr int HULL_LUTREC = 10;

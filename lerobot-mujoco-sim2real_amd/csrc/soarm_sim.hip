@@ -13,6 +13,7 @@
 #include <cstring>
 #include <string>
 #include <type_traits>
+#include <thread>
 #include <vector>
 
 #include "../../include/soarm_sim.h"
@@ -849,17 +850,27 @@ int sim_model_create(const sim_model_desc* desc, const float* hull_vert, const i
     }
     M->lutadr[g] = k * HULL_LUT_CELLS;
     const float* hv = hull_vert + 3 * (size_t)desc->geom_hulladr[g];
-    for (int c = 0; c < HULL_LUT_CELLS; c++) {
-      double d[3];
-      lut_dir(c, d);
-      int best = 0;
-      double bd = -1e300;
-      for (int i = 0; i < desc->geom_hullnum[g]; i++) {
-        const double s = d[0] * hv[3 * i] + d[1] * hv[3 * i + 1] + d[2] * hv[3 * i + 2];
-        if (s > bd) bd = s, best = i;
+    const int nv = desc->geom_hullnum[g];
+    uint16_t* out = &M->hull_lut[(size_t)k * HULL_LUT_CELLS];
+    // exact argmax per cell (brute force), cells split over host threads
+    auto cells = [hv, nv, out](int c0, int c1) {
+      for (int c = c0; c < c1; c++) {
+        double d[3];
+        lut_dir(c, d);
+        int best = 0;
+        double bd = -1e300;
+        for (int i = 0; i < nv; i++) {
+          const double s = d[0] * hv[3 * i] + d[1] * hv[3 * i + 1] + d[2] * hv[3 * i + 2];
+          if (s > bd) bd = s, best = i;
+        }
+        out[c] = (uint16_t)best;
       }
-      M->hull_lut[(size_t)k * HULL_LUT_CELLS + c] = (uint16_t)best;
-    }
+    };
+    const int nt = (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+    std::vector<std::thread> pool;
+    for (int t = 0; t < nt; t++)
+      pool.emplace_back(cells, (int)((long)HULL_LUT_CELLS * t / nt), (int)((long)HULL_LUT_CELLS * (t + 1) / nt));
+    for (auto& th : pool) th.join();
     k++;
   }
   // climbing records: coordinates, degree and the first 8 neighbours in 32 B per vertex
