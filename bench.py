@@ -221,6 +221,13 @@ def main():
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         dist.all_reduce(x, op=dist.ReduceOp.SUM)
         dt, ncon = float(mx[0]), float(x[1])
+    # validity of what was timed: states finite, soft resets (mj_checkPos/Vel/Acc status bits) counted
+    finite = bool(torch.isfinite(sim.obs).all() and torch.isfinite(sim.qpos).all() and torch.isfinite(sim.qvel).all())
+    nbad = int((sim.status != 0).sum().item())
+    if world > 1:
+        v = torch.tensor([0 if finite else 1, nbad], dtype=torch.float64, device=dev)
+        dist.all_reduce(v, op=dist.ReduceOp.SUM)
+        finite, nbad = v[0].item() == 0, int(v[1].item())
     total_envs = n * world
     value = total_envs * args.steps / dt
     contacts = ncon / (total_envs * args.steps * 10)
@@ -285,11 +292,17 @@ def main():
                        "contacts_per_env_substep": contacts, "solver": "PGS (iterations 100, tol 1e-8)",
                        "parallelism": f"env-sharded x{world} (no per-step collective)"},
             "roofline": roof, "cpu_baseline": cpu,
+            "validity": {"state_finite": finite, "envs_status_nonzero": nbad,
+                         "library": build.library_info()},
         }
         print(json.dumps(line), flush=True)
+        if not finite:
+            print("bench: non-finite simulation state after the timed region", file=sys.stderr)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    if not finite:
+        sys.exit(3)
 
 
 if __name__ == "__main__":

@@ -215,9 +215,12 @@ const char* sim_version(void);
    hull_vert [nhullvert][3], hull_adr [nhullvert+1] CSR, hull_adj [nhulladj] local ids */
 int sim_model_create(const sim_model_desc* desc, const float* hull_vert, const int32_t* hull_adr,
                      const int32_t* hull_adj, sim_model** out);
+/* frees the model and its device copies; every batch of the model must be freed first */
 void sim_model_free(sim_model* m);
 
-/* replaces MjData(model) for n_envs envs on `device` (HIP ordinal) */
+/* replaces MjData(model) for n_envs envs on `device` (HIP ordinal).  The model's
+   read-only device data (constants, hull records, support LUT) is uploaded by the
+   first batch on a device and shared by the model's later batches there. */
 int sim_batch_create(const sim_model* m, int n_envs, int device, sim_batch** out);
 void sim_batch_free(sim_batch* b);
 int sim_batch_set_params(sim_batch* b, const sim_params* p);

@@ -118,6 +118,22 @@ def cartesian_targets(kind, t_param, idx=1, scale=0.5):
     return lib.stack([x, y, z], -1)
 
 
+def stream_seed(seed, stream):
+    """32-bit seed of rollout stream `stream` under the user seed (splitmix64 finaliser).
+
+    The reference draws every dataset from ONE advancing ``np.random`` stream
+    (``SOARM101_DataCollection.py:97-132``), so train / val / test splits and
+    successive chunks are independent draws.  Here each rollout call takes the
+    next stream index and derives its reset key, action generator and sine
+    tables from ``stream_seed(seed, index)``: distinct calls never share initial
+    states or inputs, and a fixed (seed, call order) reproduces the dataset."""
+    m = (1 << 64) - 1
+    z = (int(seed) * 0x9E3779B97F4A7C15 + (int(stream) + 1) * 0xBF58476D1CE4E5B9) & m
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & m
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & m
+    return int((z ^ (z >> 31)) & 0xFFFFFFFF)
+
+
 class SOARM101DataGenerator:
     """Reference ``SOARM101DataGenerator`` (``:77-205``) with a batched GPU rollout."""
 
@@ -129,6 +145,13 @@ class SOARM101DataGenerator:
         self.model = model
         self.collate_fn = Collater(self.args.x_dim, self.args.u_dim, self.args.device)
         self._envs = {}
+        self._stream = 0  # advances per rollout call (one np.random stream in the reference)
+
+    def next_seed(self):
+        """Seed of the next rollout stream (see :func:`stream_seed`)."""
+        s = stream_seed(self.args.seed, self._stream)
+        self._stream += 1
+        return s
 
     def _env(self, n):
         if n not in self._envs:
@@ -142,16 +165,21 @@ class SOARM101DataGenerator:
                        sine=None, env_offset=0):
         """Rollout of `n` envs for `steps` env-steps; returns a device tensor [steps+1, n, 13] fp32.
 
-        actions: optional [steps+1, n, 5] (row i = u_i) to replay a fixed input sequence."""
+        actions: optional [steps+1, n, 5] (row i = u_i) to replay a fixed input sequence.
+        seed: key of the reset draw, action generator and sine tables; None takes the
+        generator's next stream (:meth:`next_seed`), so successive calls are independent."""
         import torch
 
         env = self._env(n)
         env._env_offset = env_offset
         dev = env.sim.device
+        if seed is None:
+            seed = self.next_seed()
         gen = torch.Generator(device=dev)
-        gen.manual_seed(self.args.seed if seed is None else seed)
+        gen.manual_seed(seed)
         if input_type in ("sin", "chirp") and actions is None:
-            sine = sine or SineInputGenerator(n, self.udim, (0.0025, 0.05), (-0.5, 0.5), mode=input_type)
+            sine = sine or SineInputGenerator(n, self.udim, (0.0025, 0.05), (-0.5, 0.5), mode=input_type,
+                                              rng=np.random.default_rng(seed))
             dsine = DeviceSine(sine, dev)
         ik = input_type.startswith("ik_") and actions is None
         if ik:

@@ -1,6 +1,15 @@
-"""Compile the HIP C-ABI library in-tree for gfx950 (no JIT caches)."""
+"""Compile the HIP C-ABI library in-tree for gfx950 (no JIT caches).
+
+Staleness is decided by content, not file times: the build writes
+``libsoarm_sim.so.srchash`` (sha256 of the sources, headers and flags it was
+built from) beside the library, so a tree copied to another box (where file
+times may not survive) still knows whether its library matches its sources,
+and a header edit is never benchmarked against a stale library.
+"""
+import hashlib
 import os
 import subprocess
+import time
 
 from .abi import LIB_PATH, PKG_DIR
 
@@ -12,43 +21,66 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # packing's operand shuffles (v_mov) and the extra register pressure (AGPR
 # round trips) cost ~13% of the PGS sweep's VALU issue (ISA count, k_substep).
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-fno-slp-vectorize"]
+STAMP = LIB_PATH + ".srchash"
+
+
+def source_hash():
+    """sha256 over the flags and every source/header the library is built from."""
+    h = hashlib.sha256(" ".join(FLAGS).encode())
+    deps = [os.path.join(SRC_DIR, f) for f in SOURCES + HEADERS]
+    deps.append(os.path.join(PKG_DIR, "..", "include", "soarm_sim.h"))
+    for d in deps:
+        h.update(os.path.basename(d).encode())
+        with open(d, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
+def built_hash():
+    try:
+        with open(STAMP) as f:
+            return f.read().strip()
+    except OSError:
+        return None
 
 
 def _stale():
-    if not os.path.exists(LIB_PATH):
-        return True
-    t = os.path.getmtime(LIB_PATH)
-    deps = [os.path.join(SRC_DIR, f) for f in SOURCES + HEADERS]
-    deps.append(os.path.join(PKG_DIR, "..", "include", "soarm_sim.h"))
-    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+    return not os.path.exists(LIB_PATH) or built_hash() != source_hash()
 
 
 def build(force=False, verbose=False):
-    """Build csrc/libsoarm_sim.so if missing or older than its sources."""
+    """Build csrc/libsoarm_sim.so if missing or built from other sources."""
     if not force and not _stale():
         return LIB_PATH
+    want = source_hash()
     tmp = f"{LIB_PATH}.{os.getpid()}.tmp"
     cmd = [HIPCC] + FLAGS + ["-o", tmp] + [os.path.join(SRC_DIR, s) for s in SOURCES]
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd, cwd=SRC_DIR)
     os.replace(tmp, LIB_PATH)  # atomic: concurrent loaders never see a partial file
+    with open(STAMP + f".{os.getpid()}.tmp", "w") as f:
+        f.write(want + "\n")
+    os.replace(STAMP + f".{os.getpid()}.tmp", STAMP)
     return LIB_PATH
 
 
-def ensure_built(local_rank=0, timeout_s=600):
-    """Multi-process entry (bench under torch.distributed.run): never rebuild a library
-    that exists (file times may not survive a copy to another box); if it is missing,
-    local rank 0 builds it and the other ranks wait for it."""
-    import time
-
-    if os.path.exists(LIB_PATH):
-        return LIB_PATH
+def ensure_built(local_rank=0, timeout_s=900):
+    """Multi-process entry (bench under torch.distributed.run): local rank 0 (re)builds the
+    library if it is missing or stale; the other ranks wait until the library on disk
+    matches the sources."""
     if local_rank == 0:
-        return build(force=True)
-    t0 = time.time()
-    while not os.path.exists(LIB_PATH):
+        return build()
+    want, t0 = source_hash(), time.time()
+    while not (os.path.exists(LIB_PATH) and built_hash() == want):
         if time.time() - t0 > timeout_s:
-            raise RuntimeError(f"{LIB_PATH} did not appear (built by local rank 0)")
+            raise RuntimeError(f"{LIB_PATH} was not (re)built by local rank 0 within {timeout_s} s")
         time.sleep(1.0)
     return LIB_PATH
+
+
+def library_info():
+    """What the bench line records about the library it measured."""
+    st = os.stat(LIB_PATH)
+    return {"path": os.path.relpath(LIB_PATH, os.path.join(PKG_DIR, "..")), "mtime": st.st_mtime,
+            "srchash": (built_hash() or "")[:16], "fresh": built_hash() == source_hash()}

@@ -30,14 +30,14 @@ class CartesianTrajectoryGenerator:
         self.traj_scale = 0.5
         self.model = model if model is not None else compile_mjcf(model_path, obs_site=ee_site_name)
         self.device = device
-        self._sim1 = None
+        self._sims = {}
 
     def _sim(self, n):
-        if n == 1:
-            if self._sim1 is None:
-                self._sim1 = BatchSim(self.model, 1, self.device)
-            return self._sim1
-        return BatchSim(self.model, n, self.device)
+        """One batch per size, reused across calls (the model's hull LUT and device copy are
+        shared by all of them, sim.SimModel)."""
+        if n not in self._sims:
+            self._sims[n] = BatchSim(self.model, n, self.device)
+        return self._sims[n]
 
     def cartesian_path(self, traj_name="Fig8"):
         t_param = 1.6 + 0.02 * np.linspace(0, self.time_horizon * 5, len(self.time_vector))

@@ -13,7 +13,9 @@
 #include <cstring>
 #include <string>
 #include <type_traits>
+#include <mutex>
 #include <thread>
+#include <sched.h>
 #include <vector>
 
 #include "../../include/soarm_sim.h"
@@ -34,9 +36,33 @@ static int fail(int code, const std::string& msg) {
     if (e_ != hipSuccess) return fail(SIM_E_HIP, std::string(#x ": ") + hipGetErrorString(e_)); \
   } while (0)
 
+// read-only model data on one device (constants, hull records, support LUT):
+// uploaded by the first batch created on that device, shared by every later
+// batch of the same model there, freed with the model
+struct DevModel {
+  int device = -1;
+  DModel* d_model = nullptr;
+  float4* d_hv = nullptr;
+  int32_t *d_hadr = nullptr, *d_hadj = nullptr;
+  uint16_t* d_hlut = nullptr;
+  uint4 *d_hrec = nullptr, *d_hlutrec = nullptr;
+  uint16_t* d_hovf = nullptr;
+  void release() {
+    (void)hipSetDevice(device);
+    (void)hipFree(d_model);
+    (void)hipFree(d_hv);
+    (void)hipFree(d_hadr);
+    (void)hipFree(d_hadj);
+    (void)hipFree(d_hlut);
+    (void)hipFree(d_hrec);
+    (void)hipFree(d_hlutrec);
+    (void)hipFree(d_hovf);
+  }
+};
+
 struct sim_model {
   sim_model_desc desc;
-  DModel dm;  // host copy; hull pointers filled per batch
+  DModel dm;  // host copy; hull pointers filled per device upload
   std::vector<float4> hull_vert;
   std::vector<int32_t> hull_adr, hull_adj;
   std::vector<uint16_t> hull_lut;
@@ -44,17 +70,20 @@ struct sim_model {
   std::vector<uint16_t> hull_ovf;
   int lutadr[SIM_MAXGEOM];
   int na = 0, nf = 0;
+  mutable std::mutex mu;             // guards dev (batches may be created from several threads)
+  mutable std::vector<DevModel*> dev;
+  ~sim_model() {
+    for (DevModel* d : dev) {
+      d->release();
+      delete d;
+    }
+  }
 };
 
 struct sim_batch {
   const sim_model* model = nullptr;
   int n = 0, device = 0;
-  DModel* d_model = nullptr;
-  float4* d_hv = nullptr;
-  int32_t *d_hadr = nullptr, *d_hadj = nullptr;
-  uint16_t* d_hlut = nullptr;
-  uint4 *d_hrec = nullptr, *d_hlutrec = nullptr;
-  uint16_t* d_hovf = nullptr;
+  DModel* d_model = nullptr;   // shared per (model, device): DevModel
   float* d_scratch = nullptr;  // contact rows, [slot][env]
   size_t scratch_floats = 0;
   float* d_gpose = nullptr;    // geom world poses [geom*12+k][env]
@@ -602,6 +631,17 @@ static void prof_mark(sim_batch* b, int kind, hipStream_t st) {
 }
 
 // ------------------------------------------------------------------ model
+static int host_threads() {
+  int n = 1;
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  if (sched_getaffinity(0, sizeof(set), &set) == 0)
+    n = CPU_COUNT(&set);
+  else
+    n = (int)std::thread::hardware_concurrency();
+  return std::min(16, std::max(1, n));
+}
+
 static float host_impedance(const double* si, double pos, double margin) {
   double dmin = std::fmin(std::fmax(si[0], 1e-4), 0.9999), dmax = std::fmin(std::fmax(si[1], 1e-4), 0.9999);
   if (dmin == dmax || si[2] <= 1e-15) return 0.5 * (dmin + dmax);
@@ -798,6 +838,57 @@ static int validate_and_build(const sim_model_desc& d, sim_model* M) {
   return SIM_OK;
 }
 
+static int upload_into(const sim_model* m, DevModel* D) {
+  DModel dm = m->dm;
+  auto up = [&](auto*& dst, const auto& src) -> int {
+    using T = typename std::remove_reference<decltype(src)>::type::value_type;
+    const size_t bytes = std::max<size_t>(src.size(), 1) * sizeof(T);
+    HIPCHECK(hipMalloc(&dst, bytes));
+    if (!src.empty()) HIPCHECK(hipMemcpy(dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice));
+    return SIM_OK;
+  };
+  if (!m->hull_vert.empty()) {
+    if (int rc = up(D->d_hv, m->hull_vert)) return rc;
+    if (int rc = up(D->d_hadr, m->hull_adr)) return rc;
+    if (int rc = up(D->d_hadj, m->hull_adj)) return rc;
+  }
+  if (int rc = up(D->d_hlut, m->hull_lut)) return rc;
+  if (int rc = up(D->d_hrec, m->hull_rec)) return rc;
+  if (int rc = up(D->d_hlutrec, m->hull_lutrec)) return rc;
+  if (int rc = up(D->d_hovf, m->hull_ovf)) return rc;
+  dm.hull_vert = D->d_hv;
+  dm.hull_adr = D->d_hadr;
+  dm.hull_adj = D->d_hadj;
+  dm.hull_lut = D->d_hlut;
+  dm.hull_rec = D->d_hrec;
+  dm.hull_lutrec = D->d_hlutrec;
+  dm.hull_ovf = D->d_hovf;
+  for (int g = 0; g < MAXG; g++) dm.geom_lutadr[g] = g < m->desc.ngeom ? m->lutadr[g] : -1;
+  HIPCHECK(hipMalloc(&D->d_model, sizeof(DModel)));
+  HIPCHECK(hipMemcpy(D->d_model, &dm, sizeof(DModel), hipMemcpyHostToDevice));
+  return SIM_OK;
+}
+
+// the model's device copy on `device`: made by the first batch there, reused after
+static int upload_model(const sim_model* m, int device, DModel** out) {
+  std::lock_guard<std::mutex> lk(m->mu);
+  for (DevModel* d : m->dev)
+    if (d->device == device) {
+      *out = d->d_model;
+      return SIM_OK;
+    }
+  DevModel* D = new DevModel();
+  D->device = device;
+  const int rc = upload_into(m, D);
+  if (rc) {  // nothing half-uploaded stays cached
+    D->release();
+    delete D;
+    return rc;
+  }
+  m->dev.push_back(D);
+  *out = D->d_model;
+  return SIM_OK;
+}
 // ============================================================== C ABI
 extern "C" {
 
@@ -866,10 +957,23 @@ int sim_model_create(const sim_model_desc* desc, const float* hull_vert, const i
         out[c] = (uint16_t)best;
       }
     };
-    const int nt = (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+    // pool sized to the CPUs this process may run on (the GPU box gives each job a share of
+    // the machine), at most 16; if a thread cannot be started its cells run on this one
+    const int nt = host_threads();
     std::vector<std::thread> pool;
-    for (int t = 0; t < nt; t++)
-      pool.emplace_back(cells, (int)((long)HULL_LUT_CELLS * t / nt), (int)((long)HULL_LUT_CELLS * (t + 1) / nt));
+    int started = 0;
+    for (int t = 0; t < nt; t++) {
+      const int c0 = (int)((long)HULL_LUT_CELLS * t / nt), c1 = (int)((long)HULL_LUT_CELLS * (t + 1) / nt);
+      if (t + 1 < nt && started == t) {
+        try {
+          pool.emplace_back(cells, c0, c1);
+          started++;
+          continue;
+        } catch (...) {
+        }
+      }
+      cells(c0, c1);
+    }
     for (auto& th : pool) th.join();
     k++;
   }
@@ -932,36 +1036,10 @@ int sim_batch_create(const sim_model* m, int n_envs, int device, sim_batch** out
   B->n = n_envs;
   if (const char* ng = getenv("SOARM_NO_GRAPH")) B->use_graphs = ng[0] != '1';
   B->device = device;
-  DModel dm = m->dm;
-  if (!m->hull_vert.empty()) {
-    HIPCHECK(hipMalloc(&B->d_hv, m->hull_vert.size() * sizeof(float4)));
-    HIPCHECK(hipMemcpy(B->d_hv, m->hull_vert.data(), m->hull_vert.size() * sizeof(float4), hipMemcpyHostToDevice));
-    HIPCHECK(hipMalloc(&B->d_hadr, m->hull_adr.size() * sizeof(int32_t)));
-    HIPCHECK(hipMemcpy(B->d_hadr, m->hull_adr.data(), m->hull_adr.size() * sizeof(int32_t), hipMemcpyHostToDevice));
-    HIPCHECK(hipMalloc(&B->d_hadj, m->hull_adj.size() * sizeof(int32_t)));
-    HIPCHECK(hipMemcpy(B->d_hadj, m->hull_adj.data(), m->hull_adj.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  if (int rc = upload_model(m, device, &B->d_model)) {
+    delete B;
+    return rc;
   }
-  dm.hull_vert = B->d_hv;
-  dm.hull_adr = B->d_hadr;
-  dm.hull_adj = B->d_hadj;
-  HIPCHECK(hipMalloc(&B->d_hlut, m->hull_lut.size() * sizeof(uint16_t)));
-  HIPCHECK(hipMemcpy(B->d_hlut, m->hull_lut.data(), m->hull_lut.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
-  dm.hull_lut = B->d_hlut;
-  auto up = [&](auto& dst, const auto& src) {
-    using T = typename std::remove_reference<decltype(src)>::type::value_type;
-    HIPCHECK(hipMalloc(&dst, src.size() * sizeof(T)));
-    HIPCHECK(hipMemcpy(dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice));
-    return 0;
-  };
-  if (int rc = up(B->d_hrec, m->hull_rec)) return rc;
-  if (int rc = up(B->d_hlutrec, m->hull_lutrec)) return rc;
-  if (int rc = up(B->d_hovf, m->hull_ovf)) return rc;
-  dm.hull_rec = B->d_hrec;
-  dm.hull_lutrec = B->d_hlutrec;
-  dm.hull_ovf = B->d_hovf;
-  for (int g = 0; g < MAXG; g++) dm.geom_lutadr[g] = g < m->desc.ngeom ? m->lutadr[g] : -1;
-  HIPCHECK(hipMalloc(&B->d_model, sizeof(DModel)));
-  HIPCHECK(hipMemcpy(B->d_model, &dm, sizeof(DModel), hipMemcpyHostToDevice));
   if (!m->desc.disable_contact) {
     const int nv = m->desc.nv;
     B->scratch_floats = (size_t)4 * SIM_MAXCON * (2 * nv + 4) * n_envs;
@@ -980,14 +1058,6 @@ int sim_batch_create(const sim_model* m, int n_envs, int device, sim_batch** out
 void sim_batch_free(sim_batch* b) {
   if (!b) return;
   (void)hipSetDevice(b->device);
-  (void)hipFree(b->d_model);
-  (void)hipFree(b->d_hv);
-  (void)hipFree(b->d_hadr);
-  (void)hipFree(b->d_hadj);
-  (void)hipFree(b->d_hlut);
-  (void)hipFree(b->d_hrec);
-  (void)hipFree(b->d_hlutrec);
-  (void)hipFree(b->d_hovf);
   (void)hipFree(b->d_scratch);
   (void)hipFree(b->d_gpose);
   (void)hipFree(b->d_cbuf);

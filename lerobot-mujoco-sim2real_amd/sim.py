@@ -1,6 +1,7 @@
 """Host-side batch simulator over the C ABI (``include/soarm_sim.h``).
 
-:class:`BatchSim` owns one ``sim_model`` + ``sim_batch`` and the env state as
+:class:`BatchSim` owns one ``sim_batch`` (sharing its model's cached ``sim_model``,
+:class:`SimModel`) and the env state as
 caller-owned torch tensors on the GPU (SoA ``[field][env]``).  It is the single
 object the reference-shaped APIs (``SOARM101Env``, ``SOARM101VecEnv``,
 ``SOARM101DataGenerator``, ``CartesianTrajectoryGenerator``) drive.  Every call
@@ -48,6 +49,46 @@ def reset_qpos_draw(seed, env_ids, nobs=5):
     return np.float32(-0.3) + np.float32(0.6) * u
 
 
+class SimModel:
+    """One ``sim_model`` (MJCF constants + hull records + support LUT) per compiled model.
+
+    Building the hull support LUT is the expensive part of model creation (exact
+    argmax over every hull vertex for 6x96x96 directions per mesh), so it is done
+    once per :class:`CompiledModel` and shared: every :class:`BatchSim` of the
+    model holds this handle, and the library shares the model's device copy
+    among the batches on one GPU.  The handle outlives its batches (they keep a
+    reference), as ``sim_model_free`` requires."""
+
+    def __init__(self, cm, lib):
+        self.lib = lib
+        d = cm.desc
+        self.key = bytes(d)
+        self._hv = np.ascontiguousarray(cm.hull_vert, np.float32)
+        self._hadr = np.ascontiguousarray(cm.hull_adr, np.int32)
+        self._hadj = np.ascontiguousarray(cm.hull_adj, np.int32)
+        self.ptr = C.c_void_p()
+        abi.check(lib, lib.sim_model_create(
+            C.byref(d), self._hv.ctypes.data_as(C.c_void_p), self._hadr.ctypes.data_as(C.c_void_p),
+            self._hadj.ctypes.data_as(C.c_void_p), C.byref(self.ptr)))
+
+    @classmethod
+    def of(cls, cm, lib):
+        """The cached handle of `cm` (rebuilt if its desc was edited since)."""
+        h = getattr(cm, "_sim_model", None)
+        if h is None or h.key != bytes(cm.desc):
+            h = cls(cm, lib)
+            cm._sim_model = h
+        return h
+
+    def __del__(self):
+        try:
+            if self.ptr:
+                self.lib.sim_model_free(self.ptr)
+                self.ptr = None
+        except Exception:
+            pass
+
+
 class BatchSim:
     """`n_envs` SO-ARM101 environments stepped in lockstep on one GPU."""
 
@@ -65,13 +106,8 @@ class BatchSim:
         self.nq, self.nv, self.nu = d.nq, d.nv, d.nu
         self.nact, self.obs_dim = d.nact, 3 + d.obs_nq
         self.frame_skip = max(1, int(round(0.02 / d.timestep)))
-        self._hv = np.ascontiguousarray(self.cm.hull_vert, np.float32)
-        self._hadr = np.ascontiguousarray(self.cm.hull_adr, np.int32)
-        self._hadj = np.ascontiguousarray(self.cm.hull_adj, np.int32)
-        self._model = C.c_void_p()
-        abi.check(self.lib, self.lib.sim_model_create(
-            C.byref(d), self._hv.ctypes.data_as(C.c_void_p), self._hadr.ctypes.data_as(C.c_void_p),
-            self._hadj.ctypes.data_as(C.c_void_p), C.byref(self._model)))
+        self._handle = SimModel.of(self.cm, self.lib)  # shared; kept alive by this batch
+        self._model = self._handle.ptr
         self._batch = C.c_void_p()
         abi.check(self.lib, self.lib.sim_batch_create(self._model, self.n, device, C.byref(self._batch)))
         f32 = dict(dtype=torch.float32, device=self.device)
@@ -102,9 +138,7 @@ class BatchSim:
         if getattr(self, "_batch", None):
             self.lib.sim_batch_free(self._batch)
             self._batch = None
-        if getattr(self, "_model", None):
-            self.lib.sim_model_free(self._model)
-            self._model = None
+        self._handle = None  # the model is freed when its last batch lets go
 
     def __del__(self):
         try:

@@ -407,6 +407,12 @@ def test_generate_and_save_data_cache(gpu_lib, tmp_path):
     for t in ("random", "sin", "chirp"):
         assert g.test_data_dict[t].shape == (32, 8, 13)
     assert np.abs(g.train_data[:, :, :5]).max() <= 0.5 + 1e-6
+    # splits are independent draws (one advancing stream in the reference, :97-132):
+    # no val trajectory starts where a train one does, val and test_random inputs differ
+    v0, t0 = g.val_data[:, 0, 8:13], g.train_data[:32, 0, 8:13]
+    assert (np.abs(v0 - t0).max(1) > 1e-3).all()
+    assert (np.abs(g.val_data[:, :, :5] - g.test_data_dict["random"][:, :, :5]).max((1, 2)) > 1e-3).all()
+    assert np.abs(g.test_data_dict["sin"][:, :, :5] - g.test_data_dict["chirp"][:, :, :5]).max() > 1e-3
     mt = {n: os.path.getmtime(os.path.join(d, n)) for n in names}
     g2 = SOARM101DataGenerator(a)
     g2.generate_and_save_data()  # resumes from the cache
