@@ -34,7 +34,7 @@ def parse():
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--envs", type=int, default=None, help="envs per GPU (default 4096; 8192 for dr)")
-    p.add_argument("--config", default="contact", choices=["contact", "nocontact", "dr", "rollout"])
+    p.add_argument("--config", default="contact", choices=["contact", "nocontact", "dr", "rollout", "mpc"])
     p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal on one GPU)")
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -44,7 +44,8 @@ def parse():
 
 
 def cpu_baseline(cfg_name, seconds, seed):
-    """The float64 oracle (C restatement of mj_step) on the host cores, bounded sample."""
+    """The float64 oracle (C restatement of mj_step; for `mpc` plus the numpy MPC restatement)
+    on the host cores, a bounded sample of the same workload: chunks of envs x T env-steps."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
     from oracle import Oracle
@@ -58,11 +59,16 @@ def cpu_baseline(cfg_name, seconds, seed):
     except AttributeError:
         cores = os.cpu_count()
     cores = max(1, min(cores, 16))  # the GPU box's CPU share is 16
-    n, T = 256, 10
-    done, t0 = 0, time.perf_counter()
-    chunk = 0
-    while time.perf_counter() - t0 < seconds:
-        ids = np.arange(chunk * n, (chunk + 1) * n)
+    T = 10
+    mpc = None
+    if cfg["action"] == "koopman_mpc":
+        import koopman_mpc as KO
+        net, _ = _mpc_net(seed)
+        A, B = net.lA.weight.detach().numpy(), net.lB.weight.detach().numpy()
+        mpc = (KO, A, B, net.encoder_layers(), KO.prepare(A, B))
+
+    def run_chunk(ids, nthreads):
+        n = len(ids)
         st = orc.new_state(n)
         q = W.initial_qpos(cm, ids, seed)
         orc.reset(st, init_qpos=q[:, :5], extra_qpos=q)
@@ -71,10 +77,20 @@ def cpu_baseline(cfg_name, seconds, seed):
         if cfg["dr"]:
             p = W.dr_params(ids, seed)
             prm = np.stack([p["mass_scale"], p["friction"], p["damping_scale"]], 1).astype(np.float64)
-        rng = np.random.default_rng(chunk)
+        rng = np.random.default_rng(int(ids[0]))
         phase = W.ik_phase(ids, seed)
         qstar = q.astype(np.float64)
+        if mpc:  # Koopman_MPC.py loop on the oracle (joint refs: the start pose)
+            KO, A, B, layers, qp = mpc
+            cart = np.stack([W.fig8_targets(t - 1.0, phase) for t in range(T)])
+            sref = np.concatenate([cart, np.repeat(q[None, :, :5].astype(np.float64), T, 0)], -1)
+            zref = KO.encode(layers, sref.reshape(T * n, 8)).reshape(T, n, -1)
+            x, up = sref[0], np.zeros((n, 5))
         for t in range(T):
+            if mpc:
+                up, a = KO.get_control(A, B, KO.encode(layers, x), KO.lifted_window(zref, t, 10), up, qp=qp)
+                x = orc.step(st, a, nthreads=nthreads, applied=orc.bias(st)).astype(np.float32).astype(np.float64)
+                continue
             if cfg["action"] == "chirp":
                 a = W.chirp_action(tab, t)
             elif cfg["action"] == "ik_fig8":
@@ -82,20 +98,20 @@ def cpu_baseline(cfg_name, seconds, seed):
                 a = W.ik_action(qstar[:, :5], st["qpos"][:, :5])
             else:
                 a = rng.uniform(-0.5, 0.5, (n, 5))
-            orc.step(st, a, params=prm, nthreads=cores)
-            done += n
+            orc.step(st, a, params=prm, nthreads=nthreads)
+        return n * T
+
+    n = 256
+    done, chunk, t0 = 0, 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        done += run_chunk(np.arange(chunk * n, (chunk + 1) * n), cores)
         chunk += 1
     dt = time.perf_counter() - t0
-    # the same oracle on ONE core (SURVEY 8d asks for both), a shorter sample of chunk 0's envs
-    st = orc.new_state(64)
-    q = W.initial_qpos(cm, np.arange(64), seed)
-    orc.reset(st, init_qpos=q[:, :5], extra_qpos=q)
-    tab = W.chirp_tables(np.arange(64), seed)
-    d1, t1 = 0, time.perf_counter()
+    # the same workload on ONE core (SURVEY 8d asks for both), a shorter sample of 64-env chunks
+    d1, c1, t1 = 0, 0, time.perf_counter()
     while time.perf_counter() - t1 < max(1.0, seconds / 4):
-        a = W.chirp_action(tab, d1 // 64) if cfg["action"] == "chirp" else np.zeros((64, 5))
-        orc.step(st, a, nthreads=1)
-        d1 += 64
+        d1 += run_chunk(np.arange(c1 * 64, (c1 + 1) * 64), 1)
+        c1 += 1
     t1 = time.perf_counter() - t1
     cpu_name = "unknown"
     try:
@@ -105,11 +121,23 @@ def cpu_baseline(cfg_name, seconds, seed):
         pass
     import importlib.util
     mj = "available (not used)" if importlib.util.find_spec("mujoco") else "MuJoCo unavailable"
+    what = "float64 C oracle" + (" + numpy MPC restatement" if mpc else "")
     return {"value": done / dt, "unit": "env-steps/s", "cores": cores, "kind": "port",
             "sample": f"{done} env-steps ({chunk} chunks of {n} envs x {T} steps, {cfg_name} workload) "
-                      f"of the float64 C oracle, OpenMP over envs, {dt:.1f} s",
-            "single_core": {"value": d1 / t1, "sample": f"{d1} env-steps of 64 envs on 1 thread, {t1:.1f} s"},
+                      f"of the {what}, OpenMP over envs, {dt:.1f} s",
+            "single_core": {"value": d1 / t1, "sample": f"{d1} env-steps ({c1} chunks of 64 envs x {T} steps) "
+                                                         f"on 1 thread, {t1:.1f} s"},
             "cpu_model": cpu_name, "nproc": os.cpu_count(), "mujoco": mj}
+
+
+def _mpc_net(seed):
+    """Random-init DKUC Koopman model of the reference's architecture (control/koopman.py)."""
+    import torch
+    from lerobot_mujoco_sim2real_amd.args import Args
+    from lerobot_mujoco_sim2real_amd.control.koopman import Koopmanlinear
+    torch.manual_seed(seed)
+    a = Args()
+    return Koopmanlinear(a.x_dim, a.u_dim, a.layers).double(), a
 
 
 def main():
@@ -151,6 +179,20 @@ def main():
     gen.manual_seed(args.seed * 1000003 + rank)
     act = torch.empty((n, 5), dtype=torch.float32, device=dev)
 
+    mpc = cfg["action"] == "koopman_mpc"
+    if mpc:
+        # Koopman_MPC.py loop for every env: Fig8 reference per env (warm-started DLS IK for
+        # its joint angles), lifted and turned into per-frame feedforward once, then per frame
+        # sim_bias -> qfrc_applied, k_mpc_step, sim_step (all on device)
+        from lerobot_mujoco_sim2real_amd.control.MPC_Controler import MPCController
+        from lerobot_mujoco_sim2real_amd.Koopman_MPC import KoopmanMPCTracking
+        net, margs = _mpc_net(args.seed)
+        ctl = MPCController(net, margs, device=gpu)
+        phase = torch.as_tensor(W.ik_phase(ids, args.seed), dtype=torch.float32, device=dev)
+        cart, jq = W.reference_trajectory(sim, phase, args.warmup + args.steps)
+        run = KoopmanMPCTracking(ctl, cm, cart, jq, device=gpu, sim=sim)
+        run.runBefore()
+
     rollout = cfg["action"] == "ik_fig8"
     if rollout:
         # config 5: DLS-IK toward each env's Fig8 target, action = clip((q* - q)/dt), rows
@@ -161,6 +203,9 @@ def main():
         rec = {"i": -1}
 
     def one_step(t):
+        if mpc:
+            run.runFunc()
+            return
         if rollout:
             nonlocal qstar
             qstar, _, _ = sim.ik(W.fig8_targets(float(t), phase, lib=torch), q=qstar)
@@ -201,6 +246,7 @@ def main():
     snap = [x.clone() for x in (sim.qpos, sim.qvel, sim.qacc_warmstart, sim.ctrl, sim.status, sim.obs)]
     snap_gen = gen.get_state()
     snap_qstar = qstar.clone() if rollout else None
+    snap_mpc = (run.u_prev.clone(), run.traj_index, run.state is sim.obs) if mpc else None
     sync()
     t0 = time.perf_counter()
     if rollout:
@@ -243,6 +289,10 @@ def main():
         gen.set_state(snap_gen)
         if rollout:
             qstar = snap_qstar
+        if mpc:
+            run.u_prev.copy_(snap_mpc[0])
+            run.traj_index = snap_mpc[1]
+            run.state = sim.obs if snap_mpc[2] else run.state_all_ref[0]
         t = snap_t
         sync()
         sim.profile_begin()

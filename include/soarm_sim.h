@@ -196,6 +196,10 @@ typedef struct sim_state {
   float* ctrl;            /* [nu][N]  */
   int32_t* status;        /* [N]      SIM_ST_* bits, OR-ed since last reset */
   float* ncon;            /* [N]      running contact-count sum (for contacts/env/substep) */
+  float* qfrc_applied;    /* [nv][N]  MjData.qfrc_applied, or NULL (= 0): added to the smooth
+                             forces of every substep; zeroed with the env on a reset / soft
+                             reset, as mj_resetData does.  Koopman_MPC.py:119 writes it
+                             (gravity compensation qfrc_applied = qfrc_bias) */
 } sim_state;
 
 /* Optional per-env domain-randomisation parameters (DEVICE, [N] each; NULL = nominal). */
@@ -242,6 +246,10 @@ int sim_step(sim_batch* b, const sim_state* s, const float* action, int frame_sk
 
 /* one plain mj_step-equivalent on the current ctrl, no obs (frame_skip substeps) */
 int sim_substeps(sim_batch* b, const sim_state* s, int nsub, void* stream);
+
+/* replaces reading d.qfrc_bias after mj_forward (Koopman_MPC.py:119,126): RNE with the
+   current qvel, gravity + Coriolis/centrifugal, out [nv][N] */
+int sim_bias(sim_batch* b, const sim_state* s, float* qfrc_bias, void* stream);
 
 /* observation only (mj_kinematics + _get_state) */
 int sim_observe(sim_batch* b, const sim_state* s, float* obs, void* stream);

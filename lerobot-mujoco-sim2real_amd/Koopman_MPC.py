@@ -1,0 +1,78 @@
+"""Koopman-MPC trajectory tracking, batched: the reference's ``Test`` loop for n envs at once.
+
+Reference: ``Koopman_MPC.py:29-230`` (one env, a viewer, casadi/IPOPT, ZMQ to the real arm).
+Per frame k of a T-frame reference ``state_all_ref = [cartesian xyz, joint angles]``
+(``:49``) the reference does (``runFunc`` :110-136, ``runMPC`` :197-222):
+
+1. ``qfrc_applied = qfrc_bias``  (gravity compensation from the last ``mj_forward``, :119)
+2. lift the reference window ``state_all_ref[k+1 .. k+H]`` (zero rows past the end, :199-205)
+   and the current state (``state_all_ref[0]`` on the first frame, :91; the last observation
+   afterwards, :221), solve the MPC, ``u_prev = u0`` (:219)
+3. ``env.step(clip(u0, +-0.5))`` (:220), ``mj_forward`` (:126)
+
+:class:`KoopmanMPCTracking` runs that loop for n envs on one GPU with no host round trip:
+``sim_bias`` writes ``qfrc_applied`` in place, the reference is lifted and turned into per-frame
+feedforward terms once (the reference recomputes the same lifted rows every frame), then each
+frame is ``sim_bias`` + ``sim_koopman_mpc_step`` + ``sim_step``.  The viewer drawing, the
+return-to-home playback after the last frame (:137-175) and the ZMQ send to the robot (:186-190)
+are out of scope.
+"""
+from .sim import BatchSim
+
+
+class KoopmanMPCTracking:
+    """n envs tracking their own reference trajectories with one MPCController."""
+
+    def __init__(self, controller, model, cartesian_points, joint_angle_traj, device=0, sim=None):
+        import torch
+
+        self.torch = torch
+        self.ctl = controller
+        dev = torch.device("cuda", device)
+        cp = torch.as_tensor(cartesian_points, dtype=torch.float32, device=dev)
+        jq = torch.as_tensor(joint_angle_traj, dtype=torch.float32, device=dev)
+        if cp.ndim == 2:  # one trajectory for every env
+            cp, jq = cp[:, None], jq[:, None]
+        self.total_frames, self.n = jq.shape[0], jq.shape[1]
+        self.num_joints = jq.shape[2]
+        # state_all_ref = hstack([cartesian_points, joint_angle_traj]) (Koopman_MPC.py:49)
+        self.state_all_ref = torch.cat([cp, jq], -1).contiguous()
+        self.sim = sim if sim is not None else BatchSim(model, self.n, device)
+        self.sim.enable_qfrc_applied()
+        self.H = controller.H
+        zref = controller.lift_reference(self.state_all_ref)
+        self.ff = controller.feedforward(zref)  # [T, u, n]
+        self.u_prev = torch.zeros((controller.u_dim, self.n), dtype=torch.float64, device=dev)
+        self.action = torch.empty((self.n, controller.u_dim), dtype=torch.float32, device=dev)
+        self.traj_index = 0
+
+    def runBefore(self):
+        """qpos[:num_joints] = joint_angle_traj[0] on a fresh MjData (qvel, ctrl, warm start 0),
+        mj_forward; the first MPC state is state_all_ref[0] (Koopman_MPC.py:83-91)."""
+        q0 = self.state_all_ref[0, :, 3:3 + self.num_joints]
+        self.sim.reset(init_qpos=q0, init_qvel=self.torch.zeros_like(q0))
+        self.state = self.state_all_ref[0]
+        self.traj_index = 0
+        self.u_prev.zero_()
+
+    def runFunc(self):
+        """One frame: gravity compensation, MPC, env.step (Koopman_MPC.py:110-136, 197-222)."""
+        k = self.traj_index
+        self.sim.bias(out=self.sim.qfrc_applied)
+        self.ctl.step(self.state, self.ff[k], self.u_prev, self.action)
+        self.state = self.sim.step(self.action)
+        self.traj_index += 1
+        return self.state
+
+    def run(self, frames=None, record=True):
+        """runBefore + `frames` (default: all) x runFunc; returns the observed states
+        [frames, n, 8] (device) as the reference's actual_traj."""
+        frames = self.total_frames if frames is None else min(frames, self.total_frames)
+        self.runBefore()
+        out = self.torch.empty((frames, self.n, self.state_all_ref.shape[2]), dtype=self.torch.float32,
+                               device=self.state_all_ref.device) if record else None
+        for k in range(frames):
+            s = self.runFunc()
+            if record:
+                out[k] = s
+        return out

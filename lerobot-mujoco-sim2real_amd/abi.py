@@ -92,7 +92,17 @@ class SimState(C.Structure):
     _fields_ = [
         ("qpos", C.c_void_p), ("qvel", C.c_void_p), ("qacc_warmstart", C.c_void_p),
         ("ctrl", C.c_void_p), ("status", C.c_void_p), ("ncon", C.c_void_p),
+        ("qfrc_applied", C.c_void_p),
     ]
+
+
+KMAXLAYER = 6
+
+
+class KoopmanDesc(C.Structure):
+    """``sim_koopman_desc`` (include/koopman_mpc.h)."""
+    _fields_ = [("x_dim", i32), ("u_dim", i32), ("nlayer", i32), ("width", _a(i32, KMAXLAYER + 1)),
+                ("horizon", i32), ("_pad", i32), ("u_clip", f64)]
 
 
 class SimParams(C.Structure):
@@ -106,8 +116,11 @@ LIB_PATH = os.path.join(PKG_DIR, "csrc", "libsoarm_sim.so")
 EXPORTS = [
     "sim_last_error", "sim_version", "sim_model_create", "sim_model_free",
     "sim_batch_create", "sim_batch_free", "sim_batch_set_params", "sim_reset",
-    "sim_step", "sim_substeps", "sim_observe", "sim_contacts", "sim_collide_profile", "sim_phase_profile", "sim_ik_dls",
+    "sim_step", "sim_substeps", "sim_bias", "sim_observe", "sim_contacts", "sim_collide_profile", "sim_phase_profile", "sim_ik_dls",
     "sim_profile_begin", "sim_profile_end",
+    # include/koopman_mpc.h
+    "sim_koopman_create", "sim_koopman_free", "sim_koopman_encode", "sim_koopman_feedforward",
+    "sim_koopman_mpc_step",
 ]
 PROF_KINDS = ["step_fused", "collide", "substep", "geom"]
 
@@ -138,12 +151,19 @@ def load_lib(path=None):
     lib.sim_step.argtypes = [vp, C.POINTER(SimState), vp, ip, vp, vp]
     lib.sim_substeps.argtypes = [vp, C.POINTER(SimState), ip, vp]
     lib.sim_observe.argtypes = [vp, C.POINTER(SimState), vp, vp]
+    lib.sim_bias.argtypes = [vp, C.POINTER(SimState), vp, vp]
     lib.sim_contacts.argtypes = [vp, C.POINTER(SimState), vp, vp, vp]
     lib.sim_collide_profile.argtypes = [vp, C.POINTER(SimState), vp, vp]
     lib.sim_phase_profile.argtypes = [vp, ip]
     lib.sim_profile_begin.argtypes = [vp]
     lib.sim_profile_end.argtypes = [vp, vp, vp]
     lib.sim_ik_dls.argtypes = [vp, vp, vp, vp, vp, C.POINTER(IkOpts), vp]
+    lib.sim_koopman_create.argtypes = [C.POINTER(KoopmanDesc), vp, vp, ip, C.POINTER(vp)]
+    lib.sim_koopman_free.argtypes = [vp]
+    lib.sim_koopman_free.restype = None
+    lib.sim_koopman_encode.argtypes = [vp, ip, vp, vp, vp]
+    lib.sim_koopman_feedforward.argtypes = [vp, ip, ip, ip, vp, vp, vp]
+    lib.sim_koopman_mpc_step.argtypes = [vp, ip, vp, vp, vp, vp, vp, vp]
     for name in EXPORTS:
         if not hasattr(lib, name):
             raise RuntimeError(f"{p} does not export {name}")

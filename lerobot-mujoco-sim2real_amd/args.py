@@ -1,9 +1,10 @@
 """Hot-path subset of the reference's ``Args`` (``args.py:3-122``).
 
-Only the fields the data-collection path reads are kept (SURVEY.md §2 marks
-the training/MPC fields out of scope): sample/step counts (``args.py:27-34``),
+Only the fields the data-collection and MPC-tracking paths read are kept (SURVEY.md §2 marks
+the training fields out of scope): sample/step counts (``args.py:27-34``),
 ``x_dim``/``u_dim`` (``:47-50``), ``device`` (``:70``), the scene path
-(``:91``) and the ``.npy`` cache paths (``:97-100``).  ``__getattr__`` passes
+(``:91``), the ``.npy`` cache paths (``:97-100``) and the Koopman-MPC fields the batched
+controller reads (``model`` :13, ``MPC_type`` :75, ``layers`` :103).  ``__getattr__`` passes
 through to the parsed namespace as the reference does (``:120-122``).
 """
 import argparse
@@ -29,6 +30,9 @@ class Args:
         p.add_argument("--eval_batch_size", type=int, default=128)
         p.add_argument("--device", type=str, default="cuda", choices=["cpu", "cuda"])
         p.add_argument("--data_root", type=str, default=os.path.abspath("."))
+        # Koopman-MPC tracking: model kind (:13), MPC form (:75)
+        p.add_argument("--model", type=str, default="DKUC", choices=["DKUC", "DBKN"])
+        p.add_argument("--MPC_type", type=str, default="delta_mpc", choices=["mpc", "delta_mpc"])
         self.args = p.parse_args([] if argv is None else argv)
         self.process_args()
 
@@ -40,6 +44,7 @@ class Args:
         a.data_dir_load_test = os.path.join(
             a.data_dir_save, f"test_data_{a.test_type}_{a.test_samples}_{a.test_steps}.npy")
         a.data_dir_load_val = os.path.join(a.data_dir_save, f"val_data_{a.test_samples}_{a.test_steps}.npy")
+        a.layers = [a.x_dim, 64, 64, 64, 64, 24]  # Koopman encoder widths (:103)
 
     def __getattr__(self, name):
         return getattr(self.args, name)

@@ -14,7 +14,7 @@ import time
 from .abi import LIB_PATH, PKG_DIR
 
 SRC_DIR = os.path.join(PKG_DIR, "csrc")
-SOURCES = ["soarm_sim.hip"]
+SOURCES = ["soarm_sim.hip", "koopman_mpc.hip"]
 HEADERS = ["dmodel.h", "soarm_kernels.h", "soarm_step.h", "soarm_collide.h", "soarm_pgs.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # -fno-slp-vectorize: the per-lane algebra gains nothing from v_pk_* packing; the
@@ -28,7 +28,7 @@ def source_hash():
     """sha256 over the flags and every source/header the library is built from."""
     h = hashlib.sha256(" ".join(FLAGS).encode())
     deps = [os.path.join(SRC_DIR, f) for f in SOURCES + HEADERS]
-    deps.append(os.path.join(PKG_DIR, "..", "include", "soarm_sim.h"))
+    deps += [os.path.join(PKG_DIR, "..", "include", h) for h in ("soarm_sim.h", "koopman_mpc.h")]
     for d in deps:
         h.update(os.path.basename(d).encode())
         with open(d, "rb") as f:

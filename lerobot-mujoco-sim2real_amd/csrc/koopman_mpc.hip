@@ -1,0 +1,371 @@
+// koopman_mpc.hip — batched Koopman-MPC (include/koopman_mpc.h) on float64 MFMA.
+//
+// Reference: control/MPC_Controler.py (MPCController: Psi_o :154-167, setup_mpc :65-98,
+// setup_delta_mpc :100-141, get_control :143-152) and the tracking loop Koopman_MPC.py:197-222,
+// one env, casadi/IPOPT, float64.  Here one wave serves 16 envs:
+//
+//   encoder  z = [x, MLP(x)]  (models/KoopmanBase.py:45-47): every Linear layer is a chain of
+//            v_mfma_f64_16x16x4_f64 with the 16 envs on the MFMA's N side and the layer's output
+//            rows in 16-row tiles.  The f64 MFMA's C/D layout (lane l, register r holds row
+//            (l >> 4) + 4r, column l & 15) is exactly its B-operand layout for the k-step that
+//            covers those 4 rows (B: lane l holds row k = l >> 4 of the step, column l & 15), so a
+//            layer's output tile T register r IS the next layer's B operand for k-step 4T + r:
+//            activations never leave registers, no LDS round trip, no shuffles.
+//   control  u0 = ff + [Gz | Gu] [z0; u_prev] is one more 16-row MFMA tile over the same B
+//            operands (z0's tiles, then u_prev), with ff as the accumulator's initial value.
+//
+// The weights of every layer are stored by the host in MFMA fragment order (tile, k-step, lane),
+// so a workgroup stages them into LDS with linear 16-B copies and every A-operand read is a
+// conflict-free, lane-contiguous ds_read_b64.  4096 envs = 256 waves = 64 workgroups of 4 waves.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/koopman_mpc.h"
+
+int soarm_set_error(int code, const std::string& msg);  // soarm_sim.hip (sim_last_error)
+
+namespace {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+constexpr int KT = SIM_KMAXW / 16;  // 16-row tiles of a layer's output (4)
+
+// device-side layout of one controller (kernel argument; offsets in doubles into the fragment blob)
+struct KDev {
+  int xd, ud, nl, nz, H, outw;
+  int ntile[SIM_KMAXLAYER];  // 16-row output tiles of layer l
+  int ks[SIM_KMAXLAYER];     // 4-deep k-steps of layer l (2 for layer 0: x padded to 8)
+  int frag[SIM_KMAXLAYER];   // A fragments of layer l: [ntile][ks][64]
+  int bias;                  // [nl][64]
+  int gain;                  // [Gz | Gu] fragments: [ks_gain][64], rows = u (one tile)
+  int ks_gain;               // 2 (x) + 4 * ntile[nl-1] (features) + 2 (u_prev)
+  int total;                 // doubles staged in LDS by k_mpc_step / k_encode
+  int gr_ks;                 // Gr fragments (feedforward): [gr_ks][64], K = H * nz
+  double uclip;
+};
+
+#define DEVI __device__ __forceinline__
+
+DEVI d4 mfma(double a, double b, d4 c) { return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0); }
+
+// stage `count` doubles global -> LDS (16-B copies; count is a multiple of 2, offsets 16-B aligned)
+DEVI void stage(double* lds, const double* __restrict__ g, int count) {
+  const double2* src = reinterpret_cast<const double2*>(g);
+  double2* dst = reinterpret_cast<double2*>(lds);
+  for (int i = threadIdx.x; i < count / 2; i += blockDim.x) dst[i] = src[i];
+  __syncthreads();
+}
+
+// the encoder for this wave's 16 envs: xb = x as the B operand of k-steps 0..1 (lane: row
+// 4s + (lane >> 4), env lane & 15); returns the last layer's output tiles in `act`
+DEVI void encode(const KDev& K, const double* lds, int lane, const double xb[2], d4 (&act)[KT]) {
+  const int kq = lane >> 4;
+#pragma unroll
+  for (int l = 0; l < SIM_KMAXLAYER; l++) {
+    if (l >= K.nl) continue;  // (continue, not break: the loop must unroll fully)
+    const int nt = K.ntile[l], ks = K.ks[l];
+    const double* A = lds + K.frag[l] + lane;
+    const double* bias = lds + K.bias + l * SIM_KMAXW;
+    d4 acc[KT];
+#pragma unroll
+    for (int T = 0; T < KT; T++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) acc[T][r] = bias[16 * T + kq + 4 * r];
+    // k-steps outer, tiles inner: KT independent accumulator chains
+#pragma unroll
+    for (int s = 0; s < 4 * KT; s++) {
+      if (s >= ks) continue;
+      const double b = (l == 0) ? (s < 2 ? xb[s] : 0.0) : act[s >> 2][s & 3];
+#pragma unroll
+      for (int T = 0; T < KT; T++)
+        if (T < nt) acc[T] = mfma(A[(T * ks + s) * 64], b, acc[T]);
+    }
+    const bool relu = l + 1 < K.nl;
+#pragma unroll
+    for (int T = 0; T < KT; T++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) act[T][r] = (T < nt) ? (relu ? fmax(acc[T][r], 0.0) : acc[T][r]) : 0.0;
+  }
+}
+
+// x rows of the wave's envs as B operands (f32 obs -> f64, as torch.DoubleTensor(obs))
+DEVI void load_x(const KDev& K, const float* __restrict__ x, int e, bool live, int kq, double xb[2]) {
+#pragma unroll
+  for (int s = 0; s < 2; s++) {
+    const int row = 4 * s + kq;
+    xb[s] = (live && row < K.xd) ? (double)x[(size_t)e * K.xd + row] : 0.0;
+  }
+}
+
+// Psi_o for m states: z [nz][m]
+__global__ __launch_bounds__(256) void k_encode(KDev K, const double* __restrict__ frag, int m,
+                                                const float* __restrict__ x, double* __restrict__ z) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  stage(lds, frag, K.total);
+  const int lane = threadIdx.x & 63, kq = lane >> 4;
+  const int e = blockIdx.x * 64 + (threadIdx.x >> 6) * 16 + (lane & 15);
+  const bool live = e < m;  // every lane runs the MFMAs (they need the full wave)
+  double xb[2];
+  load_x(K, x, e, live, kq, xb);
+  d4 act[KT];
+  encode(K, lds, lane, xb, act);
+  if (!live) return;
+#pragma unroll
+  for (int s = 0; s < 2; s++)
+    if (4 * s + kq < K.xd) z[(size_t)(4 * s + kq) * m + e] = xb[s];
+#pragma unroll
+  for (int T = 0; T < KT; T++)
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int row = 16 * T + kq + 4 * r;
+      if (row < K.outw) z[(size_t)(K.xd + row) * m + e] = act[T][r];
+    }
+}
+
+// u0 = ff + Gz z0 + Gu u_prev (z0 = Psi_o(x) unless given); u_prev <- u0; action = clip(u0)
+__global__ __launch_bounds__(256) void k_mpc_step(KDev K, const double* __restrict__ frag, int n,
+                                                  const float* __restrict__ x, const double* __restrict__ z0,
+                                                  const double* __restrict__ ff, double* __restrict__ uprev,
+                                                  float* __restrict__ action) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  stage(lds, frag, K.total);
+  const int lane = threadIdx.x & 63, kq = lane >> 4;
+  const int e = blockIdx.x * 64 + (threadIdx.x >> 6) * 16 + (lane & 15);
+  const bool live = e < n;
+  double xb[2];
+  d4 act[KT];
+  if (z0) {  // lifted state given (get_control(p), MPC_Controler.py:143)
+#pragma unroll
+    for (int s = 0; s < 2; s++) {
+      const int row = 4 * s + kq;
+      xb[s] = (live && row < K.xd) ? z0[(size_t)row * n + e] : 0.0;
+    }
+#pragma unroll
+    for (int T = 0; T < KT; T++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int row = 16 * T + kq + 4 * r;
+        act[T][r] = (live && row < K.outw) ? z0[(size_t)(K.xd + row) * n + e] : 0.0;
+      }
+  } else {
+    load_x(K, x, e, live, kq, xb);
+    encode(K, lds, lane, xb, act);
+  }
+  // one output tile: rows = u index (kq + 4r), columns = envs
+  d4 u;
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const int row = kq + 4 * r;
+    u[r] = (live && ff && row < K.ud) ? ff[(size_t)row * n + e] : 0.0;
+  }
+  const double* G = lds + K.gain + lane;
+  u = mfma(G[0], xb[0], u);
+  u = mfma(G[64], xb[1], u);
+  const int nf = K.ks_gain - 4;  // feature k-steps
+#pragma unroll
+  for (int s = 0; s < 4 * KT; s++) {
+    if (s >= nf) continue;
+    u = mfma(G[(2 + s) * 64], act[s >> 2][s & 3], u);
+  }
+#pragma unroll
+  for (int s = 0; s < 2; s++) {
+    const int row = 4 * s + kq;
+    const double up = (live && row < K.ud) ? uprev[(size_t)row * n + e] : 0.0;
+    u = mfma(G[(2 + nf + s) * 64], up, u);
+  }
+  if (!live) return;
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const int row = kq + 4 * r;
+    if (row < K.ud) {
+      uprev[(size_t)row * n + e] = u[r];
+      action[(size_t)e * K.ud + row] = (float)fmin(fmax(u[r], -K.uclip), K.uclip);
+    }
+  }
+}
+
+// ff[f][u][e] = sum_{t<H} Gr_t zref[f+1+t][:][e]  (zero past nref); FR frames per workgroup
+constexpr int FR = 16;
+__global__ __launch_bounds__(256) void k_feedforward(KDev K, const double* __restrict__ grfrag, int nframe,
+                                                     int nref, int n, const double* __restrict__ zref,
+                                                     double* __restrict__ ff) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  stage(lds, grfrag, K.gr_ks * 64);
+  const int lane = threadIdx.x & 63, kq = lane >> 4;
+  const int e = blockIdx.x * 64 + (threadIdx.x >> 6) * 16 + (lane & 15);
+  const bool live = e < n;
+  const int kk = K.H * K.nz;
+  const int f1 = min(nframe, (int)(blockIdx.y + 1) * FR);
+  for (int f = blockIdx.y * FR; f < f1; f++) {
+    d4 acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+    // this lane's reference element of k-step s: g = 4s + kq -> (t, j) = divmod(g, nz)
+    int t = 0, j = kq;
+    while (j >= K.nz) j -= K.nz, t++;
+    for (int s = 0; s < K.gr_ks; s++) {
+      const int g = 4 * s + kq;
+      const int fr = f + 1 + t;
+      const double b = (live && g < kk && fr < nref) ? zref[((size_t)fr * K.nz + j) * n + e] : 0.0;
+      acc[s & 3] = mfma(lds[s * 64 + lane], b, acc[s & 3]);
+      j += 4;
+      while (j >= K.nz) j -= K.nz, t++;
+    }
+    if (live) {
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int row = kq + 4 * r;
+        if (row < K.ud) ff[((size_t)f * K.ud + row) * n + e] = (acc[0][r] + acc[1][r]) + (acc[2][r] + acc[3][r]);
+      }
+    }
+  }
+}
+
+}  // namespace
+
+struct sim_koopman {
+  int device = 0;
+  sim_koopman_desc desc;
+  KDev kd;
+  double* d_frag = nullptr;    // encoder + [Gz | Gu] fragments, biases
+  double* d_grfrag = nullptr;  // Gr fragments
+};
+
+#define KCHECK(x)                                                                                  \
+  do {                                                                                             \
+    hipError_t e_ = (x);                                                                           \
+    if (e_ != hipSuccess) return soarm_set_error(SIM_E_HIP, std::string(#x ": ") + hipGetErrorString(e_)); \
+  } while (0)
+
+extern "C" {
+
+int sim_koopman_create(const sim_koopman_desc* d, const double* weights, const double* gain, int device,
+                       sim_koopman** out) {
+  if (!d || !weights || !gain || !out) return soarm_set_error(SIM_E_ARG, "null argument");
+  *out = nullptr;
+  const int xd = d->x_dim, ud = d->u_dim, nl = d->nlayer, H = d->horizon;
+  if (xd < 1 || xd > SIM_KMAXX) return soarm_set_error(SIM_E_MODEL, "x_dim must be in 1..8");
+  if (ud < 1 || ud > SIM_KMAXU) return soarm_set_error(SIM_E_MODEL, "u_dim must be in 1..8");
+  if (nl < 1 || nl > SIM_KMAXLAYER) return soarm_set_error(SIM_E_MODEL, "nlayer must be in 1..6");
+  if (H < 1 || H > SIM_KMAXH) return soarm_set_error(SIM_E_MODEL, "horizon must be in 1..32");
+  if (d->width[0] != xd) return soarm_set_error(SIM_E_MODEL, "width[0] must equal x_dim");
+  for (int l = 1; l <= nl; l++)
+    if (d->width[l] < 1 || d->width[l] > SIM_KMAXW) return soarm_set_error(SIM_E_MODEL, "encoder widths must be in 1..64");
+  KDev K{};
+  K.xd = xd, K.ud = ud, K.nl = nl, K.H = H, K.outw = d->width[nl], K.nz = xd + d->width[nl];
+  K.uclip = d->u_clip;
+  if (K.H * K.nz > 1024) return soarm_set_error(SIM_E_MODEL, "horizon * nz must be <= 1024");
+  int off = 0;
+  for (int l = 0; l < nl; l++) {
+    K.ntile[l] = (d->width[l + 1] + 15) / 16;
+    K.ks[l] = l == 0 ? 2 : 4 * K.ntile[l - 1];
+    K.frag[l] = off;
+    off += K.ntile[l] * K.ks[l] * 64;
+  }
+  K.bias = off;
+  off += nl * SIM_KMAXW;
+  K.gain = off;
+  K.ks_gain = 2 + 4 * K.ntile[nl - 1] + 2;
+  off += K.ks_gain * 64;
+  K.total = off;
+  K.gr_ks = (K.H * K.nz + 3) / 4;
+  if ((size_t)K.total * 8 > 160 * 1024 || (size_t)K.gr_ks * 64 * 8 > 160 * 1024)
+    return soarm_set_error(SIM_E_MODEL, "controller does not fit in LDS");
+
+  // host packing: fragment order, zero padding
+  std::vector<double> blob(K.total, 0.0), gr((size_t)K.gr_ks * 64, 0.0);
+  const double* w = weights;
+  for (int l = 0; l < nl; l++) {
+    const int in = d->width[l], ou = d->width[l + 1];
+    for (int T = 0; T < K.ntile[l]; T++)
+      for (int s = 0; s < K.ks[l]; s++)
+        for (int lane = 0; lane < 64; lane++) {
+          const int row = 16 * T + (lane & 15), col = 4 * s + (lane >> 4);
+          blob[K.frag[l] + (T * K.ks[l] + s) * 64 + lane] = (row < ou && col < in) ? w[(size_t)row * in + col] : 0.0;
+        }
+    w += (size_t)ou * in;
+    for (int r = 0; r < ou; r++) blob[K.bias + l * SIM_KMAXW + r] = w[r];
+    w += ou;
+  }
+  // gain columns: [Gr (H*nz) | Gz (nz) | Gu (ud)]; B-operand order of the step kernel:
+  // x rows 0..7 (k-steps 0,1), feature rows (4 per k-step), u_prev rows 0..7
+  const int gcols = K.H * K.nz + K.nz + ud;
+  auto gz_col = [&](int kk) -> int {  // padded k index -> gain column (or -1)
+    if (kk < 8) return kk < xd ? K.H * K.nz + kk : -1;
+    kk -= 8;
+    const int nfr = 16 * K.ntile[nl - 1];
+    if (kk < nfr) return kk < K.outw ? K.H * K.nz + xd + kk : -1;
+    kk -= nfr;
+    return kk < ud ? K.H * K.nz + K.nz + kk : -1;
+  };
+  for (int s = 0; s < K.ks_gain; s++)
+    for (int lane = 0; lane < 64; lane++) {
+      const int row = lane & 15, c = gz_col(4 * s + (lane >> 4));
+      blob[K.gain + s * 64 + lane] = (row < ud && c >= 0) ? gain[(size_t)row * gcols + c] : 0.0;
+    }
+  for (int s = 0; s < K.gr_ks; s++)
+    for (int lane = 0; lane < 64; lane++) {
+      const int row = lane & 15, c = 4 * s + (lane >> 4);
+      gr[s * 64 + lane] = (row < ud && c < K.H * K.nz) ? gain[(size_t)row * gcols + c] : 0.0;
+    }
+
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return soarm_set_error(SIM_E_NODEVICE, "no HIP device visible");
+  if (device < 0 || device >= ndev) return soarm_set_error(SIM_E_ARG, "bad device ordinal");
+  KCHECK(hipSetDevice(device));
+  sim_koopman* k = new sim_koopman;
+  k->device = device, k->desc = *d, k->kd = K;
+  if (hipMalloc(&k->d_frag, blob.size() * sizeof(double)) != hipSuccess ||
+      hipMalloc(&k->d_grfrag, gr.size() * sizeof(double)) != hipSuccess) {
+    sim_koopman_free(k);
+    return soarm_set_error(SIM_E_HIP, "hipMalloc failed");
+  }
+  KCHECK(hipMemcpy(k->d_frag, blob.data(), blob.size() * sizeof(double), hipMemcpyHostToDevice));
+  KCHECK(hipMemcpy(k->d_grfrag, gr.data(), gr.size() * sizeof(double), hipMemcpyHostToDevice));
+  KCHECK(hipFuncSetAttribute((const void*)k_encode, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  KCHECK(hipFuncSetAttribute((const void*)k_mpc_step, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  KCHECK(hipFuncSetAttribute((const void*)k_feedforward, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  *out = k;
+  return SIM_OK;
+}
+
+void sim_koopman_free(sim_koopman* k) {
+  if (!k) return;
+  (void)hipSetDevice(k->device);
+  (void)hipFree(k->d_frag);
+  (void)hipFree(k->d_grfrag);
+  delete k;
+}
+
+int sim_koopman_encode(sim_koopman* k, int m, const float* x, double* z, void* stream) {
+  if (!k || !x || !z || m < 0) return soarm_set_error(SIM_E_ARG, "bad argument");
+  if (m == 0) return SIM_OK;
+  hipLaunchKernelGGL(k_encode, dim3((m + 63) / 64), dim3(256), k->kd.total * sizeof(double), (hipStream_t)stream,
+                     k->kd, k->d_frag, m, x, z);
+  KCHECK(hipGetLastError());
+  return SIM_OK;
+}
+
+int sim_koopman_feedforward(sim_koopman* k, int nframe, int nref, int n, const double* zref, double* ff,
+                            void* stream) {
+  if (!k || !zref || !ff || nframe < 0 || nref < 0 || n < 0) return soarm_set_error(SIM_E_ARG, "bad argument");
+  if (nframe == 0 || n == 0) return SIM_OK;
+  hipLaunchKernelGGL(k_feedforward, dim3((n + 63) / 64, (nframe + FR - 1) / FR), dim3(256),
+                     k->kd.gr_ks * 64 * sizeof(double), (hipStream_t)stream, k->kd, k->d_grfrag, nframe, nref, n,
+                     zref, ff);
+  KCHECK(hipGetLastError());
+  return SIM_OK;
+}
+
+int sim_koopman_mpc_step(sim_koopman* k, int n, const float* x, const double* z0, const double* ff,
+                         double* u_prev, float* action, void* stream) {
+  if (!k || (!x && !z0) || !u_prev || !action || n < 0) return soarm_set_error(SIM_E_ARG, "bad argument");
+  if (n == 0) return SIM_OK;
+  hipLaunchKernelGGL(k_mpc_step, dim3((n + 63) / 64), dim3(256), k->kd.total * sizeof(double), (hipStream_t)stream,
+                     k->kd, k->d_frag, n, x, z0, ff, u_prev, action);
+  KCHECK(hipGetLastError());
+  return SIM_OK;
+}
+
+}  // extern "C"

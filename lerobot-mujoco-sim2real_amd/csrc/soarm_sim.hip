@@ -30,6 +30,8 @@ static int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
 }
+// the same error slot for the library's other translation units (koopman_mpc.hip)
+int soarm_set_error(int code, const std::string& msg) { return fail(code, msg); }
 #define HIPCHECK(x)                                                                   \
   do {                                                                                \
     hipError_t e_ = (x);                                                              \
@@ -209,16 +211,23 @@ __device__ unsigned long long g_phase[57];  // [53..56] contact-row build split 
 // (cbuf/ccount, may be null) were produced by k_collide from this substep's positions
 template <int NA, int NF, bool CON>
 DEVI int forward(Sim<NA, NF>& S, const float* cbuf, const int* ccount, const uint32_t* pmask, int n, int e,
-                 const RowLds& L, const ContactRows<NA, NF>& cr) {
+                 const RowLds& L, const ContactRows<NA, NF>& cr, const float* applied = nullptr) {
   S.kinematics();
   S.com_crb();
   S.factor();
   S.smooth_forces();
+  if (applied) S.add_applied(applied, n, e);
   return solve_constraints<NA, NF, CON>(S, cbuf, ccount, pmask, n, e, L, cr);
 }
 
-// contact-free scenes (mjDSBL_CONTACT): all frame_skip substeps fused in one launch
-template <int NA, int NF>
+// mj_resetData zeroes d.qfrc_applied: a reset / soft reset of env e clears its row
+DEVI void zero_applied(float* applied, int nv, int n, int e) {
+  for (int i = 0; i < nv; i++) soa(applied, i, n, e) = 0.f;
+}
+
+// contact-free scenes (mjDSBL_CONTACT): all frame_skip substeps fused in one launch.
+// AP: st.qfrc_applied is set (a separate instantiation keeps the common case's code as is)
+template <int NA, int NF, bool AP>
 __global__ __launch_bounds__(64) void k_step(const DModel* __restrict__ dm, int n, int nsub,
                                              sim_state st, const float* __restrict__ action,
                                              float* __restrict__ obs, sim_params pp) {
@@ -236,12 +245,16 @@ __global__ __launch_bounds__(64) void k_step(const DModel* __restrict__ dm, int 
   __shared__ float s_lim[NA * LF][64];
   const RowLds L{nullptr, &s_lim[0][0], nullptr, nullptr, (int)threadIdx.x, (int)threadIdx.x, 64};
   const ContactRows<NA, NF> cr{nullptr, n};
+  float* const applied = AP ? st.qfrc_applied : nullptr;
   for (int s = 0; s < nsub; s++) {
     S.relaunder();
+    const int sb = S.status;
     S.check_state();
-    forward<NA, NF, false>(S, nullptr, nullptr, nullptr, n, e, L, cr);
+    if (AP && S.status != sb) zero_applied(applied, Sim<NA, NF>::NV, n, e);
+    forward<NA, NF, false>(S, nullptr, nullptr, nullptr, n, e, L, cr, applied);
     if (S.acc_bad()) {
       S.soft_reset(SIM_ST_BADQACC);
+      if (AP) zero_applied(applied, Sim<NA, NF>::NV, n, e);
       forward<NA, NF, false>(S, nullptr, nullptr, nullptr, n, e, L, cr);
     }
     S.integrate();
@@ -315,7 +328,8 @@ DEVI int gather_contacts(const DModel& m, int n, int e, const float* __restrict_
 }
 
 // one substep with contacts: gather -> forward -> Euler -> next substep's geom poses
-template <int NA, int NF>
+// (AP: st.qfrc_applied is set, as in k_step)
+template <int NA, int NF, bool AP>
 __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, int n, sim_state st,
                                                 const float* __restrict__ action,
                                                 float* __restrict__ obs, sim_params pp,
@@ -350,7 +364,10 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
   S.check_state();
   // positions / velocities are re-read from HBM after the solve instead of being held in
   // registers through it: a soft reset must reach HBM first
-  if (S.status != st0) store_state(S, st, n, e);
+  if (S.status != st0) {
+    store_state(S, st, n, e);
+    if (AP) zero_applied(st.qfrc_applied, Sim<NA, NF>::NV, n, e);
+  }
   // a soft reset moved the env: the collide output no longer applies
   const bool use = S.status == st0 && ccount != nullptr;
 #ifdef SOARM_PHASE_PROF
@@ -366,13 +383,16 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
   PSTAMP(4);
   PHASE_T(t2);
   PSTAMP(5);
+  if (AP) S.add_applied(st.qfrc_applied, n, e);
   int ncon = solve_constraints<NA, NF, true>(S, use ? cbuf : nullptr, use ? ccount : nullptr, pmask, n, e, L, cr);
 #else
-  int ncon = forward<NA, NF, true>(S, use ? cbuf : nullptr, use ? ccount : nullptr, pmask, n, e, L, cr);
+  int ncon = forward<NA, NF, true>(S, use ? cbuf : nullptr, use ? ccount : nullptr, pmask, n, e, L, cr,
+                                   AP ? st.qfrc_applied : nullptr);
 #endif
   if (S.acc_bad()) {
     S.soft_reset(SIM_ST_BADQACC);
     store_state(S, st, n, e);
+    if (AP) zero_applied(st.qfrc_applied, Sim<NA, NF>::NV, n, e);
     ncon = forward<NA, NF, true>(S, nullptr, nullptr, nullptr, n, e, L, cr);
   }
   PSTAMP(10);
@@ -513,7 +533,24 @@ __global__ __launch_bounds__(64) void k_reset(const DModel* __restrict__ dm, int
   S.kinematics();
   store_state(S, st, n, e);
   if (st.ncon) st.ncon[e] = 0.f;
+  if (st.qfrc_applied) zero_applied(st.qfrc_applied, NV, n, e);
   if (obs) write_obs(S, obs, e);
+}
+
+// qfrc_bias at the current state (mj_comVel + mj_rne with flg_acc = 0, as left by mj_forward)
+template <int NA, int NF>
+__global__ __launch_bounds__(64) void k_bias(const DModel* __restrict__ dm, int n, sim_state st,
+                                             float* __restrict__ bias, sim_params pp) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  Sim<NA, NF> S(dm, pp.mass_scale ? pp.mass_scale[e] : 1.f, pp.friction ? pp.friction[e] : -1.f,
+                pp.damping_scale ? pp.damping_scale[e] : 1.f);
+  load_state(S, st, n, e);
+  S.kinematics();
+  S.com_crb();
+  S.template smooth_forces<true>();
+#pragma unroll
+  for (int i = 0; i < Sim<NA, NF>::NV; i++) soa(bias, i, n, e) = -S.fsmooth[i];
 }
 
 template <int NA, int NF>
@@ -1109,8 +1146,12 @@ int sim_step(sim_batch* b, const sim_state* s, const float* action, int frame_sk
     dispatch_nf(b->model->nf, [&](auto nfc) {
       constexpr int NA = 6, NF = decltype(nfc)::value;
       prof_mark(b, 0, st);
-      hipLaunchKernelGGL((k_step<NA, NF>), grid_for(b->n), dim3(64), 0, st, b->d_model, b->n,
-                         frame_skip, *s, action, obs, b->params);
+      if (s->qfrc_applied)
+        hipLaunchKernelGGL((k_step<NA, NF, true>), grid_for(b->n), dim3(64), 0, st, b->d_model, b->n,
+                           frame_skip, *s, action, obs, b->params);
+      else
+        hipLaunchKernelGGL((k_step<NA, NF, false>), grid_for(b->n), dim3(64), 0, st, b->d_model, b->n,
+                           frame_skip, *s, action, obs, b->params);
       prof_mark(b, -1, st);
     });
     HIPCHECK(hipGetLastError());
@@ -1134,7 +1175,8 @@ int sim_step(sim_batch* b, const sim_state* s, const float* action, int frame_sk
         }
         const bool last = sub == frame_skip - 1;
         prof_mark(b, 2, q);
-        hipLaunchKernelGGL((k_substep<NA, NF>), dim3((b->n + 64 / lpe<NF>() - 1) / (64 / lpe<NF>())), dim3(64), 0, q,
+        auto kern = s->qfrc_applied ? k_substep<NA, NF, true> : k_substep<NA, NF, false>;
+        hipLaunchKernelGGL(kern, dim3((b->n + 64 / lpe<NF>() - 1) / (64 / lpe<NF>())), dim3(64), 0, q,
                            b->d_model, b->n, *s,
                            sub == 0 ? action : nullptr, last ? obs : nullptr, b->params, b->d_scratch,
                            b->d_cbuf, np > 0 ? b->d_ccount : nullptr, np > 0 ? b->d_pmask : nullptr,
@@ -1261,6 +1303,19 @@ int sim_phase_profile(double* out, int reset) {
 
 int sim_substeps(sim_batch* b, const sim_state* s, int nsub, void* stream) {
   return sim_step(b, s, nullptr, nsub, nullptr, stream);
+}
+
+int sim_bias(sim_batch* b, const sim_state* s, float* qfrc_bias, void* stream) {
+  if (int rc = check_state(b, s)) return rc;
+  if (!qfrc_bias) return fail(SIM_E_ARG, "qfrc_bias is null");
+  hipStream_t st = (hipStream_t)stream;
+  dispatch_nf(b->model->nf, [&](auto nfc) {
+    constexpr int NA = 6, NF = decltype(nfc)::value;
+    hipLaunchKernelGGL((k_bias<NA, NF>), grid_for(b->n), dim3(64), 0, st, b->d_model, b->n, *s, qfrc_bias,
+                       b->params);
+  });
+  HIPCHECK(hipGetLastError());
+  return SIM_OK;
 }
 
 int sim_observe(sim_batch* b, const sim_state* s, float* obs, void* stream) {

@@ -208,6 +208,8 @@ struct Sim {
   }
 
   // ------------------------------- mj_comVel + mj_rne(flg_acc=0) + passive + actuation
+  // RNE_ONLY: fsmooth = -qfrc_bias (gravity + Coriolis/centrifugal), no passive/actuation
+  template <bool RNE_ONLY = false>
   DEVI void smooth_forces() {
     const DModel& m = *mp;
     // arm chain
@@ -265,6 +267,7 @@ struct Sim {
 #pragma unroll
       for (int k = 0; k < 6; k++) fsmooth[d0 + k] = -dot6(cdof[d0 + k], fb);
     }
+    if constexpr (RNE_ONLY) return;
     // passive damping + actuators (actuator a -> dof a)
 #pragma unroll
     for (int i = 0; i < NV; i++) fsmooth[i] -= m.dof_damping[i] * dscale * qvel[i];
@@ -280,6 +283,12 @@ struct Sim {
         force = fminf(fmaxf(force, m.act_forcerange[a][0]), m.act_forcerange[a][1]);
       fsmooth[a] += g * force;
     }
+  }
+
+  // qfrc_smooth += qfrc_applied ([nv][N] SoA, caller-owned)
+  DEVI void add_applied(const float* applied, int n, int e) {
+#pragma unroll
+    for (int i = 0; i < NV; i++) fsmooth[i] += soa(applied, i, n, e);
   }
 
   // ---------------------------------------------------------- Euler integration

@@ -118,9 +118,23 @@ class BatchSim:
         self.status = torch.zeros(self.n, dtype=torch.int32, device=self.device)
         self.ncon = torch.zeros(self.n, **f32)
         self.obs = torch.zeros((self.n, self.obs_dim), **f32)
-        self._state = abi.SimState(_ptr(self.qpos), _ptr(self.qvel), _ptr(self.qacc_warmstart),
-                                   _ptr(self.ctrl), _ptr(self.status), _ptr(self.ncon))
+        self.qfrc_applied = None  # [nv, n] once enable_qfrc_applied() is called
+        self._bind_state()
         self._params = None
+
+    def _bind_state(self):
+        self._state = abi.SimState(_ptr(self.qpos), _ptr(self.qvel), _ptr(self.qacc_warmstart),
+                                   _ptr(self.ctrl), _ptr(self.status), _ptr(self.ncon),
+                                   _ptr(self.qfrc_applied))
+
+    def enable_qfrc_applied(self):
+        """Allocate ``qfrc_applied`` [nv, n] (zeros; MjData.qfrc_applied): from now on every
+        substep adds it to the smooth forces, and a reset / soft reset zeroes the env's row
+        (``mj_resetData``).  ``Koopman_MPC.py:119`` writes it every frame."""
+        if self.qfrc_applied is None:
+            self.qfrc_applied = self.torch.zeros((self.nv, self.n), dtype=self.torch.float32, device=self.device)
+            self._bind_state()
+        return self.qfrc_applied
 
     # ------------------------------------------------------------------ utils
     def _stream(self):
@@ -185,6 +199,14 @@ class BatchSim:
     def substeps(self, nsub):
         abi.check(self.lib, self.lib.sim_substeps(self._batch, C.byref(self._state), int(nsub),
                                                   self._stream()))
+
+    def bias(self, out=None):
+        """qfrc_bias [nv, n] at the current state (gravity + Coriolis/centrifugal with the
+        current qvel), what ``mj_forward`` leaves in ``d.qfrc_bias`` (``Koopman_MPC.py:119,126``)."""
+        if out is None:
+            out = self.torch.empty((self.nv, self.n), dtype=self.torch.float32, device=self.device)
+        abi.check(self.lib, self.lib.sim_bias(self._batch, C.byref(self._state), _ptr(out), self._stream()))
+        return out
 
     def observe(self):
         abi.check(self.lib, self.lib.sim_observe(self._batch, C.byref(self._state), _ptr(self.obs),

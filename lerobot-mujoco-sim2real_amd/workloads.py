@@ -20,6 +20,11 @@ batch runs on 1 or 8 GPUs.
   env-step runs position-only DLS IK (warm-started) and applies
   ``clip((q* - q) / dt, +-max_speed)`` (``SOARM101_Env.py:57``); rows
   ``[u(5) | ee(3) | q(5)]`` as in ``SOARM101_DataCollection.py:106-134``.
+* ``mpc``: the reference's Koopman-MPC tracking loop
+  (``Koopman_MPC.py:110-136,197-222``) for every env: a Fig8 reference per env (per-env phase)
+  with joint angles from warm-started DLS IK (``control/TrajectoryGenerator.py:180-205``), a
+  random-init DKUC Koopman model (``models/KoopmanBase.py``), delta-MPC with H = 10, gravity
+  compensation ``qfrc_applied = qfrc_bias``.
 """
 import numpy as np
 
@@ -36,6 +41,9 @@ CONFIGS = {
     "rollout": dict(xml=SCENE_XML, disable_contact=False, action="ik_fig8", dr=False,
                     desc="SOARM101_DataCollection rollout: batched DLS-IK actions toward Fig8 targets, "
                          "rows [T+1, N, 13] on device, gathered to rank 0 (config 5)"),
+    "mpc": dict(xml=SCENE_XML, disable_contact=False, action="koopman_mpc", dr=False,
+                desc="Koopman-MPC Fig8 tracking (Koopman_MPC.py loop, SURVEY 8f rank 2): per env and frame "
+                     "gravity compensation + f64 MFMA encoder/MPC + env step, 4096 envs"),
 }
 
 
@@ -106,3 +114,23 @@ def fig8_targets(t, phase, lib=np):
 def ik_action(qstar, q, dt=0.02, max_speed=0.5, lib=np):
     """action = clip((q* - q) / dt, +-max_speed) over the 5 arm joints."""
     return lib.clip((qstar - q) / dt, -max_speed, max_speed)
+
+
+def reference_trajectory(sim, phase, T, lib=None):
+    """Per-env Fig8 reference [T, n, 3] and its joint angles [T, n, 5] by warm-started DLS IK,
+    repeating the previous solution where a point fails (control/TrajectoryGenerator.py:180-205).
+    phase: [n] device tensor; runs on sim's device."""
+    import torch
+    q = sim.qpos.clone()
+    cart, joints = [], []
+    prev = q[:5].clone()
+    for t in range(T):
+        tgt = fig8_targets(float(t) - 1.0, phase, lib=torch)  # parameter 1.6 + 0.02 t + phase
+        last = q.clone()
+        qn, ok, _ = sim.ik(tgt, q=q)  # warm start, updated in place
+        good = ok.bool()
+        q = torch.where(good[None], qn, last)
+        prev = torch.where(good[None], q[:5], prev)
+        cart.append(tgt.float())
+        joints.append(prev.T.clone())
+    return torch.stack(cart), torch.stack(joints)

@@ -700,7 +700,7 @@ void orc_forward(const orc_model* om, orc_data* d) {
   orc_passive_actuation(om, d);
   orc_rne(om, d);
   for (int i = 0; i < nv; i++)
-    d->qfrc_smooth[i] = d->qfrc_passive[i] - d->qfrc_bias[i] + d->qfrc_actuator[i];
+    d->qfrc_smooth[i] = d->qfrc_passive[i] - d->qfrc_bias[i] + d->qfrc_actuator[i] + d->qfrc_applied[i];
   orc_solve_m(om, d, d->qacc_smooth, d->qfrc_smooth);
   orc_make_constraint(om, d);
   if (d->nefc) {
@@ -848,7 +848,8 @@ void orc_batch_reset(const sim_model_desc* m, int n, double* qpos, double* qvel,
 void orc_batch_step(const sim_model_desc* m, const float* hv, const int32_t* hadr,
                     const int32_t* hadj, int n, double* qpos, double* qvel, double* warm,
                     double* ctrl, const double* action, int nsub, double* obs, int32_t* status,
-                    double* ncon_sum, const double* params, int nthreads, double* flops) {
+                    double* ncon_sum, const double* params, int nthreads, double* flops,
+                    double* applied) {
   double fl_total = 0, cf_total = 0;
   int32_t seeds[SIM_MAXGEOM * ORC_NSEED];
   if (hv) orc_hull_seeds(m, hv, seeds);
@@ -871,6 +872,8 @@ void orc_batch_step(const sim_model_desc* m, const float* hv, const int32_t* had
     if (action)
       for (int i = 0; i < m->nact; i++) d.ctrl[i] = action[e * m->nact + i];
     d.status = status ? status[e] : 0;
+    if (applied)
+      for (int i = 0; i < m->nv; i++) d.qfrc_applied[i] = applied[e * m->nv + i];
     double nc = 0;
     for (int s = 0; s < nsub; s++) {
       orc_step(&om, &d);
@@ -883,6 +886,8 @@ void orc_batch_step(const sim_model_desc* m, const float* hv, const int32_t* had
     }
     for (int i = 0; i < m->nu; i++) ctrl[e * m->nu + i] = d.ctrl[i];
     if (status) status[e] = d.status;
+    if (applied)
+      for (int i = 0; i < m->nv; i++) applied[e * m->nv + i] = d.qfrc_applied[i];
     if (ncon_sum) ncon_sum[e] += nc;
     if (obs) write_obs(m, &d, obs + e * (3 + m->obs_nq));
     fl_total += d.flops;
@@ -892,6 +897,25 @@ void orc_batch_step(const sim_model_desc* m, const float* hv, const int32_t* had
   if (flops) {
     flops[0] = fl_total; /* total */
     flops[1] = cf_total; /* of which collision */
+  }
+}
+
+/* Koopman_MPC.py:119 reads d.qfrc_bias as left by mj_forward (Koopman_MPC.py:126) */
+void orc_batch_bias(const sim_model_desc* m, int n, const double* qpos, const double* qvel,
+                    const double* params, double* bias) {
+  for (int e = 0; e < n; e++) {
+    orc_model om;
+    make_om(&om, m, NULL, NULL, NULL, params ? params + 3 * e : NULL);
+    orc_data d;
+    orc_reset_data(&om, &d);
+    for (int i = 0; i < m->nq; i++) d.qpos[i] = qpos[e * m->nq + i];
+    for (int i = 0; i < m->nv; i++) d.qvel[i] = qvel[e * m->nv + i];
+    orc_kinematics(&om, &d);
+    orc_com_pos(&om, &d);
+    orc_crb(&om, &d);
+    orc_com_vel(&om, &d);
+    orc_rne(&om, &d);
+    for (int i = 0; i < m->nv; i++) bias[e * m->nv + i] = d.qfrc_bias[i];
   }
 }
 

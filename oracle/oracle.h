@@ -66,6 +66,7 @@ typedef struct orc_data {
   double cvel[SIM_MAXBODY][6], cdof_dot[SIM_MAXDOF][6];
   double qfrc_bias[SIM_MAXDOF], qfrc_passive[SIM_MAXDOF], qfrc_actuator[SIM_MAXDOF];
   double qfrc_smooth[SIM_MAXDOF], qacc_smooth[SIM_MAXDOF], qfrc_constraint[SIM_MAXDOF];
+  double qfrc_applied[SIM_MAXDOF]; /* user input (mjData.qfrc_applied), zeroed by a reset */
   double actuator_force[SIM_MAXU];
   /* contacts & constraints */
   int ncon;
@@ -125,7 +126,11 @@ void orc_batch_reset(const sim_model_desc* m, int n, double* qpos, double* qvel,
 void orc_batch_step(const sim_model_desc* m, const float* hv, const int32_t* hadr,
                     const int32_t* hadj, int n, double* qpos, double* qvel, double* warm,
                     double* ctrl, const double* action, int nsub, double* obs, int32_t* status,
-                    double* ncon_sum, const double* params, int nthreads, double* flops);
+                    double* ncon_sum, const double* params, int nthreads, double* flops,
+                    double* applied /* [n][nv] qfrc_applied in/out (zeroed by a soft reset) or NULL */);
+/* qfrc_bias (mj_forward: comVel + RNE with qvel, flg_acc = 0) at n states: bias [n][nv] */
+void orc_batch_bias(const sim_model_desc* m, int n, const double* qpos, const double* qvel,
+                    const double* params, double* bias);
 /* full diagnostic forward at a state: writes M[nv*nv], bias[nv], qacc[nv],
    ncon, contacts [ncon][14] = dist,pos3,frame9,geom1? (dist,pos,normal,g1,g2) */
 int orc_debug_forward(const sim_model_desc* m, const float* hv, const int32_t* hadr,

@@ -38,7 +38,9 @@ def lib():
         L.orc_batch_reset.argtypes = [vp, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp]
         L.orc_batch_reset.restype = None
         L.orc_batch_step.argtypes = [vp, vp, vp, vp, C.c_int, vp, vp, vp, vp, vp, C.c_int, vp, vp,
-                                     vp, vp, C.c_int, vp]
+                                     vp, vp, C.c_int, vp, vp]
+        L.orc_batch_bias.argtypes = [vp, C.c_int, vp, vp, vp, vp]
+        L.orc_batch_bias.restype = None
         L.orc_batch_step.restype = None
         L.orc_debug_forward.argtypes = [vp] * 4 + [vp] * 4 + [vp] * 8
         L.orc_debug_forward.restype = C.c_int
@@ -86,7 +88,8 @@ class Oracle:
         st["ncon"][:] = 0
         return obs
 
-    def step(self, st, action=None, nsub=10, params=None, nthreads=1):
+    def step(self, st, action=None, nsub=10, params=None, nthreads=1, applied=None):
+        """applied: [n, nv] qfrc_applied (float64, modified in place: a soft reset zeroes its row)."""
         n = st["qpos"].shape[0]
         d = self.desc
         obs = np.zeros((n, 3 + d.obs_nq))
@@ -96,10 +99,19 @@ class Oracle:
         lib().orc_batch_step(self._desc_p, _p(self.hv), _p(self.hadr), _p(self.hadj), n,
                              _p(st["qpos"]), _p(st["qvel"]), _p(st["warm"]), _p(st["ctrl"]), _p(a),
                              nsub, _p(obs), _p(st["status"]), _p(st["ncon"]), _p(pr), nthreads,
-                             _p(fl))
+                             _p(fl), _p(applied))
         self.last_flops = float(fl[0])
         self.last_collision_flops = float(fl[1])
         return obs
+
+    def bias(self, st, params=None):
+        """qfrc_bias [n, nv] at the states of `st` (gravity + Coriolis, as mj_forward leaves it)."""
+        n = st["qpos"].shape[0]
+        out = np.zeros((n, self.desc.nv))
+        pr = None if params is None else np.ascontiguousarray(params, np.float64)
+        lib().orc_batch_bias(self._desc_p, n, _p(np.ascontiguousarray(st["qpos"])),
+                             _p(np.ascontiguousarray(st["qvel"])), _p(pr), _p(out))
+        return out
 
     def forward(self, qpos, qvel=None, ctrl=None, warm=None):
         d = self.desc

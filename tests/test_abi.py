@@ -13,7 +13,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def header_functions():
-    src = open(os.path.join(ROOT, "include", "soarm_sim.h")).read()
+    src = "".join(open(os.path.join(ROOT, "include", h)).read() for h in ("soarm_sim.h", "koopman_mpc.h"))
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(sim_\w+)\s*\(", src, flags=re.M)))
 

@@ -1,0 +1,264 @@
+"""Batched Koopman-MPC (include/koopman_mpc.h) against the float64 oracle.
+
+The reference solves the MPC with casadi/IPOPT (absent here; running the reference is denied,
+SURVEY.md §8c), so the oracle (oracle/koopman_mpc.py) restates the reference's cost loop and
+minimises it exactly; these tests first pin that minimiser (zero gradient and positive curvature
+of the literal cost), then hold the product to it:
+
+* host gains (control/koopman.condensed_gains, a different construction) == oracle minimiser, 1e-9;
+* GPU encoder (f64 MFMA) == numpy float64 MLP, 1e-12 relative;
+* GPU control step (encoder + feedforward + gains) == oracle get_control, 1e-9 absolute;
+* qfrc_bias / qfrc_applied in the physics == the oracle's, fp32 tolerances as test_gpu_parity;
+* the batched tracking loop: every frame's action == the oracle MPC on the GPU's own state.
+
+Weights are random (the reference's checkpoint is not used: DESIGN.md §9 records why), drawn with
+the reference's initialisers (control/koopman.py).
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import koopman_mpc as KO
+from oracle import Oracle
+
+RNG = np.random.default_rng(11)
+LAYERS = [8, 64, 64, 64, 64, 24]
+
+
+class _Args:
+    x_dim, u_dim, model, layers = 8, 5, "DKUC", LAYERS
+
+    def __init__(self, kind="delta_mpc"):
+        self.MPC_type = kind
+
+
+def make_net(seed=0):
+    import torch
+    from lerobot_mujoco_sim2real_amd.control.koopman import Koopmanlinear
+    torch.manual_seed(seed)
+    return Koopmanlinear(8, 5, LAYERS).double()
+
+
+def net_mats(net):
+    return (net.lA.weight.detach().numpy().astype(np.float64), net.lB.weight.detach().numpy().astype(np.float64),
+            net.encoder_layers())
+
+
+def sample_states(n):
+    """[n, 8] plausible SO-ARM101 states: ee xyz, 5 joint angles."""
+    return np.concatenate([RNG.uniform([0.1, -0.2, 0.0], [0.45, 0.2, 0.35], (n, 3)),
+                           RNG.uniform(-1.0, 1.0, (n, 5))], 1)
+
+
+# ------------------------------------------------------------------ CPU: oracle + host
+@pytest.mark.parametrize("kind", ["delta_mpc", "mpc"])
+def test_oracle_minimises_the_reference_cost(kind):
+    """The oracle's solution is the minimiser of the reference's cost loop
+    (control/MPC_Controler.py:80-86 / :115-127): gradient 0, every perturbation costs more."""
+    net = make_net(1)
+    A, B, layers = net_mats(net)
+    H, nz = 10, 32
+    z0 = KO.encode(layers, sample_states(1))[0]
+    ref = KO.encode(layers, sample_states(H))
+    up = RNG.uniform(-0.5, 0.5, 5)
+    v = KO.solve(A, B, z0[None], ref[None], up[None], kind)[0].ravel()
+    J0 = KO.cost(A, B, v, z0, ref, up, kind)
+    h = 1e-6
+    g = np.array([(KO.cost(A, B, v + h * e, z0, ref, up, kind) - KO.cost(A, B, v - h * e, z0, ref, up, kind)) / (2 * h)
+                  for e in np.eye(v.size)])
+    scale = max(1.0, abs(J0))
+    assert np.abs(g).max() < 1e-5 * scale
+    for _ in range(20):
+        d = RNG.normal(0, 1e-3, v.size)
+        assert KO.cost(A, B, v + d, z0, ref, up, kind) > J0
+
+
+def test_oracle_encoder_matches_torch():
+    """x_encoder = cat([x, MLP(x)]) (models/KoopmanBase.py:45-47) in float64."""
+    import torch
+    net = make_net(2)
+    x = sample_states(257)
+    want = net.x_encoder(torch.as_tensor(x)).detach().numpy()
+    got = KO.encode(net.encoder_layers(), x)
+    np.testing.assert_allclose(got, want, rtol=1e-13, atol=1e-13)
+
+
+@pytest.mark.parametrize("kind", ["delta_mpc", "mpc"])
+def test_condensed_gains_equal_oracle_minimiser(kind):
+    """u0 = Gr r + Gz z0 + Gu u_prev (host closed form) == oracle get_control u0."""
+    from lerobot_mujoco_sim2real_amd.control.koopman import condensed_gains
+    net = make_net(3)
+    A, B, layers = net_mats(net)
+    n, H = 64, 10
+    z0 = KO.encode(layers, sample_states(n))
+    ref = KO.encode(layers, sample_states(n * H)).reshape(n, H, -1)
+    up = RNG.uniform(-0.5, 0.5, (n, 5))
+    Gr, Gz, Gu = condensed_gains(A, B, H, kind)
+    u0 = ref.reshape(n, -1) @ Gr.T + z0 @ Gz.T + up @ Gu.T
+    want, _ = KO.get_control(A, B, z0, ref, up, kind)
+    np.testing.assert_allclose(u0, want, rtol=1e-9, atol=1e-9)
+
+
+def test_koopman_create_validates_before_device():
+    """Bad shapes -> SIM_E_MODEL; a good controller without a GPU -> SIM_E_NODEVICE (no CPU path)."""
+    from lerobot_mujoco_sim2real_amd import abi, build
+    build.build()
+    lib = abi.load_lib()
+    d = abi.KoopmanDesc()
+    d.x_dim, d.u_dim, d.nlayer, d.horizon, d.u_clip = 8, 5, 5, 10, 0.5
+    for i, w in enumerate(LAYERS):
+        d.width[i] = w
+    w = np.zeros(100000)
+    g = np.zeros(5 * (10 * 32 + 32 + 5))
+    h = C.c_void_p()
+    d.width[2] = 65
+    assert lib.sim_koopman_create(C.byref(d), w.ctypes.data_as(C.c_void_p), g.ctypes.data_as(C.c_void_p), 0,
+                                  C.byref(h)) == -2
+    d.width[2] = 64
+    d.horizon = 40
+    assert lib.sim_koopman_create(C.byref(d), w.ctypes.data_as(C.c_void_p), g.ctypes.data_as(C.c_void_p), 0,
+                                  C.byref(h)) == -2
+    d.horizon = 10
+    import torch
+    if not torch.cuda.is_available():
+        rc = lib.sim_koopman_create(C.byref(d), w.ctypes.data_as(C.c_void_p), g.ctypes.data_as(C.c_void_p), 0,
+                                    C.byref(h))
+        assert rc == -4 and b"no HIP device" in lib.sim_last_error()
+
+
+# ------------------------------------------------------------------------- GPU
+def _ctl(net, kind="delta_mpc"):
+    from lerobot_mujoco_sim2real_amd.control.MPC_Controler import MPCController
+    return MPCController(net, _Args(kind))
+
+
+@pytest.mark.gpu
+def test_encode_gpu(gpu_lib):
+    net = make_net(4)
+    ctl = _ctl(net)
+    x = sample_states(1000).astype(np.float32)
+    z = ctl.encode(x).cpu().numpy().T
+    want = KO.encode(net.encoder_layers(), x.astype(np.float64))
+    np.testing.assert_allclose(z, want, rtol=1e-12, atol=1e-13)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["delta_mpc", "mpc"])
+def test_control_step_gpu(gpu_lib, kind):
+    """lift refs -> feedforward -> mpc_step(x) on the GPU == oracle get_control, for every frame
+    of a short reference, including the zero-padded tail windows (Koopman_MPC.py:199-205)."""
+    import torch
+    net = make_net(5)
+    ctl = _ctl(net, kind)
+    A, B, layers = net_mats(net)
+    T, n, H = 14, 300, 10
+    sref = sample_states(T * n).reshape(T, n, 8).astype(np.float32)
+    zref_dev = ctl.lift_reference(torch.as_tensor(sref, device=ctl.device))
+    ff = ctl.feedforward(zref_dev)
+    zref = KO.encode(layers, sref.reshape(T * n, 8).astype(np.float64)).reshape(T, n, -1)
+    np.testing.assert_allclose(zref_dev.permute(0, 2, 1).cpu().numpy(), zref, rtol=1e-12, atol=1e-13)
+    up0 = RNG.uniform(-0.6, 0.6, (n, 5))
+    for k in (0, 5, T - 3, T - 1):
+        x = sample_states(n).astype(np.float32)
+        up = torch.as_tensor(up0.T.copy(), device=ctl.device)
+        a = ctl.step(torch.as_tensor(x, device=ctl.device), ff[k], up).cpu().numpy()
+        u0, aw = KO.get_control(A, B, KO.encode(layers, x.astype(np.float64)), KO.lifted_window(zref, k, H), up0, kind)
+        np.testing.assert_allclose(up.cpu().numpy().T, u0, rtol=1e-9, atol=1e-9)
+        np.testing.assert_allclose(a, aw.astype(np.float32), atol=1e-6)
+        assert (np.abs(a) <= 0.5).all()
+
+
+@pytest.mark.gpu
+def test_get_control_single_env(gpu_lib):
+    """MPCController.get_control(p) with the reference's p layout (Koopman_MPC.py:199-213)."""
+    net = make_net(6)
+    ctl = _ctl(net)
+    A, B, layers = net_mats(net)
+    ref = KO.encode(layers, sample_states(10))
+    z0 = KO.encode(layers, sample_states(1))[0]
+    ctl.u_prev = RNG.uniform(-0.3, 0.3, 5)
+    p = np.concatenate([ref.ravel(), z0, ctl.u_prev]).reshape(-1, 1)
+    u0, a = ctl.get_control(p)
+    w0, wa = KO.get_control(A, B, z0[None], ref[None], p[-5:, 0][None])
+    np.testing.assert_allclose(u0, w0[0], rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(a, wa[0], atol=1e-12)
+    np.testing.assert_allclose(ctl.u_prev, wa[0])  # delta_mpc keeps a (MPC_Controler.py:150-151)
+    psi = ctl.Psi_o(sample_states(1))
+    assert psi.shape == (32, 1)
+
+
+@pytest.mark.gpu
+def test_bias_matches_oracle(gpu_lib, arm_model, cube_model):
+    from test_gpu_parity import load_state, random_states, to_np, make_sim
+    for cm in (arm_model, cube_model):
+        n = 256
+        S, orc = make_sim(cm, n), Oracle(cm)
+        st = random_states(cm, orc, n)
+        if cm.nq > 6:  # the free cube spinning: Coriolis terms on the free body too
+            st["qvel"][:, 6:] = RNG.uniform(-1, 1, (n, 6))
+        load_state(S, st)
+        b = to_np(S.bias()).T
+        want = orc.bias(st)
+        np.testing.assert_allclose(b, want, atol=2e-5, rtol=1e-4)
+
+
+@pytest.mark.gpu
+def test_step_with_applied_force(gpu_lib, arm_model_nocontact, arm_model):
+    """qfrc_applied enters the smooth forces of every substep; a reset zeroes it."""
+    import torch
+    from test_gpu_parity import load_state, random_states, to_np, make_sim
+    for cm in (arm_model_nocontact, arm_model):
+        n = 512
+        S, orc = make_sim(cm, n), Oracle(cm)
+        st = random_states(cm, orc, n)
+        load_state(S, st)
+        app = RNG.uniform(-0.5, 0.5, (n, cm.nv))
+        S.enable_qfrc_applied().copy_(torch.as_tensor(app.T, dtype=torch.float32, device=S.device))
+        a = RNG.uniform(-0.5, 0.5, (n, 5)).astype(np.float32)
+        og = to_np(S.step(a))
+        app64 = app.astype(np.float32).astype(np.float64)
+        oc = orc.step(st, a.astype(np.float64), applied=app64)
+        err = np.abs(og - oc)
+        assert np.median(err) < 1e-6 and err.max() < 5e-4, (np.median(err), err.max())
+        S.reset(init_qpos=np.zeros((n, 5), np.float32))
+        assert float(S.qfrc_applied.abs().max()) == 0.0
+
+
+@pytest.mark.gpu
+def test_tracking_loop_matches_oracle(gpu_lib, arm_model):
+    """KoopmanMPCTracking: frame by frame, the GPU's action equals the oracle MPC applied to the
+    GPU's own state and u_prev (1e-6, the action is float32), and the GPU's next state equals one
+    oracle env-step with qfrc_applied = qfrc_bias from that state (fp32 step tolerances)."""
+    import torch
+    from lerobot_mujoco_sim2real_amd.Koopman_MPC import KoopmanMPCTracking
+    net = make_net(7)
+    ctl = _ctl(net)
+    A, B, layers = net_mats(net)
+    T, n = 30, 64
+    t = np.linspace(0, 2 * np.pi, T)
+    phase = RNG.uniform(0, 2 * np.pi, n)
+    cart = np.stack([0.3 + 0.0 * t[:, None] + 0 * phase, 0.1 * np.cos(t[:, None] + phase),
+                     0.15 + 0.05 * np.sin(t[:, None] + phase)], -1)
+    jq = RNG.uniform(-0.3, 0.3, (1, n, 5)) + 0.1 * np.sin(t[:, None, None] + phase[None, :, None])
+    run = KoopmanMPCTracking(ctl, arm_model, cart, jq)
+    sref = run.state_all_ref.cpu().numpy().astype(np.float64)
+    zref = KO.encode(layers, sref.reshape(T * n, 8)).reshape(T, n, -1)
+    orc = Oracle(arm_model)
+    run.runBefore()
+    for k in range(T):
+        x = run.state.cpu().numpy().astype(np.float64)
+        up = run.u_prev.cpu().numpy().T.copy()
+        c64 = lambda t: np.ascontiguousarray(t.cpu().numpy().T, dtype=np.float64)  # oracle: C order
+        st = {"qpos": c64(run.sim.qpos), "qvel": c64(run.sim.qvel), "warm": c64(run.sim.qacc_warmstart),
+              "ctrl": c64(run.sim.ctrl),
+              "status": run.sim.status.cpu().numpy().copy(), "ncon": np.zeros(n)}
+        obs = run.runFunc().cpu().numpy()
+        u0, aw = KO.get_control(A, B, KO.encode(layers, x), KO.lifted_window(zref, k, 10), up)
+        np.testing.assert_allclose(run.action.cpu().numpy(), aw.astype(np.float32), atol=1e-6)
+        np.testing.assert_allclose(run.u_prev.cpu().numpy().T, u0, rtol=1e-9, atol=1e-9)
+        applied = orc.bias(st)
+        oc = orc.step(st, run.action.cpu().numpy().astype(np.float64), applied=applied)
+        err = np.abs(obs - oc)
+        assert np.median(err) < 2e-6 and err.max() < 1e-3, (k, np.median(err), err.max())
+    assert int(run.sim.status.abs().sum()) == 0

@@ -27,9 +27,23 @@ def state_bytes(cm, dr):
     return b + (4 * 3 if dr else 0)
 
 
+def mpc_net(seed=0):
+    """The bench's random-init DKUC model (bench.py: torch.manual_seed(seed))."""
+    import torch
+    from lerobot_mujoco_sim2real_amd.control.koopman import Koopmanlinear
+    from lerobot_mujoco_sim2real_amd.args import Args
+    torch.manual_seed(seed)
+    a = Args()
+    return Koopmanlinear(a.x_dim, a.u_dim, a.layers).double()
+
+
 def main():
-    out = {}
+    only = sys.argv[1:]
+    path = os.path.join(ROOT, "profiles", "algorithmic_cost.json")
+    out = json.load(open(path)) if only else {}
     for name, c in W.CONFIGS.items():
+        if only and name not in only:
+            continue
         cm = W.model(name)
         orc = Oracle(cm)
         ids = np.arange(N)
@@ -44,7 +58,24 @@ def main():
         rng = np.random.default_rng(0)
         tot = col = 0.0
         phase, qstar = W.ik_phase(ids), q.astype(np.float64)
+        if c["action"] == "koopman_mpc":  # the tracking loop: physics with qfrc_applied = qfrc_bias
+            import koopman_mpc as KO
+            net = mpc_net()
+            A, B = net.lA.weight.detach().numpy(), net.lB.weight.detach().numpy()
+            layers = net.encoder_layers()
+            cart = np.stack([W.fig8_targets(t - 1.0, phase) for t in range(T)])
+            sref = np.concatenate([cart, np.repeat(q[None, :, :5], T, 0)], -1)  # joint refs: start pose
+            zref = KO.encode(layers, sref.reshape(T * N, 8)).reshape(T, N, -1)
+            x, up = sref[0], np.zeros((N, 5))
         for t in range(T):
+            if c["action"] == "koopman_mpc":
+                u0, a = KO.get_control(A, B, KO.encode(layers, x), KO.lifted_window(zref, t, 10), up)
+                up = u0
+                obs = orc.step(st, a, nthreads=8, applied=orc.bias(st))
+                x = obs.astype(np.float32).astype(np.float64)
+                tot += orc.last_flops
+                col += orc.last_collision_flops
+                continue
             if c["action"] == "chirp":
                 a = W.chirp_action(tab, t)
             elif c["action"] == "ik_fig8":  # IK flops are not counted: physics only
@@ -66,8 +97,14 @@ def main():
             hbm_bytes_per_env_step=state_bytes(cm, c["dr"]),
             sample=f"{N} envs x {T} env-steps, oracle float64, seed 0",
         )
+        if c["action"] == "koopman_mpc":
+            # per env and frame: encoder 2 sum(in*out) + control 2 u (nz + u), counted from the widths
+            ws = [l[0].shape for l in layers]
+            enc = 2.0 * sum(o * i for o, i in ws)
+            out[name]["mpc_flops_per_env_step"] = enc + 2.0 * 5 * (32 + 5)
+            out[name]["mpc_note"] = ("encoder + [Gz|Gu] per env-step (f64 MFMA, k_mpc_step); the physics "
+                                     "share above is the arm scene with gravity compensation")
         print(name, json.dumps(out[name]))
-    path = os.path.join(ROOT, "profiles", "algorithmic_cost.json")
     json.dump(out, open(path, "w"), indent=1)
     print("wrote", path)
 
