@@ -55,11 +55,15 @@ DEVI void load_pose(const float* __restrict__ gpose, int n, int e, int g, GeomPo
   for (int k = 0; k < 9; k++) o.R[k] = soa(gpose, g * 12 + 3 + k, n, e);
 }
 
-// contacts of one candidate pair (<= 4: box-box / plane-box corners; 1 otherwise)
+// contacts of one candidate pair (<= 4: box-box / plane-box corners; 1 otherwise), written
+// straight to the pair's slots of the contact buffer cbuf [slot*7 + f][env]: f = dist, pos(3),
+// normal(3) geom1 -> geom2.  (A register array indexed by the running count ends up in
+// scratch memory: the count differs per lane.)
 constexpr int PAIR_MAXCON = 4;
 struct PairOut {
-  int n;
-  float c[PAIR_MAXCON][7];  // dist, pos(3), normal(3) geom1 -> geom2
+  float* cbuf;
+  int nenv, e, s0, cap;  // env count / env, first slot and slot count of the pair
+  int n;                 // contacts written
 };
 
 // hill-climbing support on a mesh hull; returns the local vertex.  Opens at the cube-map
@@ -197,20 +201,25 @@ DEVI bool reach_tol(const MSup p[4], const MSup& v4, const float d[3]) {
   const float mn = fminf(fminf(d4 - dot3(p[1].v, d), d4 - dot3(p[2].v, d)), d4 - dot3(p[3].v, d));
   return mn <= MPR_TOLF;
 }
+// dst = c ? src : dst, element by element (v_cndmask): a branchy `p[i] = v4` lets the
+// compiler sink the stores into one store through a computed index, which puts the whole
+// portal in scratch memory
+DEVI void sel(MSup& dst, bool c, const MSup& src) {
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    dst.v[k] = c ? src.v[k] : dst.v[k];
+    dst.v1[k] = c ? src.v1[k] : dst.v1[k];
+    dst.v2[k] = c ? src.v2[k] : dst.v2[k];
+  }
+}
 DEVI void expand(MSup p[4], const MSup& v4) {
   float x[3];
   cross(x, v4.v, p[0].v);
-  if (dot3(p[1].v, x) > 0.f) {
-    if (dot3(p[2].v, x) > 0.f)
-      p[1] = v4;
-    else
-      p[3] = v4;
-  } else {
-    if (dot3(p[3].v, x) > 0.f)
-      p[2] = v4;
-    else
-      p[1] = v4;
-  }
+  const bool c1 = dot3(p[1].v, x) > 0.f, c2 = dot3(p[2].v, x) > 0.f, c3 = dot3(p[3].v, x) > 0.f;
+  // c1: (c2 ? p1 : p3) = v4;  !c1: (c3 ? p2 : p1) = v4
+  sel(p[1], c1 ? c2 : !c3, v4);
+  sel(p[2], !c1 && c3, v4);
+  sel(p[3], c1 && !c2, v4);
 }
 // -1 separated, 0 portal, 1 origin on v1, 2 origin on segment v0-v1
 DEVI int discover(const MPair& P, MSup p[4]) {
@@ -248,22 +257,15 @@ DEVI int discover(const MPair& P, MSup p[4]) {
     P.sup(d, p[3]);
     dt = dot3(p[3].v, d);
     if (fz(dt) || dt < 0.f) return -1;
-    bool cont = false;
     cross(va, p[1].v, p[3].v);
     dt = dot3(va, p[0].v);
-    if (dt < 0.f && !fz(dt)) {
-      p[2] = p[3];
-      cont = true;
-    }
-    if (!cont) {
-      cross(va, p[3].v, p[2].v);
-      dt = dot3(va, p[0].v);
-      if (dt < 0.f && !fz(dt)) {
-        p[1] = p[3];
-        cont = true;
-      }
-    }
-    if (!cont) return 0;
+    const bool r2 = dt < 0.f && !fz(dt);
+    cross(va, p[3].v, p[2].v);
+    dt = dot3(va, p[0].v);
+    const bool r1 = !r2 && dt < 0.f && !fz(dt);
+    if (!r1 && !r2) return 0;
+    sel(p[2], r2, p[3]);
+    sel(p[1], r1, p[3]);
     sub(va, p[1].v, p[0].v);
     sub(vb, p[2].v, p[0].v);
     cross(d, va, vb);
@@ -396,16 +398,14 @@ DEVI int mpr(const MPair& P, float& depth, float dir[3], float pos[3]) {
 }
 
 // ------------------------------------------------------------- primitives
-// append one contact; slot indices are compile-time so PairOut stays in registers
+// append one contact (dropped past the pair's slot count)
 DEVI void emit(PairOut& o, float dist, const float pos[3], const float n[3]) {
+  if (o.n >= o.cap) return;
+  const int r = (o.s0 + o.n) * 7;
+  soa(o.cbuf, r, o.nenv, o.e) = dist;
 #pragma unroll
-  for (int s = 0; s < PAIR_MAXCON; s++)
-    if (s == o.n) {
-      o.c[s][0] = dist;
-#pragma unroll
-      for (int k = 0; k < 3; k++) o.c[s][1 + k] = pos[k], o.c[s][4 + k] = n[k];
-    }
-  if (o.n < PAIR_MAXCON) o.n++;
+  for (int k = 0; k < 3; k++) soa(o.cbuf, r + 1 + k, o.nenv, o.e) = pos[k], soa(o.cbuf, r + 4 + k, o.nenv, o.e) = n[k];
+  o.n++;
 }
 
 DEVI void plane_box(const DModel& m, int gp, int gb, const GeomPose& Pp, const GeomPose& Pb, PairOut& o) {

@@ -289,16 +289,10 @@ __global__ __launch_bounds__(256) void k_collide(const DModel* __restrict__ dm, 
   GeomPose P1, P2;
   load_pose(gpose, n, e, m.pair_geom1[p], P1);
   load_pose(gpose, n, e, m.pair_geom2[p], P2);
-  PairOut o;
+  PairOut o{cbuf, n, e, m.pair_slot[p], m.pair_cap[p], 0};
   collide_pair(m, p, P1, P2, o);
   soa(ccount, p, n, e) = o.n;
   if (o.n > 0) atomicOr(&pmask[(size_t)(p >> 5) * n + e], 1u << (p & 31));
-  const int s0 = m.pair_slot[p];
-#pragma unroll
-  for (int k = 0; k < PAIR_MAXCON; k++)
-    if (k < o.n)
-#pragma unroll
-      for (int f = 0; f < 7; f++) soa(cbuf, (s0 + k) * 7 + f, n, e) = o.c[k][f];
   if (pcyc && (threadIdx.x & 63) == 0) atomicAdd(&pcyc[p], (unsigned long long)(clock64() - t0));
 }
 
