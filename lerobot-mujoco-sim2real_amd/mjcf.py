@@ -43,6 +43,8 @@ CUBE_SCENE_XML = os.path.join(ASSET_DIR, "scene_with_table_cube_v.xml")
 # position-servo scenes (kp = 50 class default, forcerange +-33.5) of the viewer / sim2real scripts
 POSITION_SCENE_XML = os.path.join(ASSET_DIR, "scene_with_table.xml")
 FLOOR_SCENE_XML = os.path.join(ASSET_DIR, "scene.xml")
+# the old calibration's arm on its own (no scene includes it; SO101/so101_old_calib.xml)
+OLD_CALIB_XML = os.path.join(ASSET_DIR, "so101_old_calib.xml")
 
 # MuJoCo defaults (mjmodel.h / user_objects docs)
 DEF_SOLREF = (0.02, 1.0)
@@ -171,8 +173,15 @@ def _apply_actuator_shortcut(act, kind, attrib, is_default=False):
     if kind == "position":
         kp = float(attrib.get("kp", gain))
         act["gainprm0"] = kp
-        kv = float(attrib.get("kv", 0.0))
-        act["biasprm"] = [0.0, -kp, -kv]
+        # kv / dampratio not given: the actuator keeps its current (class default) value.
+        # dampratio is kept as a positive biasprm[2] and turned into -kv once the model's
+        # inertia is known (mj_setConst), see _set_dampratio
+        b2 = float(act.get("biasprm", [0.0, 0.0, 0.0])[2])
+        if "dampratio" in attrib:
+            b2 = float(attrib["dampratio"])
+        elif "kv" in attrib:
+            b2 = -float(attrib["kv"])
+        act["biasprm"] = [0.0, -kp, b2]
     elif kind == "velocity":
         kv = float(attrib.get("kv", gain))   # no kv attribute -> class default gain
         act["gainprm0"] = kv
@@ -678,7 +687,24 @@ def compile_mjcf(xml_path=SCENE_XML, kv=None, disable_contact=False, iterations=
                 d.dof_invweight0[adr + k] = r
         else:
             d.dof_invweight0[adr] = Minv[adr, adr]
+    _set_dampratio(d)
     return cm
+
+
+def _set_dampratio(d):
+    """Position actuators given ``dampratio`` (``so101_new_calib.xml:11,23``) [ext, mj_setConst]:
+    a positive biasprm[2] marks a damping ratio; it becomes the velocity gain
+    kv = dampratio * 2 * sqrt(kp * m), m = gear^2 / dof_invweight0 the inertia the actuator moves
+    at qpos0, stored as biasprm[2] = -kv.  (Only the position-servo scenes use it: the hot-path
+    velocity servos override biasprm, so101_new_calib_v.xml:160-165.)"""
+    for a in range(d.nu):
+        b = d.actuator_biasprm[a]
+        kp = d.actuator_gainprm[a]
+        if b[2] <= 0.0 or kp != -b[1]:
+            continue
+        dof = d.jnt_dofadr[d.actuator_trnid[a]]
+        m = d.actuator_gear[a] ** 2 / d.dof_invweight0[dof]
+        b[2] = -b[2] * 2.0 * np.sqrt(kp * m)
 
 
 class NumpyKinematics:

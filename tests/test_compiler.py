@@ -107,8 +107,32 @@ def test_position_servo_scenes():
     assert (d.nq, d.nv, d.nu) == (6, 6, 6) and d.npair == 71
     for a in range(6):
         assert d.actuator_gainprm[a] == 50.0
-        assert list(d.actuator_biasprm[a]) == [0.0, -50.0, 0.0]
+        # kp = 50 with dampratio = 1 (so101_new_calib.xml:23): kv = 2 sqrt(kp m), m = 1 / dof_invweight0
+        kv = 2.0 * np.sqrt(50.0 / d.dof_invweight0[d.jnt_dofadr[d.actuator_trnid[a]]])
+        assert list(d.actuator_biasprm[a][:2]) == [0.0, -50.0]
+        assert abs(d.actuator_biasprm[a][2] + kv) < 1e-12 and 0.1 < kv < 50
         assert list(d.actuator_forcerange[a]) == [-33.5, 33.5]
+    # the velocity-servo scene keeps biasprm = [0, 0, -kv] whatever the class default's dampratio
+    dv = mjcf.compile_mjcf(mjcf.SCENE_XML).desc
+    assert all(list(dv.actuator_biasprm[a]) == [0.0, 0.0, -50.0] for a in range(6))
     assert abs(d.actuator_ctrlrange[0][1] - 1.91986) < 1e-9
     cf = mjcf.compile_mjcf(mjcf.FLOOR_SCENE_XML)
     assert cf.desc.nu == 6 and cf.desc.npair == 58  # 45 self pairs + 13 floor pairs
+
+
+def test_old_calibration_model():
+    """so101_old_calib.xml compiles standalone (no scene, no table):
+    position servos kp = 17.8 (class sts3215, :23), its own body frames and sites
+    ('base', 'gripper'), the same 13 collision meshes (45 self pairs, nothing else)."""
+    from lerobot_mujoco_sim2real_amd import mjcf
+    cm = mjcf.compile_mjcf(mjcf.OLD_CALIB_XML, obs_site="gripper")
+    d = cm.desc
+    assert (d.nq, d.nv, d.nu, d.nbody) == (6, 6, 6, 8)
+    assert cm.site_names == ["base", "gripper"]
+    assert d.npair == 45
+    for a in range(6):
+        assert d.actuator_gainprm[a] == 17.8 and list(d.actuator_biasprm[a]) == [0.0, -17.8, 0.0]
+        assert list(d.actuator_forcerange[a]) == [-3.35, 3.35]
+    assert abs(d.actuator_ctrlrange[1][0] + 3.31612) < 1e-9 and abs(d.actuator_ctrlrange[2][1] - 3.14159) < 1e-9
+    new = mjcf.compile_mjcf(mjcf.POSITION_SCENE_XML)
+    assert not np.allclose(np.array(d.body_pos[2]), np.array(new.desc.body_pos[2]))  # other calibration

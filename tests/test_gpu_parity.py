@@ -368,10 +368,16 @@ def test_ik_rollout_tracks_fig8(gpu_lib):
     assert err[-1] < 0.02 and err[-1] < 0.5 * err[0], err[::20]
 
 
-def test_position_servo_scene_substep(gpu_lib):
-    """The position-servo scene (kp = 50, force +-33.5), arm-table contacts on."""
+@pytest.mark.parametrize("which", ["new_calib_table", "old_calib"])
+def test_position_servo_scene_substep(gpu_lib, which):
+    """The position-servo scenes: scene_with_table.xml (kp = 50 with
+    dampratio 1, force +-33.5, arm-table contacts on) and the old calibration's arm alone
+    (kp = 17.8, force +-3.35, self-collision pairs only)."""
     from lerobot_mujoco_sim2real_amd import mjcf
-    cm = mjcf.compile_mjcf(mjcf.POSITION_SCENE_XML)
+    if which == "old_calib":
+        cm = mjcf.compile_mjcf(mjcf.OLD_CALIB_XML, obs_site="gripper")
+    else:
+        cm = mjcf.compile_mjcf(mjcf.POSITION_SCENE_XML)
     n = 256
     orc = Oracle(cm)
     st = orc.new_state(n)

@@ -30,7 +30,7 @@ OUT = os.path.join(HERE, "..", "lerobot-mujoco-sim2real_amd", "assets", "so101")
 # the hot path's scene (velocity servos) and, for the position-servo scenes the viewer /
 # sim2real scripts load, scene_with_table.xml + scene.xml
 XMLS = ["scene_with_table_v.xml", "so101_new_calib_v.xml", "scene_with_table.xml", "so101_new_calib.xml",
-        "scene.xml"]
+        "scene.xml", "so101_old_calib.xml"]
 
 
 def read_stl(path):
