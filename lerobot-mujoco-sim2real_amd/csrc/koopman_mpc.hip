@@ -60,34 +60,60 @@ DEVI void stage(double* lds, const double* __restrict__ g, int count) {
 }
 
 // the encoder for this wave's 16 envs: xb = x as the B operand of k-steps 0..1 (lane: row
-// 4s + (lane >> 4), env lane & 15); returns the last layer's output tiles in `act`
+// 4s + (lane >> 4), env lane & 15); returns the last layer's output tiles in `act`.
+// Shapes are static so every MFMA, LDS offset and register index is a compile-time constant:
+// layer 0 is 4 tiles x 2 k-steps (x padded to 8 rows), hidden layers 4 tiles x 16 k-steps
+// (widths zero-padded to 64), the last layer NTL tiles x 16 k-steps.
+template <int NTL>
 DEVI void encode(const KDev& K, const double* lds, int lane, const double xb[2], d4 (&act)[KT]) {
   const int kq = lane >> 4;
+  d4 acc[KT];
+  {  // layer 0 (ReLU: nl >= 2)
+    const double* A = lds + K.frag[0] + lane;
+    const double* bias = lds + K.bias;
 #pragma unroll
-  for (int l = 0; l < SIM_KMAXLAYER; l++) {
-    if (l >= K.nl) continue;  // (continue, not break: the loop must unroll fully)
-    const int nt = K.ntile[l], ks = K.ks[l];
+    for (int T = 0; T < KT; T++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) acc[T][r] = bias[16 * T + kq + 4 * r];
+#pragma unroll
+    for (int s = 0; s < 2; s++)
+#pragma unroll
+      for (int T = 0; T < KT; T++) acc[T] = mfma(A[(T * 2 + s) * 64], xb[s], acc[T]);
+#pragma unroll
+    for (int T = 0; T < KT; T++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) act[T][r] = fmax(acc[T][r], 0.0);
+  }
+  for (int l = 1; l < K.nl - 1; l++) {  // hidden layers: one static body, runtime count
     const double* A = lds + K.frag[l] + lane;
     const double* bias = lds + K.bias + l * SIM_KMAXW;
-    d4 acc[KT];
 #pragma unroll
     for (int T = 0; T < KT; T++)
 #pragma unroll
       for (int r = 0; r < 4; r++) acc[T][r] = bias[16 * T + kq + 4 * r];
     // k-steps outer, tiles inner: KT independent accumulator chains
 #pragma unroll
-    for (int s = 0; s < 4 * KT; s++) {
-      if (s >= ks) continue;
-      const double b = (l == 0) ? (s < 2 ? xb[s] : 0.0) : act[s >> 2][s & 3];
+    for (int s = 0; s < 4 * KT; s++)
 #pragma unroll
-      for (int T = 0; T < KT; T++)
-        if (T < nt) acc[T] = mfma(A[(T * ks + s) * 64], b, acc[T]);
-    }
-    const bool relu = l + 1 < K.nl;
+      for (int T = 0; T < KT; T++) acc[T] = mfma(A[(T * 16 + s) * 64], act[s >> 2][s & 3], acc[T]);
 #pragma unroll
     for (int T = 0; T < KT; T++)
 #pragma unroll
-      for (int r = 0; r < 4; r++) act[T][r] = (T < nt) ? (relu ? fmax(acc[T][r], 0.0) : acc[T][r]) : 0.0;
+      for (int r = 0; r < 4; r++) act[T][r] = fmax(acc[T][r], 0.0);
+  }
+  {  // last layer: no ReLU (models/KoopmanBase.py:20-25)
+    const double* A = lds + K.frag[K.nl - 1] + lane;
+    const double* bias = lds + K.bias + (K.nl - 1) * SIM_KMAXW;
+#pragma unroll
+    for (int T = 0; T < NTL; T++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) acc[T][r] = bias[16 * T + kq + 4 * r];
+#pragma unroll
+    for (int s = 0; s < 4 * KT; s++)
+#pragma unroll
+      for (int T = 0; T < NTL; T++) acc[T] = mfma(A[(T * 16 + s) * 64], act[s >> 2][s & 3], acc[T]);
+#pragma unroll
+    for (int T = 0; T < KT; T++) act[T] = T < NTL ? acc[T] : d4{0, 0, 0, 0};
   }
 }
 
@@ -101,6 +127,7 @@ DEVI void load_x(const KDev& K, const float* __restrict__ x, int e, bool live, i
 }
 
 // Psi_o for m states: z [nz][m]
+template <int NTL>
 __global__ __launch_bounds__(256) void k_encode(KDev K, const double* __restrict__ frag, int m,
                                                 const float* __restrict__ x, double* __restrict__ z) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
@@ -111,13 +138,13 @@ __global__ __launch_bounds__(256) void k_encode(KDev K, const double* __restrict
   double xb[2];
   load_x(K, x, e, live, kq, xb);
   d4 act[KT];
-  encode(K, lds, lane, xb, act);
+  encode<NTL>(K, lds, lane, xb, act);
   if (!live) return;
 #pragma unroll
   for (int s = 0; s < 2; s++)
     if (4 * s + kq < K.xd) z[(size_t)(4 * s + kq) * m + e] = xb[s];
 #pragma unroll
-  for (int T = 0; T < KT; T++)
+  for (int T = 0; T < NTL; T++)
 #pragma unroll
     for (int r = 0; r < 4; r++) {
       const int row = 16 * T + kq + 4 * r;
@@ -126,6 +153,7 @@ __global__ __launch_bounds__(256) void k_encode(KDev K, const double* __restrict
 }
 
 // u0 = ff + Gz z0 + Gu u_prev (z0 = Psi_o(x) unless given); u_prev <- u0; action = clip(u0)
+template <int NTL>
 __global__ __launch_bounds__(256) void k_mpc_step(KDev K, const double* __restrict__ frag, int n,
                                                   const float* __restrict__ x, const double* __restrict__ z0,
                                                   const double* __restrict__ ff, double* __restrict__ uprev,
@@ -135,6 +163,18 @@ __global__ __launch_bounds__(256) void k_mpc_step(KDev K, const double* __restri
   const int lane = threadIdx.x & 63, kq = lane >> 4;
   const int e = blockIdx.x * 64 + (threadIdx.x >> 6) * 16 + (lane & 15);
   const bool live = e < n;
+  // issued before the encoder: consumed after it
+  double up[2], f0[4];
+#pragma unroll
+  for (int s = 0; s < 2; s++) {
+    const int row = 4 * s + kq;
+    up[s] = (live && row < K.ud) ? uprev[(size_t)row * n + e] : 0.0;
+  }
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const int row = kq + 4 * r;
+    f0[r] = (live && ff && row < K.ud) ? ff[(size_t)row * n + e] : 0.0;
+  }
   double xb[2];
   d4 act[KT];
   if (z0) {  // lifted state given (get_control(p), MPC_Controler.py:143)
@@ -148,34 +188,21 @@ __global__ __launch_bounds__(256) void k_mpc_step(KDev K, const double* __restri
 #pragma unroll
       for (int r = 0; r < 4; r++) {
         const int row = 16 * T + kq + 4 * r;
-        act[T][r] = (live && row < K.outw) ? z0[(size_t)(K.xd + row) * n + e] : 0.0;
+        act[T][r] = (live && T < NTL && row < K.outw) ? z0[(size_t)(K.xd + row) * n + e] : 0.0;
       }
   } else {
     load_x(K, x, e, live, kq, xb);
-    encode(K, lds, lane, xb, act);
+    encode<NTL>(K, lds, lane, xb, act);
   }
-  // one output tile: rows = u index (kq + 4r), columns = envs
-  d4 u;
-#pragma unroll
-  for (int r = 0; r < 4; r++) {
-    const int row = kq + 4 * r;
-    u[r] = (live && ff && row < K.ud) ? ff[(size_t)row * n + e] : 0.0;
-  }
+  // one output tile: rows = u index (kq + 4r), columns = envs; ff is the initial accumulator
+  d4 u = {f0[0], f0[1], f0[2], f0[3]};
   const double* G = lds + K.gain + lane;
   u = mfma(G[0], xb[0], u);
   u = mfma(G[64], xb[1], u);
-  const int nf = K.ks_gain - 4;  // feature k-steps
 #pragma unroll
-  for (int s = 0; s < 4 * KT; s++) {
-    if (s >= nf) continue;
-    u = mfma(G[(2 + s) * 64], act[s >> 2][s & 3], u);
-  }
+  for (int s = 0; s < 4 * NTL; s++) u = mfma(G[(2 + s) * 64], act[s >> 2][s & 3], u);
 #pragma unroll
-  for (int s = 0; s < 2; s++) {
-    const int row = 4 * s + kq;
-    const double up = (live && row < K.ud) ? uprev[(size_t)row * n + e] : 0.0;
-    u = mfma(G[(2 + nf + s) * 64], up, u);
-  }
+  for (int s = 0; s < 2; s++) u = mfma(G[(2 + 4 * NTL + s) * 64], up[s], u);
   if (!live) return;
 #pragma unroll
   for (int r = 0; r < 4; r++) {
@@ -187,7 +214,8 @@ __global__ __launch_bounds__(256) void k_mpc_step(KDev K, const double* __restri
   }
 }
 
-// ff[f][u][e] = sum_{t<H} Gr_t zref[f+1+t][:][e]  (zero past nref); FR frames per workgroup
+// ff[f][u][e] = sum_{t<H} Gr_t zref[f+1+t][:][e]  (zero past nref); FR frames per workgroup.
+// gr_ks is a multiple of 4 (zero fragments past K = H nz): 4 static accumulator chains.
 constexpr int FR = 16;
 __global__ __launch_bounds__(256) void k_feedforward(KDev K, const double* __restrict__ grfrag, int nframe,
                                                      int nref, int n, const double* __restrict__ zref,
@@ -204,13 +232,16 @@ __global__ __launch_bounds__(256) void k_feedforward(KDev K, const double* __res
     // this lane's reference element of k-step s: g = 4s + kq -> (t, j) = divmod(g, nz)
     int t = 0, j = kq;
     while (j >= K.nz) j -= K.nz, t++;
-    for (int s = 0; s < K.gr_ks; s++) {
-      const int g = 4 * s + kq;
-      const int fr = f + 1 + t;
-      const double b = (live && g < kk && fr < nref) ? zref[((size_t)fr * K.nz + j) * n + e] : 0.0;
-      acc[s & 3] = mfma(lds[s * 64 + lane], b, acc[s & 3]);
-      j += 4;
-      while (j >= K.nz) j -= K.nz, t++;
+    for (int s0 = 0; s0 < K.gr_ks; s0 += 4) {
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const int g = 4 * (s0 + q) + kq;
+        const int fr = f + 1 + t;
+        const double b = (live && g < kk && fr < nref) ? zref[((size_t)fr * K.nz + j) * n + e] : 0.0;
+        acc[q] = mfma(lds[(s0 + q) * 64 + lane], b, acc[q]);
+        j += 4;
+        while (j >= K.nz) j -= K.nz, t++;
+      }
     }
     if (live) {
 #pragma unroll
@@ -221,6 +252,11 @@ __global__ __launch_bounds__(256) void k_feedforward(KDev K, const double* __res
     }
   }
 }
+
+typedef void (*EncodeFn)(KDev, const double*, int, const float*, double*);
+typedef void (*StepFn)(KDev, const double*, int, const float*, const double*, const double*, double*, float*);
+const EncodeFn ENCODE[4] = {k_encode<1>, k_encode<2>, k_encode<3>, k_encode<4>};
+const StepFn STEP[4] = {k_mpc_step<1>, k_mpc_step<2>, k_mpc_step<3>, k_mpc_step<4>};
 
 }  // namespace
 
@@ -247,7 +283,7 @@ int sim_koopman_create(const sim_koopman_desc* d, const double* weights, const d
   const int xd = d->x_dim, ud = d->u_dim, nl = d->nlayer, H = d->horizon;
   if (xd < 1 || xd > SIM_KMAXX) return soarm_set_error(SIM_E_MODEL, "x_dim must be in 1..8");
   if (ud < 1 || ud > SIM_KMAXU) return soarm_set_error(SIM_E_MODEL, "u_dim must be in 1..8");
-  if (nl < 1 || nl > SIM_KMAXLAYER) return soarm_set_error(SIM_E_MODEL, "nlayer must be in 1..6");
+  if (nl < 2 || nl > SIM_KMAXLAYER) return soarm_set_error(SIM_E_MODEL, "nlayer must be in 2..6");
   if (H < 1 || H > SIM_KMAXH) return soarm_set_error(SIM_E_MODEL, "horizon must be in 1..32");
   if (d->width[0] != xd) return soarm_set_error(SIM_E_MODEL, "width[0] must equal x_dim");
   for (int l = 1; l <= nl; l++)
@@ -256,10 +292,11 @@ int sim_koopman_create(const sim_koopman_desc* d, const double* weights, const d
   K.xd = xd, K.ud = ud, K.nl = nl, K.H = H, K.outw = d->width[nl], K.nz = xd + d->width[nl];
   K.uclip = d->u_clip;
   if (K.H * K.nz > 1024) return soarm_set_error(SIM_E_MODEL, "horizon * nz must be <= 1024");
+  // static kernel shapes: layer 0 = 4 tiles x 2 k-steps, hidden = 4 x 16, last = ntl x 16
   int off = 0;
   for (int l = 0; l < nl; l++) {
-    K.ntile[l] = (d->width[l + 1] + 15) / 16;
-    K.ks[l] = l == 0 ? 2 : 4 * K.ntile[l - 1];
+    K.ntile[l] = l == nl - 1 ? (d->width[l + 1] + 15) / 16 : 4;
+    K.ks[l] = l == 0 ? 2 : 16;
     K.frag[l] = off;
     off += K.ntile[l] * K.ks[l] * 64;
   }
@@ -269,7 +306,7 @@ int sim_koopman_create(const sim_koopman_desc* d, const double* weights, const d
   K.ks_gain = 2 + 4 * K.ntile[nl - 1] + 2;
   off += K.ks_gain * 64;
   K.total = off;
-  K.gr_ks = (K.H * K.nz + 3) / 4;
+  K.gr_ks = 4 * ((K.H * K.nz + 15) / 16);  // a multiple of 4 k-steps (zero fragments past H nz)
   if ((size_t)K.total * 8 > 160 * 1024 || (size_t)K.gr_ks * 64 * 8 > 160 * 1024)
     return soarm_set_error(SIM_E_MODEL, "controller does not fit in LDS");
 
@@ -323,8 +360,9 @@ int sim_koopman_create(const sim_koopman_desc* d, const double* weights, const d
   }
   KCHECK(hipMemcpy(k->d_frag, blob.data(), blob.size() * sizeof(double), hipMemcpyHostToDevice));
   KCHECK(hipMemcpy(k->d_grfrag, gr.data(), gr.size() * sizeof(double), hipMemcpyHostToDevice));
-  KCHECK(hipFuncSetAttribute((const void*)k_encode, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-  KCHECK(hipFuncSetAttribute((const void*)k_mpc_step, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  const int ti = K.ntile[nl - 1] - 1;
+  KCHECK(hipFuncSetAttribute((const void*)ENCODE[ti], hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  KCHECK(hipFuncSetAttribute((const void*)STEP[ti], hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   KCHECK(hipFuncSetAttribute((const void*)k_feedforward, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   *out = k;
   return SIM_OK;
@@ -341,8 +379,8 @@ void sim_koopman_free(sim_koopman* k) {
 int sim_koopman_encode(sim_koopman* k, int m, const float* x, double* z, void* stream) {
   if (!k || !x || !z || m < 0) return soarm_set_error(SIM_E_ARG, "bad argument");
   if (m == 0) return SIM_OK;
-  hipLaunchKernelGGL(k_encode, dim3((m + 63) / 64), dim3(256), k->kd.total * sizeof(double), (hipStream_t)stream,
-                     k->kd, k->d_frag, m, x, z);
+  hipLaunchKernelGGL(ENCODE[k->kd.ntile[k->kd.nl - 1] - 1], dim3((m + 63) / 64), dim3(256),
+                     k->kd.total * sizeof(double), (hipStream_t)stream, k->kd, k->d_frag, m, x, z);
   KCHECK(hipGetLastError());
   return SIM_OK;
 }
@@ -362,8 +400,9 @@ int sim_koopman_mpc_step(sim_koopman* k, int n, const float* x, const double* z0
                          double* u_prev, float* action, void* stream) {
   if (!k || (!x && !z0) || !u_prev || !action || n < 0) return soarm_set_error(SIM_E_ARG, "bad argument");
   if (n == 0) return SIM_OK;
-  hipLaunchKernelGGL(k_mpc_step, dim3((n + 63) / 64), dim3(256), k->kd.total * sizeof(double), (hipStream_t)stream,
-                     k->kd, k->d_frag, n, x, z0, ff, u_prev, action);
+  hipLaunchKernelGGL(STEP[k->kd.ntile[k->kd.nl - 1] - 1], dim3((n + 63) / 64), dim3(256),
+                     k->kd.total * sizeof(double), (hipStream_t)stream, k->kd, k->d_frag, n, x, z0, ff, u_prev,
+                     action);
   KCHECK(hipGetLastError());
   return SIM_OK;
 }

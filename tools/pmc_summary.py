@@ -7,7 +7,7 @@ FETCH_SIZE and WRITE_SIZE (kilobytes, memory-side L2 requests) come from
 separate passes; on gfx950 FETCH_SIZE tallies 128-B requests at 64 B, so it is
 doubled; WRITE_SIZE is taken as is.  SQ_* cycle counters are quad-cycles.
 
-    python tools/pmc_summary.py gpurun_out/prof_r01 r01 [config]
+    python tools/pmc_summary.py gpurun_out/prof_r02_contact r02 [config]
 """
 import collections
 import csv
@@ -16,7 +16,8 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SHORT = {"k_substep": "substep", "k_collide": "collide", "k_step": "step_fused", "k_geom": "geom"}
+SHORT = {"k_substep": "substep", "k_collide": "collide", "k_step": "step_fused", "k_geom": "geom",
+         "k_mpc_step": "mpc_step", "k_bias": "bias"}
 
 
 def short(name):
@@ -75,7 +76,7 @@ def main():
                              "active_frac": c.get("SQ_ACTIVE_INST_ANY", 0) / c["SQ_WAVE_CYCLES"]}
         out["kernels"][k] = e
     pdir = os.path.join(ROOT, "profiles")
-    json.dump(out, open(os.path.join(pdir, f"{tag}_pmc_summary.json"), "w"), indent=1)
+    json.dump(out, open(os.path.join(pdir, f"{tag}_pmc_summary_{cfg}.json"), "w"), indent=1)
     tp = os.path.join(pdir, "pmc_traffic.json")
     allt = json.load(open(tp)) if os.path.exists(tp) else {}
     allt[cfg] = traffic
