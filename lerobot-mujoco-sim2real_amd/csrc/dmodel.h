@@ -80,6 +80,10 @@ struct DModel {
   const uint4* hull_rec;
   const uint4* hull_lutrec;
   const uint16_t* hull_ovf;
+  // support-bound table (see HULL_SB_K): per mesh geom, the hull's support value at every grid
+  // point of a cube map of directions, rounded up; geom_sbadr = first float of the geom's table
+  const float* hull_sb;
+  int geom_sbadr[MAXG];
 };
 
 // Support-point start table: a cube map of HULL_LUT_K x HULL_LUT_K cells per
@@ -94,6 +98,14 @@ constexpr int HULL_LUT_K = 96;
 // neighbours as (x, y, z, local id) -- the first climbing step needs no second round trip
 constexpr int HULL_LUTREC = 10;
 constexpr int HULL_LUT_CELLS = 6 * HULL_LUT_K * HULL_LUT_K;
+
+// Support-bound table: h(p) = max_v v.p at the (HULL_SB_K + 1)^2 grid points p = (+-1, u, v)
+// (axis order as lut_dir) of every cube face.  The support function is convex and positively
+// homogeneous, so for l = m q (q on a face, inside a grid cell's triangle with barycentric
+// weights b_k >= 0 on corners p_k) h(l) = m h(q) <= m sum_k b_k h(p_k): an upper bound on the
+// hull's support from 3 table values, no vertex data touched.  Slack ~ R (cell angle)^2.
+constexpr int HULL_SB_K = 32;
+constexpr int HULL_SB_FACE = (HULL_SB_K + 1) * (HULL_SB_K + 1);
 
 // cube-map cell of a (not necessarily unit) direction; same mapping on host and device
 inline __host__ __device__ int lut_cell(float l0, float l1, float l2) {

@@ -31,6 +31,9 @@ constexpr int CON_MAXG = 16;  // collidable geoms supported by the contact kerne
 constexpr float FEPS = 1e-30f;
 constexpr float MPR_TOLF = 1e-6f;
 constexpr int MPR_ITERS = 50;
+// m: a support-bound test declares a pair apart only beyond this (fp32 rounding of the bound
+// is ~1e-8 m at the arm's scale, so such a pair is apart for MPR in any precision as well)
+constexpr float SEP_MARGIN = 1e-6f;
 
 // per-lane contact list of the dynamics kernel (LDS, [slot][lane])
 struct ConLds {
@@ -139,6 +142,30 @@ DEVI float3 hull_support(const DModel& m, int g, const float l[3]) {
 }
 
 // world support point of geom g (type uniform across the wave)
+// upper bound on a mesh hull's support value along a (not necessarily unit) local direction l
+// from the support-bound table (dmodel.h HULL_SB_K): 3 table loads, no hull data
+DEVI float support_ub(const DModel& m, int g, const float l[3]) {
+  const float a0 = fabsf(l[0]), a1 = fabsf(l[1]), a2 = fabsf(l[2]);
+  int face;
+  float u, v, mx;
+  if (a0 >= a1 && a0 >= a2) {
+    face = l[0] >= 0.f ? 0 : 1, mx = a0, u = l[1], v = l[2];
+  } else if (a1 >= a2) {
+    face = l[1] >= 0.f ? 2 : 3, mx = a1, u = l[0], v = l[2];
+  } else {
+    face = l[2] >= 0.f ? 4 : 5, mx = a2, u = l[0], v = l[1];
+  }
+  const float s = 0.5f * HULL_SB_K / mx;
+  const float fu = fminf(fmaxf((u + mx) * s, 0.f), (float)HULL_SB_K), fv = fminf(fmaxf((v + mx) * s, 0.f), (float)HULL_SB_K);
+  const int i = min((int)fu, HULL_SB_K - 1), j = min((int)fv, HULL_SB_K - 1);
+  const float a = fu - i, b = fv - j;
+  const float* t = m.hull_sb + m.geom_sbadr[g] + face * HULL_SB_FACE + i * (HULL_SB_K + 1) + j;
+  const float h00 = t[0], h10 = t[HULL_SB_K + 1], h01 = t[1], h11 = t[HULL_SB_K + 2];
+  const float q = (a + b <= 1.f) ? (1.f - a - b) * h00 + a * h10 + b * h01
+                                 : (a + b - 1.f) * h11 + (1.f - a) * h01 + (1.f - b) * h10;
+  return mx * q;
+}
+
 DEVI void support(const DModel& m, int g, const GeomPose& P, const float d[3], float out[3]) {
   float l[3];
   mtv(l, P.R, d);
@@ -663,11 +690,10 @@ DEVI void write_geom_poses(const Sim<NA, NF>& S, float* __restrict__ gpose, int 
   }
 }
 
-// midphase + narrowphase of candidate pair p (geom types are wave-uniform)
-DEVI void collide_pair(const DModel& m, int p, const GeomPose& P1, const GeomPose& P2, PairOut& o) {
-  o.n = 0;
+// midphase of candidate pair p: bounding spheres and world-aligned boxes, and for a plane the
+// other geom's bounding sphere above it.  false: no contact is possible.
+DEVI bool midphase(const DModel& m, int p, const GeomPose& P1, const GeomPose& P2) {
   const int g1 = m.pair_geom1[p], g2 = m.pair_geom2[p];
-  const int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
   if (m.geom_rbound[g1] > 0.f && m.geom_rbound[g2] > 0.f) {
     float c1[3], c2[3], r[3];
     geom_center(m, g1, P1, c1);
@@ -675,7 +701,7 @@ DEVI void collide_pair(const DModel& m, int p, const GeomPose& P1, const GeomPos
     sub(r, c1, c2);
     const float mg = m.pair_margin[p];
     const float rr = m.geom_rbound[g1] + m.geom_rbound[g2] + mg;
-    if (dot3(r, r) > rr * rr) return;
+    if (dot3(r, r) > rr * rr) return false;
     bool sep = false;
 #pragma unroll
     for (int k = 0; k < 3; k++) {
@@ -685,16 +711,24 @@ DEVI void collide_pair(const DModel& m, int p, const GeomPose& P1, const GeomPos
                        fabsf(P2.R[3 * k + 2]) * m.geom_half[g2][2];
       sep |= fabsf(r[k]) > e1 + e2 + mg;
     }
-    if (sep) return;
+    if (sep) return false;
   }
-  if (t1 == SIM_GEOM_PLANE) {
+  if (m.geom_type[g1] == SIM_GEOM_PLANE && m.geom_rbound[g2] > 0.f) {
     // bounding sphere of geom2 entirely above the plane (beyond the margin): no contact
-    if (m.geom_rbound[g2] > 0.f) {
-      float c2[3];
-      geom_center(m, g2, P2, c2);
-      const float h = (c2[0] - P1.p[0]) * P1.R[2] + (c2[1] - P1.p[1]) * P1.R[5] + (c2[2] - P1.p[2]) * P1.R[8];
-      if (h > m.geom_rbound[g2] + m.pair_margin[p]) return;
-    }
+    float c2[3];
+    geom_center(m, g2, P2, c2);
+    const float h = (c2[0] - P1.p[0]) * P1.R[2] + (c2[1] - P1.p[1]) * P1.R[5] + (c2[2] - P1.p[2]) * P1.R[8];
+    if (h > m.geom_rbound[g2] + m.pair_margin[p]) return false;
+  }
+  return true;
+}
+
+// narrowphase of a pair that passed the midphase (geom types are uniform over a pair)
+DEVI void narrowphase(const DModel& m, int p, const GeomPose& P1, const GeomPose& P2, PairOut& o) {
+  o.n = 0;
+  const int g1 = m.pair_geom1[p], g2 = m.pair_geom2[p];
+  const int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
+  if (t1 == SIM_GEOM_PLANE) {
     if (t2 == SIM_GEOM_BOX)
       plane_box(m, g1, g2, P1, P2, o);
     else if (t2 == SIM_GEOM_MESH)
@@ -725,14 +759,55 @@ DEVI void collide_pair(const DModel& m, int p, const GeomPose& P1, const GeomPos
       }
     }
     const float nd[3] = {-ax[0], -ax[1], -ax[2]};
+    {  // the same test on the support bound first: no hull data when it already separates
+      const float l[3] = {P2.R[0] * nd[0] + P2.R[3] * nd[1] + P2.R[6] * nd[2],
+                          P2.R[1] * nd[0] + P2.R[4] * nd[1] + P2.R[7] * nd[2],
+                          P2.R[2] * nd[0] + P2.R[5] * nd[1] + P2.R[8] * nd[2]};
+      const float lo = -support_ub(m, g2, l) + (P2.p[0] - P1.p[0]) * ax[0] + (P2.p[1] - P1.p[1]) * ax[1] +
+                       (P2.p[2] - P1.p[2]) * ax[2] - h;  // <= the hull's distance beyond the face
+      if (lo > m.pair_margin[p] + SEP_MARGIN) return;
+    }
     float sp[3];
     support(m, g2, P2, nd, sp);
     const float dist = (sp[0] - P1.p[0]) * ax[0] + (sp[1] - P1.p[1]) * ax[1] + (sp[2] - P1.p[2]) * ax[2] - h;
     if (dist > m.pair_margin[p]) return;
+  }
+  if (t1 == SIM_GEOM_MESH && t2 == SIM_GEOM_MESH) {
+    // MPR's first test on support bounds: along d = c2 - c1 (MPR's first search direction) the
+    // Minkowski difference reaches at most ub = h1(d) + h2(-d); ub < 0 proves the hulls apart,
+    // exactly where MPR would stop at its first support point (discover's first `dt < 0`), but
+    // without the two hull support queries (persistently separated near pairs such as the
+    // wrist/jaw meshes otherwise cost the collide kernel its longest waves)
+    float c1[3], c2[3];
+    geom_center(m, g1, P1, c1);
+    geom_center(m, g2, P2, c2);
+    float d[3] = {c2[0] - c1[0], c2[1] - c1[1], c2[2] - c1[2]};
+    const float n2 = dot3(d, d);
+    if (n2 > 1e-20f) {
+      const float inv = rsqrtf(n2);
+      d[0] *= inv, d[1] *= inv, d[2] *= inv;
+      const float l1[3] = {P1.R[0] * d[0] + P1.R[3] * d[1] + P1.R[6] * d[2],
+                           P1.R[1] * d[0] + P1.R[4] * d[1] + P1.R[7] * d[2],
+                           P1.R[2] * d[0] + P1.R[5] * d[1] + P1.R[8] * d[2]};
+      const float l2[3] = {-(P2.R[0] * d[0] + P2.R[3] * d[1] + P2.R[6] * d[2]),
+                           -(P2.R[1] * d[0] + P2.R[4] * d[1] + P2.R[7] * d[2]),
+                           -(P2.R[2] * d[0] + P2.R[5] * d[1] + P2.R[8] * d[2])};
+      const float ub = (P1.p[0] - P2.p[0]) * d[0] + (P1.p[1] - P2.p[1]) * d[1] + (P1.p[2] - P2.p[2]) * d[2] +
+                       support_ub(m, g1, l1) + support_ub(m, g2, l2);
+      if (ub < -SEP_MARGIN) return;
+    }
   }
   MPair mp{m, g1, g2, P1, P2};
   float depth, dir[3], pos[3];
   if (mpr(mp, depth, dir, pos)) emit(o, -depth, pos, dir);
 }
 
+}  // namespace soarm
+
+namespace soarm {
+// midphase + narrowphase of candidate pair p
+DEVI void collide_pair(const DModel& m, int p, const GeomPose& P1, const GeomPose& P2, PairOut& o) {
+  o.n = 0;
+  if (midphase(m, p, P1, P2)) narrowphase(m, p, P1, P2, o);
+}
 }  // namespace soarm

@@ -49,6 +49,7 @@ struct DevModel {
   uint16_t* d_hlut = nullptr;
   uint4 *d_hrec = nullptr, *d_hlutrec = nullptr;
   uint16_t* d_hovf = nullptr;
+  float* d_hsb = nullptr;
   void release() {
     (void)hipSetDevice(device);
     (void)hipFree(d_model);
@@ -59,6 +60,7 @@ struct DevModel {
     (void)hipFree(d_hrec);
     (void)hipFree(d_hlutrec);
     (void)hipFree(d_hovf);
+    (void)hipFree(d_hsb);
   }
 };
 
@@ -70,7 +72,8 @@ struct sim_model {
   std::vector<uint16_t> hull_lut;
   std::vector<uint4> hull_rec, hull_lutrec;  // climbing records (dmodel.h)
   std::vector<uint16_t> hull_ovf;
-  int lutadr[SIM_MAXGEOM];
+  std::vector<float> hull_sb;  // support-bound table (dmodel.h HULL_SB_K)
+  int lutadr[SIM_MAXGEOM], sbadr[SIM_MAXGEOM];
   int na = 0, nf = 0;
   mutable std::mutex mu;             // guards dev (batches may be created from several threads)
   mutable std::vector<DevModel*> dev;
@@ -294,6 +297,12 @@ __global__ __launch_bounds__(256) void k_collide(const DModel* __restrict__ dm, 
   soa(ccount, p, n, e) = o.n;
   if (o.n > 0) atomicOr(&pmask[(size_t)(p >> 5) * n + e], 1u << (p & 31));
   if (pcyc && (threadIdx.x & 63) == 0) atomicAdd(&pcyc[p], (unsigned long long)(clock64() - t0));
+}
+
+// the collide launch: (env, pair) lanes, 256-env blocks x npair
+static void launch_collide(const sim_batch* b, hipStream_t q, unsigned long long* pcyc) {
+  hipLaunchKernelGGL(k_collide, dim3((b->n + 255) / 256, b->model->desc.npair), dim3(256), 0, q, b->d_model, b->n,
+                     b->d_gpose, b->d_cbuf, b->d_ccount, b->d_pmask, pcyc);
 }
 
 // walk the pairs in order and append their contacts (deterministic indexing)
@@ -887,6 +896,7 @@ static int upload_into(const sim_model* m, DevModel* D) {
   if (int rc = up(D->d_hrec, m->hull_rec)) return rc;
   if (int rc = up(D->d_hlutrec, m->hull_lutrec)) return rc;
   if (int rc = up(D->d_hovf, m->hull_ovf)) return rc;
+  if (int rc = up(D->d_hsb, m->hull_sb)) return rc;
   dm.hull_vert = D->d_hv;
   dm.hull_adr = D->d_hadr;
   dm.hull_adj = D->d_hadj;
@@ -894,7 +904,11 @@ static int upload_into(const sim_model* m, DevModel* D) {
   dm.hull_rec = D->d_hrec;
   dm.hull_lutrec = D->d_hlutrec;
   dm.hull_ovf = D->d_hovf;
-  for (int g = 0; g < MAXG; g++) dm.geom_lutadr[g] = g < m->desc.ngeom ? m->lutadr[g] : -1;
+  dm.hull_sb = D->d_hsb;
+  for (int g = 0; g < MAXG; g++) {
+    dm.geom_lutadr[g] = g < m->desc.ngeom ? m->lutadr[g] : -1;
+    dm.geom_sbadr[g] = g < m->desc.ngeom ? m->sbadr[g] : -1;
+  }
   HIPCHECK(hipMalloc(&D->d_model, sizeof(DModel)));
   HIPCHECK(hipMemcpy(D->d_model, &dm, sizeof(DModel), hipMemcpyHostToDevice));
   return SIM_OK;
@@ -1031,6 +1045,32 @@ int sim_model_create(const sim_model_desc* desc, const float* hull_vert, const i
       M->hull_rec[2 * i + 1] = make_uint4(id[0] | id[1] << 16, id[2] | id[3] << 16, id[4] | id[5] << 16, id[6] | id[7] << 16);
     }
   }
+  // support-bound table: exact support at every grid point, rounded up to the next float
+  M->hull_sb.assign((size_t)std::max(nmesh, 1) * 6 * HULL_SB_FACE, 0.f);
+  for (int g = 0, k = 0; g < desc->ngeom; g++) {
+    M->sbadr[g] = -1;
+    if (desc->geom_type[g] != SIM_GEOM_MESH) continue;
+    M->sbadr[g] = k * 6 * HULL_SB_FACE;
+    const float* hv = hull_vert + 3 * (size_t)desc->geom_hulladr[g];
+    const int nv = desc->geom_hullnum[g];
+    for (int f = 0; f < 6; f++)
+      for (int i = 0; i <= HULL_SB_K; i++)
+        for (int j = 0; j <= HULL_SB_K; j++) {
+          const double u = -1.0 + 2.0 * i / HULL_SB_K, v = -1.0 + 2.0 * j / HULL_SB_K, sg = (f & 1) ? -1.0 : 1.0;
+          double d[3];
+          switch (f >> 1) {
+            case 0: d[0] = sg, d[1] = u, d[2] = v; break;
+            case 1: d[0] = u, d[1] = sg, d[2] = v; break;
+            default: d[0] = u, d[1] = v, d[2] = sg; break;
+          }
+          double bd = -1e300;
+          for (int a = 0; a < nv; a++)
+            bd = std::fmax(bd, d[0] * hv[3 * a] + d[1] * hv[3 * a + 1] + d[2] * hv[3 * a + 2]);
+          M->hull_sb[(size_t)M->sbadr[g] + f * HULL_SB_FACE + i * (HULL_SB_K + 1) + j] =
+              std::nextafter((float)bd, 3.0e38f);
+        }
+    k++;
+  }
   M->hull_lutrec.assign((size_t)HULL_LUTREC * M->hull_lut.size(), make_uint4(0, 0, 0, 0));
   for (int g = 0; g < desc->ngeom; g++) {
     if (M->lutadr[g] < 0) continue;
@@ -1163,8 +1203,7 @@ int sim_step(sim_batch* b, const sim_state* s, const float* action, int frame_sk
       for (int sub = 0; sub < frame_skip; sub++) {
         if (np > 0) {
           prof_mark(b, 1, q);
-          hipLaunchKernelGGL(k_collide, dim3((b->n + 255) / 256, np), dim3(256), 0, q, b->d_model, b->n,
-                             b->d_gpose, b->d_cbuf, b->d_ccount, b->d_pmask, nullptr);
+          launch_collide(b, q, nullptr);
           prof_mark(b, -1, q);
         }
         const bool last = sub == frame_skip - 1;
@@ -1242,8 +1281,7 @@ int sim_contacts(sim_batch* b, const sim_state* s, float* out, int32_t* ncon, vo
                        b->d_gpose);
   });
   if (np > 0)
-    hipLaunchKernelGGL(k_collide, dim3((b->n + 255) / 256, np), dim3(256), 0, st, b->d_model, b->n,
-                       b->d_gpose, b->d_cbuf, b->d_ccount, b->d_pmask, nullptr);
+    launch_collide(b, st, nullptr);
   hipLaunchKernelGGL(k_gather, grid_for(b->n), dim3(64), 0, st, b->d_model, b->n, b->d_cbuf, b->d_ccount, b->d_pmask,
                      out, ncon);
   HIPCHECK(hipGetLastError());
@@ -1265,8 +1303,7 @@ int sim_collide_profile(sim_batch* b, const sim_state* s, double* cycles, void* 
     hipLaunchKernelGGL((k_geom<NA, NF>), grid_for(b->n), dim3(64), 0, st, b->d_model, b->n, *s,
                        b->d_gpose);
   });
-  hipLaunchKernelGGL(k_collide, dim3((b->n + 255) / 256, np), dim3(256), 0, st, b->d_model, b->n,
-                     b->d_gpose, b->d_cbuf, b->d_ccount, b->d_pmask, d_cyc);
+  launch_collide(b, st, d_cyc);
   HIPCHECK(hipMemsetAsync(b->d_pmask, 0, (size_t)((np + 31) / 32) * b->n * sizeof(uint32_t), st));
   std::vector<unsigned long long> h(np);
   HIPCHECK(hipMemcpyAsync(h.data(), d_cyc, np * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
