@@ -259,9 +259,9 @@ int sim_observe(sim_batch* b, const sim_state* s, float* obs, void* stream);
    int32 bits), ncon [N].  Contact order = candidate-pair order (MuJoCo's). */
 int sim_contacts(sim_batch* b, const sim_state* s, float* out, int32_t* ncon, void* stream);
 
-/* diagnostic: geom poses + one collide pass with per-pair timing; cycles [npair]
-   (host) = sum over waves of each wave's shader-clock cycles for that pair.
-   Synchronous. */
+/* diagnostic: geom poses + one collide pass with per-pair timing; cycles [2][npair]
+   (host) = per pair, the sum over its waves of each wave's shader-clock cycles, then the
+   largest single wave's.  Synchronous. */
 int sim_collide_profile(sim_batch* b, const sim_state* s, double* cycles, void* stream);
 
 /* diagnostic: summed wave cycles per phase of the contact substep kernel in a

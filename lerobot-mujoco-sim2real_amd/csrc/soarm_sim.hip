@@ -279,7 +279,7 @@ __global__ __launch_bounds__(64) void k_geom(const DModel* __restrict__ dm, int 
 }
 
 // mj_collision, one lane per (env, candidate pair); blockIdx.y = pair
-__global__ __launch_bounds__(256) void k_collide(const DModel* __restrict__ dm, int n,
+__global__ __launch_bounds__(256, 3) void k_collide(const DModel* __restrict__ dm, int n,
                                                  const float* __restrict__ gpose,
                                                  float* __restrict__ cbuf, int* __restrict__ ccount,
                                                  uint32_t* __restrict__ pmask,
@@ -296,7 +296,11 @@ __global__ __launch_bounds__(256) void k_collide(const DModel* __restrict__ dm, 
   collide_pair(m, p, P1, P2, o);
   soa(ccount, p, n, e) = o.n;
   if (o.n > 0) atomicOr(&pmask[(size_t)(p >> 5) * n + e], 1u << (p & 31));
-  if (pcyc && (threadIdx.x & 63) == 0) atomicAdd(&pcyc[p], (unsigned long long)(clock64() - t0));
+  if (pcyc && (threadIdx.x & 63) == 0) {
+    const unsigned long long dt = (unsigned long long)(clock64() - t0);
+    atomicAdd(&pcyc[p], dt);
+    atomicMax(&pcyc[gridDim.y + p], dt);
+  }
 }
 
 // the collide launch: (env, pair) lanes, 256-env blocks x npair
@@ -1296,8 +1300,8 @@ int sim_collide_profile(sim_batch* b, const sim_state* s, double* cycles, void* 
   const int np = b->model->desc.npair;
   if (np <= 0) return SIM_OK;
   unsigned long long* d_cyc = nullptr;
-  HIPCHECK(hipMalloc(&d_cyc, np * sizeof(unsigned long long)));
-  HIPCHECK(hipMemsetAsync(d_cyc, 0, np * sizeof(unsigned long long), st));
+  HIPCHECK(hipMalloc(&d_cyc, 2 * np * sizeof(unsigned long long)));
+  HIPCHECK(hipMemsetAsync(d_cyc, 0, 2 * np * sizeof(unsigned long long), st));
   dispatch_nf(b->model->nf, [&](auto nfc) {
     constexpr int NA = 6, NF = decltype(nfc)::value;
     hipLaunchKernelGGL((k_geom<NA, NF>), grid_for(b->n), dim3(64), 0, st, b->d_model, b->n, *s,
@@ -1305,11 +1309,11 @@ int sim_collide_profile(sim_batch* b, const sim_state* s, double* cycles, void* 
   });
   launch_collide(b, st, d_cyc);
   HIPCHECK(hipMemsetAsync(b->d_pmask, 0, (size_t)((np + 31) / 32) * b->n * sizeof(uint32_t), st));
-  std::vector<unsigned long long> h(np);
-  HIPCHECK(hipMemcpyAsync(h.data(), d_cyc, np * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+  std::vector<unsigned long long> h(2 * np);
+  HIPCHECK(hipMemcpyAsync(h.data(), d_cyc, 2 * np * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
   HIPCHECK(hipStreamSynchronize(st));
   HIPCHECK(hipFree(d_cyc));
-  for (int p = 0; p < np; p++) cycles[p] = (double)h[p];
+  for (int p = 0; p < 2 * np; p++) cycles[p] = (double)h[p];
   return SIM_OK;
 }
 

@@ -232,12 +232,14 @@ class BatchSim:
                                                   self._stream()))
         return out, nc
 
-    def collide_profile(self):
-        """Per candidate pair, summed wave cycles of one collide pass (numpy [npair])."""
-        cyc = np.zeros(max(self.cm.desc.npair, 1), dtype=np.float64)
+    def collide_profile(self, with_max=False):
+        """Per candidate pair, summed wave cycles of one collide pass (numpy [npair]); with_max:
+        also the largest single wave's cycles per pair (the pass's critical path)."""
+        npair = self.cm.desc.npair
+        cyc = np.zeros(2 * max(npair, 1), dtype=np.float64)
         abi.check(self.lib, self.lib.sim_collide_profile(self._batch, C.byref(self._state),
                                                          cyc.ctypes.data, self._stream()))
-        return cyc[:self.cm.desc.npair]
+        return (cyc[:npair], cyc[npair:2 * npair]) if with_max else cyc[:npair]
 
     def ik(self, target, q=None, tol=1e-6, regularization_threshold=0.1, regularization_strength=1e-2,
            max_update_norm=2.0, progress_thresh=20.0, max_steps=100, ndof=5):

@@ -17,7 +17,7 @@ from lerobot_mujoco_sim2real_amd import workloads as W  # noqa: E402
 from lerobot_mujoco_sim2real_amd.sim import BatchSim  # noqa: E402
 
 n = 4096
-cm = W.model("contact")
+cm = W.model(os.environ.get("CONFIG", "contact"))
 ids = np.arange(n)
 sim = BatchSim(cm, n, 0)
 q0 = W.initial_qpos(cm, ids, 0)
@@ -28,13 +28,16 @@ res = {}
 T = int(sys.argv[1]) if len(sys.argv) > 1 else 120
 for t in range(T + 1):
     if t in (5, T // 2, T):
-        cyc = sim.collide_profile()
+        cyc, mx = sim.collide_profile(with_max=True)
         tot = cyc.sum()
         top = np.argsort(-cyc)[:12]
         d = cm.desc
         rows = [(int(p), cm.geom_names[d.pair_geom1[p]], cm.geom_names[d.pair_geom2[p]], round(cyc[p] / tot, 4))
                 for p in top]
-        res[t] = {"total_wave_cycles": tot, "top": rows}
+        topm = np.argsort(-mx)[:12]
+        rows_max = [(int(p), cm.geom_names[d.pair_geom1[p]], cm.geom_names[d.pair_geom2[p]], int(mx[p])) for p in topm]
+        res[t] = {"total_wave_cycles": tot, "top": rows, "top_max_wave": rows_max}
+        print(t, "max-wave", rows_max, flush=True)
         print(t, f"total {tot:.3e}", rows, flush=True)
     sim.step(W.chirp_action(tab, float(t), lib=torch))
 os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
