@@ -37,7 +37,7 @@ from lerobot_mujoco_sim2real_amd.sim import BatchSim  # noqa: E402
 
 n = int(os.environ.get("ENVS", 4096))
 T = int(sys.argv[1]) if len(sys.argv) > 1 else 120
-cm = W.model("contact")
+cm = W.model(os.environ.get("CONFIG", "contact"))
 ids = np.arange(n)
 sim = BatchSim(cm, n, 0)
 q0 = W.initial_qpos(cm, ids, 0)
@@ -83,4 +83,4 @@ for t in range(T):
                                    enumerate(["loads+frame", "jacobian", "gram", "edges+writes"])}
         res[t] = r
         print(t, json.dumps(r), flush=True)
-json.dump(res, open(os.path.join(ROOT, "gpurun_out", "phase_prof.json"), "w"), indent=1)
+json.dump(res, open(os.path.join(ROOT, "gpurun_out", f"phase_prof_{os.environ.get('CONFIG', 'contact')}.json"), "w"), indent=1)
