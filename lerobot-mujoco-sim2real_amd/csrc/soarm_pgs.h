@@ -116,6 +116,9 @@ template <int NA, int NF>
 constexpr int keep_floats() { return NA * (NA + 1) / 2 + 6 * NF + (NA + 6 * NF) + 3; }
 // joint-limit rows (rare): compact list, one record per active limit
 constexpr int LF = 7;  // dof, sign, aref, R, ARdiag, 1/ARdiag, force
+// PGS: the arm's rows are retired from the sweeps of a pure-block / uncoupled-extra solve once
+// one sweep moves their forces by at most this much in total (N, N m); see ysweeps
+constexpr float ARM_RETIRE = 1e-6f;
 constexpr int XS_LIST = SIM_MAXCON;           // ext[0, XS_LIST): the env's contact list (quad build)
 constexpr int XS_EXT = XS_LIST + 98;           // + extra-slot scratch beyond the limit list
 enum { L_DOF = 0, L_SGN = 1, L_AREF = 2, L_R = 3, L_ARD = 4, L_IARD = 5, L_FRC = 6 };
@@ -715,7 +718,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
 #ifdef SOARM_PHASE_PROF
   if (e < 65536) g_pgs_prof[8 * e] = clock64();
   PSTAMP(9);
-  int nsweep = m.iterations;
+  int nsweep = m.iterations, armstop = 0;
 #endif
   // dof-frictionloss rows (J = e_i): one pass.  Branch-free: a dof with frictionloss 0
   // (no row in MuJoCo) clamps to [0, 0] and stays an exact no-op.
@@ -1207,12 +1210,13 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   };
   // dof-frictionloss rows of the y variants, short-chain form: df = clamp(-res/ARdiag,
   // -fl - f, fl - f) (the projected step), v_arm += M^-1 e_i df
-  auto fric_row_y = [&](const int i, float& improvement, auto ext, auto pk) {
+  auto fric_row_y = [&](const int i, float& improvement, auto ext, auto pk, float& famax) {
     {
       const float fl = m.dof_frictionloss[i];
       const float res = fmaf(fR[i], ff[i], v[i] - fa[i]);
       const float fn = fminf(fmaxf(fmaf(res, -fiD[i], ff[i]), -fl), fl);
       const float df = fn - ff[i];
+      famax += fabsf(df);  // a NaN step keeps famax from passing the retire test
       if constexpr (decltype(pk)::value) {
 #pragma unroll
         for (int k = 0; k + 1 < NA; k += 2) {  // v_arm += M^-1 e_i df, two dofs per packed FMA
@@ -1451,7 +1455,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       v[2 * k] = t.x, v[2 * k + 1] = t.y;
     }
   };
-  auto yf_row_q = [&](f2& imp) {
+  auto yf_row_q = [&](f2& imp, float& famax) {
     f2 y01 = xq.fSh01;
     float y2 = xq.fSh2;
 #pragma unroll
@@ -1459,6 +1463,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
     float df[4];
     qchain(y01.x, y01.y, y2, fF, xq.fMu, xq.fRp, xq.fIA, xq.fA10, xq.fA2030, xq.fA2131, xq.fA32, xq.fHD01, xq.fHD23,
            imp, df);
+    famax += (fabsf(df[0]) + fabsf(df[1])) + (fabsf(df[2]) + fabsf(df[3]));
     const float mu = xq.fMu;
     const float D[3] = {(df[0] + df[1]) + (df[2] + df[3]), mu * (df[0] - df[1]), mu * (df[2] - df[3])};
     qvarm(xq.fWp, D);
@@ -1467,10 +1472,11 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
     for (int rr = 0; rr < 3; rr++) e01 = fma2(xq.fXp[rr], splat2(D[rr]), e01), yE[2] = fmaf(xq.fX2[rr], D[rr], yE[2]);
     yE[0] = e01.x, yE[1] = e01.y;
   };
-  auto yext_row_q = [&](f2& imp, auto coupled) {
+  auto yext_row_q = [&](f2& imp, auto coupled, float& famax) {
     float df[4];
     qchain(yE[0], yE[1], yE[2], fE, xq.eMu, xq.eRp, xq.eIA, xq.eA10, xq.eA2030, xq.eA2131, xq.eA32, xq.eHD01, xq.eHD23,
            imp, df);
+    if constexpr (!decltype(coupled)::value) famax += (fabsf(df[0]) + fabsf(df[1])) + (fabsf(df[2]) + fabsf(df[3]));
     const float mu = xq.eMu;
     const float D[3] = {(df[0] + df[1]) + (df[2] + df[3]), mu * (df[0] - df[1]), mu * (df[2] - df[3])};
     qvarm(xq.eWp, D);
@@ -1611,7 +1617,9 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       yext_setup(cE, cF);
       if constexpr (PK::value) yext_preload();
     }
-    for (int it = 0; it < m.iterations; it++) {
+    // one sweep; ARM = false leaves out the arm's rows (see below).  Returns the
+    // improvement; famax gets the sum of |df| over the arm's rows.
+    auto sweep = [&](auto arm, float& famax) {
       // the arm's frictionloss rows and the cube block touch disjoint dofs (M is block
       // diagonal): the two Gauss-Seidel chains commute, so their rows are interleaved in
       // program order to give the (latency-bound) issue stream independent work; the
@@ -1622,31 +1630,73 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       // (NA = 6, FC = 4: rows {0,1} c0 {2} c1 {3,4} c2 {5} c3)
 #pragma unroll
       for (int j = 0; j < FC; j++) {
+        if constexpr (decltype(arm)::value) {
 #pragma unroll
-        for (int i = (j * NA + FC - 1) / FC; i < ((j + 1) * NA + FC - 1) / FC; i++) fric_row_y(i, improvement, ext, PK{});
+          for (int i = (j * NA + FC - 1) / FC; i < ((j + 1) * NA + FC - 1) / FC; i++)
+            fric_row_y(i, improvement, ext, PK{}, famax);
+        }
         yblock_contact(j, imp_b, impq, dsel, coupled, PK{});
       }
       if constexpr (FC == 0) {
 #pragma unroll
-        for (int i = 0; i < NA; i++) fric_row_y(i, improvement, ext, PK{});
+        for (int i = 0; i < NA; i++) fric_row_y(i, improvement, ext, PK{}, famax);
       }
       if constexpr (PK::value) {
         if constexpr (decltype(ext)::value && decltype(coupled)::value) yblock_to_e(dsel);
-        if constexpr (decltype(ext2)::value) yf_row_q(impq);
-        if constexpr (decltype(ext)::value) yext_row_q(impq, coupled);
+        if constexpr (decltype(arm)::value && decltype(ext2)::value) yf_row_q(impq, famax);
+        if constexpr (decltype(arm)::value && decltype(ext)::value) yext_row_q(impq, coupled, famax);
         improvement += impq.x + impq.y;
       } else {
         improvement += imp_b;
         if constexpr (decltype(ext2)::value) yf_row(improvement);
         if constexpr (decltype(ext)::value) yext_row(improvement, coupled);
       }
-      if (improvement * scale < m.tolerance) {
-#ifdef SOARM_PHASE_PROF
-        nsweep = it + 1;
-#endif
+      return improvement;
+    };
+    // Arm retirement.  Unless an extra contact touches the cube, the arm's rows (its dof
+    // frictionloss rows and the arm-only extra slots E/F) and the cube block share no dof:
+    // two Gauss-Seidel systems that only meet in the stopping test.  Once a sweep moves the
+    // arm's forces by at most ARM_RETIRE in total (N, N m) on every lane of the wave, the
+    // remaining sweeps run the block alone (the pure block converges ~95 sweeps slower than
+    // the arm, which settles in ~3).  The threshold sits an order below what MuJoCo's own
+    // stopping test resolves: a row's step df lowers the cost by >= ARdiag df^2 / 2, and the
+    // solve stops at improvement / trace(M) < tolerance (1e-8), which for the arm's rows
+    // (ARdiag ~ 30, trace(M) ~ 0.3) leaves steps of order 1e-5.  Exactly-zero steps (the
+    // common case: frictionloss rows saturated at +-frictionloss) leave the result bit for
+    // bit equal to sweeping all rows.
+    constexpr bool RETIRE = PK::value && FC > 0 && !decltype(coupled)::value;
+    int it = 0;
+    bool done = false;
+    for (; it < m.iterations; it++) {
+      float famax = 0.f;
+      if (sweep(std::true_type{}, famax) * scale < m.tolerance) {
+        done = true;
         break;
       }
+      if constexpr (RETIRE) {
+        if (__all(famax <= ARM_RETIRE)) {
+#ifdef SOARM_PHASE_PROF
+          armstop = it + 1;
+#endif
+          it++;
+          break;
+        }
+      }
     }
+    if constexpr (RETIRE) {
+      if (!done)
+        for (; it < m.iterations; it++) {
+          float unused = 0.f;
+          if (sweep(std::false_type{}, unused) * scale < m.tolerance) {
+            done = true;
+            break;
+          }
+        }
+    }
+#ifdef SOARM_PHASE_PROF
+    nsweep = done ? it + 1 : m.iterations;
+#endif
+    (void)done;
     yblock_finish();
     if constexpr (decltype(ext)::value) yext_finish(cE, hasE, cF, hasF, coupled);
   };
@@ -1726,7 +1776,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
     g_pgs_prof[8 * e + 1] = clock64(), g_pgs_prof[8 * e + 2] = nsweep,
     g_pgs_prof[8 * e + 3] = (ypure ? 0 : yext ? 1 : block_first ? 2 : 3) | (npost > 0 && npost_free ? 16 : 0) |
                             (min(npost, 3) << 8) | (min(nfree_x, 3) << 12) | ((nl > 5) << 16) | ((nlim > 0) << 17) |
-                            ((nl != ncon) << 18),
+                            ((nl != ncon) << 18) | ((long long)min(armstop, 255) << 20),
     g_pgs_prof[8 * e + 4] = nlim, g_pgs_prof[8 * e + 5] = ncon;
 #endif
 

@@ -12,7 +12,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB = os.path.join(ROOT, "tools", "_prof", "libsoarm_sim_prof.so")
+LIB = os.environ.get("PROF_LIB") or os.path.join(ROOT, "tools", "_prof", "libsoarm_sim_prof.so")
 SRC = os.path.join(ROOT, "lerobot-mujoco-sim2real_amd", "csrc", "soarm_sim.hip")
 
 if "--build" in sys.argv:
@@ -21,7 +21,7 @@ if "--build" in sys.argv:
     from lerobot_mujoco_sim2real_amd.build import FLAGS, HIPCC, SOURCES, SRC_DIR
 
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
-    subprocess.check_call([HIPCC] + FLAGS + ["-DSOARM_PHASE_PROF", "-o", LIB] + [os.path.join(SRC_DIR, f) for f in SOURCES])
+    subprocess.check_call([HIPCC] + FLAGS + ["-DSOARM_PHASE_PROF"] + [a for a in sys.argv[1:] if a.startswith("-D")] + ["-o", LIB] + [os.path.join(SRC_DIR, f) for f in SOURCES])
     sys.exit(0)
 
 sys.path.insert(0, ROOT)
@@ -44,7 +44,7 @@ q0 = W.initial_qpos(cm, ids, 0)
 sim.reset(init_qpos=q0[:, :5], extra_qpos=q0, seed=0)
 tab = {k: (torch.as_tensor(v, dtype=torch.float32, device="cuda") if isinstance(v, np.ndarray) else v)
        for k, v in W.chirp_tables(ids, 0).items()}
-out = (ctypes.c_double * 57)()
+out = (ctypes.c_double * 61)()
 res = {}
 every = int(os.environ.get("EVERY", 0))
 starts = set(range(0, T, every)) if every else {0, T // 2, T - 10}
@@ -81,6 +81,9 @@ for t in range(T):
         r["nony_lanes"] = {"npost": v[43:47], "free_extras": v[47:50], "nl>5": v[50], "limit": v[51], "overflow": v[52]}
         r["row_split_per_wave"] = {nm: round(v[53 + i] / max(v[5], 1)) for i, nm in
                                    enumerate(["loads+frame", "jacobian", "gram", "edges+writes"])}
+        r["armstop_waves"] = v[57] / max(v[5], 1)
+        r["mean_armstop_sweep"] = v[58] / max(v[57], 1)
+        r["max_wave_cycles_kept_retired"] = [v[59], v[60]]
         res[t] = r
         print(t, json.dumps(r), flush=True)
 json.dump(res, open(os.path.join(ROOT, "gpurun_out", f"phase_prof_{os.environ.get('CONFIG', 'contact')}.json"), "w"), indent=1)
