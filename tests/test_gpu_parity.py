@@ -264,6 +264,11 @@ def test_one_substep_bench_state_mixed_contacts(gpu_lib):
     np.testing.assert_allclose(to_np(S.qpos).T, st["qpos"], atol=5e-6)
     np.testing.assert_allclose(to_np(S.qvel).T, st["qvel"], atol=5e-3)
     assert to_np(S.ncon).sum() == st["ncon"].sum()
+    # the arm's velocities (its rows retire from the sweeps early, soarm_pgs.h ysweeps): the
+    # bulk stays at fp32 resolution, as with the full sweep schedule (measured p99 8e-8,
+    # max 2e-5 on 1024 envs, identical to a build without retirement)
+    err = np.abs(to_np(S.qvel).T[:, :6] - st["qvel"][:, :6]).max(1)
+    assert np.percentile(err, 99) < 1e-6 and err.max() < 2e-4, (np.percentile(err, 99), err.max())
 
 
 def test_one_substep_extra_contact_sweeps(gpu_lib):
