@@ -982,7 +982,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   // register pairs the packed loop consumes (no memory reads inside the sweep loop)
   struct ExtQ {
     float eIA[4], fIA[4], muo, eA10, eA32, fA10, fA32, eMu, eRp, fMu, fRp, fJ2[6], fX2[3], eG2[3], xo[9], fSh2;
-    f2 eWp[9], eA2030, eA2131, fA2030, fA2131, eHD01, eHD23, fHD01, fHD23, fJp[6], fWp[9], fXp[3], eGp[3], xop[3], fSh01;
+    f2 eWp[9], eA2030, eA2131, fA2030, fA2131, eHD01, eHD23, fHD01, fHD23, fJp[6], fWp[9], fXp[3], eGp[3], qe01[3], qe23[3], fSh01;
   } xq;
   constexpr int NX = FC * (FC - 1) / 2;
   float yb[FC][3], xg[NX > 0 ? NX : 1][9];
@@ -991,6 +991,9 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   // quad mode: this lane's block contact (sub) — its y and its cross-Gram row X_sub,j
   // (j = sub: the contact's own 3x3 Gram block), full 3x3 per j
   float yo[3] = {0.f, 0.f, 0.f}, xr[QUAD ? FC : 1][9];
+  // quad mode, packed: this lane's contact's 4 edge residuals r_e = y_0 + s_e y_t(e) + R f_e
+  // (pairs (r0, r1), (r2, r3)); the sweep broadcasts them instead of y
+  f2 ro01 = f2{0.f, 0.f}, ro23 = f2{0.f, 0.f};
   // rows of the arm block of M^-1 as dof pairs (packed v_arm updates of the friction rows)
   f2 Mp[NA][NA / 2];
   auto ypair = [](int j, int k) { return j * FC - j * (j + 1) / 2 + (k - j - 1); };  // j < k
@@ -1065,10 +1068,10 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   // per-sweep constants of the block in registers: 1/ARdiag, ARdiag/2, mu, R, the
   // off-diagonal edge-Gram entries A_ed = J_e M^-1 J_d' (d < e) and the 3x3 Gram block
   float yia[FC][4], yhd[FC][4], ymu[FC], yRp[FC], yA[FC][6], yG[FC][6];
-  // quad mode, packed: (mu, -mu), edge-Gram pairs (A20, A30), (A21, A31), ARdiag/2 pairs, and
-  // the own row's update folded per edge, K_e = X_sub,j (1, s_e on t(e)): y_own += K_e df_e
-  f2 qmu2[FC], qA2030[FC], qA2131[FC], qhd01[FC], qhd23[FC], K01[QUAD ? FC : 1][4];
-  float K2[QUAD ? FC : 1][4];
+  // quad mode, packed: edge-Gram pairs (A20, A30), (A21, A31), ARdiag/2 pairs, and the own
+  // residuals' update per edge of contact j: C_e'e = (1, s'_e' on t(e')) X_sub,j (1, s_e on
+  // t(e)) + R delta (own contact), as pairs over e': r_own += C_.e df_e
+  f2 qA2030[FC], qA2131[FC], qhd01[FC], qhd23[FC], C01[QUAD ? FC : 1][4], C23[QUAD ? FC : 1][4];
   auto yblock_consts = [&](auto pk) {
     if constexpr (NF == 1 && CON) {
 #pragma unroll
@@ -1098,14 +1101,36 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
           for (int d = 0; d < ed; d++)
             yA[k][q++] = G[0] + sg(ed) * gt(ed) + sg(d) * gt(d) + sg(ed) * sg(d) * gtt(ed, d);
         if constexpr (QUAD && decltype(pk)::value) {
-          qmu2[k] = f2{mu, -mu};
           qA2030[k] = f2{yA[k][1], yA[k][3]}, qA2131[k] = f2{yA[k][2], yA[k][4]};
           qhd01[k] = f2{yhd[k][0], yhd[k][1]}, qhd23[k] = f2{yhd[k][2], yhd[k][3]};
+        }
+      }
+      if constexpr (QUAD && decltype(pk)::value) {
+        // own contact (sub): mu, R, forces; its residuals from y; the folded coefficients
+        const float muo = sub == 0 ? ymu[0] : sub == 1 ? ymu[1] : sub == 2 ? ymu[2] : ymu[3];
+        const float Rpo = sub == 0 ? yRp[0] : sub == 1 ? yRp[1] : sub == 2 ? yRp[2] : yRp[3];
+        float fo[4];
+#pragma unroll
+        for (int ed = 0; ed < 4; ed++) fo[ed] = sub == 0 ? cfo[0][ed] : sub == 1 ? cfo[1][ed] : sub == 2 ? cfo[2][ed] : cfo[3][ed];
+        ro01 = f2{fmaf(Rpo, fo[0], fmaf(muo, yo[1], yo[0])), fmaf(Rpo, fo[1], fmaf(-muo, yo[1], yo[0]))};
+        ro23 = f2{fmaf(Rpo, fo[2], fmaf(muo, yo[2], yo[0])), fmaf(Rpo, fo[3], fmaf(-muo, yo[2], yo[0]))};
+#pragma unroll
+        for (int k = 0; k < FC; k++) {
+          const float mu = ymu[k];
 #pragma unroll
           for (int ed = 0; ed < 4; ed++) {
             const int t = 1 + (ed >> 1);
-            K01[k][ed] = f2{fmaf(sg(ed), xr[k][t], xr[k][0]), fmaf(sg(ed), xr[k][3 + t], xr[k][3])};
-            K2[k][ed] = fmaf(sg(ed), xr[k][6 + t], xr[k][6]);
+            const float se = (ed & 1) ? -mu : mu;
+            // y_own moves by K = X_sub,k (1, s_e on t(e)) per unit step of edge ed of contact k
+            const float K[3] = {fmaf(se, xr[k][t], xr[k][0]), fmaf(se, xr[k][3 + t], xr[k][3]),
+                                fmaf(se, xr[k][6 + t], xr[k][6])};
+            float c[4];
+#pragma unroll
+            for (int e2 = 0; e2 < 4; e2++) {
+              const float so = (e2 & 1) ? -muo : muo;
+              c[e2] = fmaf(so, K[1 + (e2 >> 1)], K[0]) + ((k == sub && e2 == ed) ? Rpo : 0.f);
+            }
+            C01[k][ed] = f2{c[0], c[1]}, C23[k][ed] = f2{c[2], c[3]};
           }
         }
       }
@@ -1116,32 +1141,24 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   // adds A_ed df_d to the later edges' residuals, so the dependent chain per edge is
   // mul -> max -> fma (df = max(-res/ARdiag, -f) is the projected step f' - f).
   auto yblock_contact = [&](const int j, float& improvement, f2& impq, float (&dsel)[4], auto coupled, auto pk) {
-    if constexpr (QUAD && decltype(pk)::value) {  // packed form; contact j's y lives in lane j of the quad
-      const float a = qbcast(yo[0], j), b = qbcast(yo[1], j), cc = qbcast(yo[2], j);
+    if constexpr (QUAD && decltype(pk)::value) {  // packed residual form; contact j's residuals live in lane j
       const f2 c01 = f2{cfo[j][0], cfo[j][1]}, c23 = f2{cfo[j][2], cfo[j][3]};
-      f2 r01 = fma2(splat2(yRp[j]), c01, fma2(qmu2[j], splat2(b), splat2(a)));
-      f2 r23 = fma2(splat2(yRp[j]), c23, fma2(qmu2[j], splat2(cc), splat2(a)));
+      const f2 r01 = f2{qbcast(ro01.x, j), qbcast(ro01.y, j)};
+      f2 r23 = f2{qbcast(ro23.x, j), qbcast(ro23.y, j)};
       const float df0 = max_neg(r01.x * -yia[j][0], c01.x);
       const float r1 = fmaf(yA[j][0], df0, r01.y);
       r23 = fma2(qA2030[j], splat2(df0), r23);
       const float df1 = max_neg(r1 * -yia[j][1], c01.y);
-      r23 = fma2(qA2131[j], splat2(df1), r23);
-      const float df2 = max_neg(r23.x * -yia[j][2], c23.x);
-      const float r3 = fmaf(yA[j][5], df2, r23.y);
+      const f2 r23b = fma2(qA2131[j], splat2(df1), r23);
+      const float df2 = max_neg(r23b.x * -yia[j][2], c23.x);
+      const float r3 = fmaf(yA[j][5], df2, r23b.y);
       const float df3 = max_neg(r3 * -yia[j][3], c23.y);
       const f2 d01 = f2{df0, df1}, d23 = f2{df2, df3};
       const f2 n01 = c01 + d01, n23 = c23 + d23;
       cfo[j][0] = n01.x, cfo[j][1] = n01.y, cfo[j][2] = n23.x, cfo[j][3] = n23.y;
       impq = fma2(-d01, fma2(qhd01[j], d01, f2{r01.x, r1}), impq);
-      impq = fma2(-d23, fma2(qhd23[j], d23, f2{r23.x, r3}), impq);
-      f2 y01 = f2{yo[0], yo[1]};
+      impq = fma2(-d23, fma2(qhd23[j], d23, f2{r23b.x, r3}), impq);
       const float dfs[4] = {df0, df1, df2, df3};
-#pragma unroll
-      for (int ed = 0; ed < 4; ed++) {
-        y01 = fma2(K01[j][ed], splat2(dfs[ed]), y01);
-        yo[2] = fmaf(K2[j][ed], dfs[ed], yo[2]);
-      }
-      yo[0] = y01.x, yo[1] = y01.y;
       if constexpr (decltype(coupled)::value) {  // y_E moves by X_jE D_j: lane j keeps its own
 #pragma unroll                                   // contact's steps, the quad sums them before E
         for (int ed = 0; ed < 4; ed++) dsel[ed] = sub == j ? dfs[ed] : dsel[ed];
@@ -1481,10 +1498,11 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
     const float D[3] = {(df[0] + df[1]) + (df[2] + df[3]), mu * (df[0] - df[1]), mu * (df[2] - df[3])};
     qvarm(xq.eWp, D);
     if constexpr (decltype(coupled)::value) {  // this lane's block contact moves by X_own,E D
-      f2 o01 = f2{yo[0], yo[1]};
 #pragma unroll
-      for (int qq = 0; qq < 3; qq++) o01 = fma2(xq.xop[qq], splat2(D[qq]), o01), yo[2] = fmaf(xq.xo[6 + qq], D[qq], yo[2]);
-      yo[0] = o01.x, yo[1] = o01.y;
+      for (int qq = 0; qq < 3; qq++) {
+        ro01 = fma2(xq.qe01[qq], splat2(D[qq]), ro01);
+        ro23 = fma2(xq.qe23[qq], splat2(D[qq]), ro23);
+      }
     }
     f2 e01 = f2{yE[0], yE[1]};
     float e2 = yE[2];
@@ -1520,7 +1538,10 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
     for (int t = 0; t < 9; t++) xq.xo[t] = EX(E_X + 9 * sub + t);
     xq.muo = sub == 0 ? ymu[0] : sub == 1 ? ymu[1] : sub == 2 ? ymu[2] : ymu[3];
 #pragma unroll
-    for (int qq = 0; qq < 3; qq++) xq.xop[qq] = f2{xq.xo[qq], xq.xo[3 + qq]};
+    for (int qq = 0; qq < 3; qq++) {  // residual form of X_own,E: rows (1, s_e on t(e)) of the own contact
+      xq.qe01[qq] = f2{fmaf(xq.muo, xq.xo[3 + qq], xq.xo[qq]), fmaf(-xq.muo, xq.xo[3 + qq], xq.xo[qq])};
+      xq.qe23[qq] = f2{fmaf(xq.muo, xq.xo[6 + qq], xq.xo[qq]), fmaf(-xq.muo, xq.xo[6 + qq], xq.xo[qq])};
+    }
     xq.fSh01 = f2{-EX(F_SH + 0), -EX(F_SH + 1)}, xq.fSh2 = -EX(F_SH + 2);
   };
   // one sweep step of the extra contact (after the friction rows and the block)
