@@ -311,10 +311,10 @@ def main():
         tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(tpath):
             traffic = json.load(open(tpath)).get(name, {}).get(kind)
-        # 64-lane waves, one lane per env (four per env in k_substep when the scene has a free
-        # body: quad mode, soarm_pgs.h lpe()): the kernel can occupy at most that many of the
-        # chip's 1024 SIMDs; the VALU peak those SIMDs can issue bounds it first
-        lanes = 4 if kind == "substep" and cm.desc.nq - cm.desc.nv == 1 else 1
+        # 64-lane waves, one lane per env (four per env in k_substep: quad mode, soarm_pgs.h
+        # lpe()): the kernel can occupy at most that many of the chip's 1024 SIMDs; the VALU
+        # peak those SIMDs can issue bounds it first
+        lanes = 4 if kind == "substep" else 1
         waves = -(-n * lanes // 64)
         capped = PEAK_FP32_TFLOPS * min(1.0, waves / 1024)
         roof = {"bound": "mfma", "achieved": achieved, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",

@@ -58,15 +58,20 @@ __device__ long long g_rowprof[65536 * 4];
 #endif
 
 constexpr int LDS_CON = 6;  // contacts whose rows stay in LDS
-// Lanes per env of the contact substep kernel for scenes with a free body: 4 lanes run the
-// same per-env code (identical values, so identical stores), and the contact-space sweep
-// of the cube block gives lane k ownership of block contact k's y (its cross-Gram row),
-// broadcasting y within the quad (DPP) on that contact's turn.
+// Lanes per env of the contact substep kernel: 4 lanes run the same per-env code
+// (identical values, so identical stores) and split the parts that fan out -- contact-row
+// construction, the warm start, the next substep's geom poses -- and, in scenes with a
+// free body, the contact-space sweep of the cube block gives lane k ownership of block
+// contact k's residuals (its cross-Gram row), broadcast within the quad (DPP) on that
+// contact's turn.  The arm-only scene has no block; its quad splits the other parts.
 #ifndef SOARM_LPE
 #define SOARM_LPE 4
 #endif
+#ifndef SOARM_LPE_ARM
+#define SOARM_LPE_ARM 4
+#endif
 template <int NF>
-constexpr int lpe() { return NF == 1 ? SOARM_LPE : 1; }
+constexpr int lpe() { return NF == 1 ? SOARM_LPE : SOARM_LPE_ARM; }
 // value of lane J of each quad (DPP quad_perm broadcast); J is a compile-time 0..3
 // projected Gauss-Seidel step of a pyramid edge, max(x, -f): one VOP3 max with a
 // negated source.  fmaxf(x, -f) on a loop-carried f costs an extra canonicalising
@@ -475,7 +480,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       }
   };
 
-  constexpr bool QUADR = lpe<NF>() == 4 && NF == 1 && CON;
+  constexpr bool QUADR = lpe<NF>() == 4 && CON;
   if constexpr (CON && QUADR) {
     if (ccount != nullptr) {
       // lane-split build (quad mode): every lane lists the env's contacts (pair, slot) in
@@ -1159,6 +1164,11 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       impq = fma2(-d01, fma2(qhd01[j], d01, f2{r01.x, r1}), impq);
       impq = fma2(-d23, fma2(qhd23[j], d23, f2{r23b.x, r3}), impq);
       const float dfs[4] = {df0, df1, df2, df3};
+#pragma unroll
+      for (int ed = 0; ed < 4; ed++) {  // this lane's residuals take the 4 steps
+        ro01 = fma2(C01[j][ed], splat2(dfs[ed]), ro01);
+        ro23 = fma2(C23[j][ed], splat2(dfs[ed]), ro23);
+      }
       if constexpr (decltype(coupled)::value) {  // y_E moves by X_jE D_j: lane j keeps its own
 #pragma unroll                                   // contact's steps, the quad sums them before E
         for (int ed = 0; ed < 4; ed++) dsel[ed] = sub == j ? dfs[ed] : dsel[ed];

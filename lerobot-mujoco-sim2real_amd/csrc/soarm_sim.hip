@@ -364,7 +364,7 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
   __shared__ float s_rows[(LDS_CON + 1) * CF][COLS];  // + one all-zero record
   __shared__ float s_lim[NA * LF][COLS];
   __shared__ float s_keep[keep_floats<NA, NF>()][COLS];
-  __shared__ float s_ext[NF == 1 ? XS_EXT : 1][COLS];  // y sweep: contact list, extra-contact slots
+  __shared__ float s_ext[NF == 1 ? XS_EXT : (lpe<NF>() == 4 ? XS_LIST : 1)][COLS];  // contact list (quad), y-sweep slots
   const RowLds L{&s_rows[0][0], &s_lim[0][0], NF == 1 ? &s_keep[0][0] : nullptr, &s_ext[0][0], (int)threadIdx.x,
                  (int)threadIdx.x / lpe<NF>(), COLS};
   const ContactRows<NA, NF> cr{scratch + e, n};
