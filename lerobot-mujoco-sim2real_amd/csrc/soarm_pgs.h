@@ -146,6 +146,24 @@ struct RowLds {
   DEVI float& ex(int k) const { return ext[k * cols + col]; }
 };
 
+// The env's pair-mask words, loaded at the top of the substep (they come from the previous
+// collide launch) so their round trip overlaps the smooth dynamics instead of starting the
+// contact-row build; `hold` pins them (the loads stay above, the registers are not sunk).
+// Zero (no contacts) unless loaded.
+struct PairMask {
+  static constexpr int MAXW = (SIM_MAXPAIR + 31) / 32;
+  uint32_t w[MAXW] = {};
+  DEVI void load(const uint32_t* __restrict__ pmask, int npair, int n, int e) {
+    const int nw = (npair + 31) >> 5;
+#pragma unroll
+    for (int k = 0; k < MAXW; k++) w[k] = k < nw ? soa(pmask, k, n, e) : 0u;
+  }
+  DEVI void hold() {
+#pragma unroll
+    for (int k = 0; k < MAXW; k++) asm volatile("" : "+v"(w[k]));
+  }
+};
+
 template <int NA, int NF>
 struct ContactRows {
   static constexpr int NV = NA + 6 * NF;
@@ -309,7 +327,7 @@ DEVI void gram_step(float* v6, const float* jn, const float* j1, const float* j2
 template <int NA, int NF, bool CON>
 DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const int* __restrict__ ccount,
                            const uint32_t* __restrict__ pmask, int n, int e, const RowLds& L,
-                           const ContactRows<NA, NF>& cr) {
+                           const ContactRows<NA, NF>& cr, const PairMask& pm) {
   constexpr int NV = Sim<NA, NF>::NV;
   const DModel& m = *S.mp;
   S.solve_m(S.qacc_s, S.fsmooth);
@@ -488,8 +506,9 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       // and writes each into the quad's 4 columns; overflow contacts (rare) are built by
       // every lane (identical values in the env's slab)
       const int nw = (m.npair + 31) >> 5;
-      for (int w = 0; w < nw; w++) {
-        uint32_t bits = soa(pmask, w, n, e);
+#pragma unroll
+      for (int w = 0; w < PairMask::MAXW; w++) {  // unrolled: pm->w[] stays in registers
+        uint32_t bits = w >= nw ? 0u : pm.w[w];
         while (bits) {
           const int p = 32 * w + __builtin_ctz(bits);
           bits &= bits - 1;
@@ -528,8 +547,9 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   } else if constexpr (CON) {
     if (ccount != nullptr) {
       const int nw = (m.npair + 31) >> 5;
-      for (int w = 0; w < nw; w++) {
-        uint32_t bits = soa(pmask, w, n, e);
+#pragma unroll
+      for (int w = 0; w < PairMask::MAXW; w++) {  // unrolled: pm->w[] stays in registers
+        uint32_t bits = w >= nw ? 0u : pm.w[w];
         while (bits) {
           const int p = 32 * w + __builtin_ctz(bits);
           bits &= bits - 1;

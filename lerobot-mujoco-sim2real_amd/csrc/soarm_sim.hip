@@ -216,13 +216,15 @@ __device__ unsigned long long g_phase[61];  // [53..56] contact-row build split 
 // (cbuf/ccount, may be null) were produced by k_collide from this substep's positions
 template <int NA, int NF, bool CON>
 DEVI int forward(Sim<NA, NF>& S, const float* cbuf, const int* ccount, const uint32_t* pmask, int n, int e,
-                 const RowLds& L, const ContactRows<NA, NF>& cr, const float* applied = nullptr) {
+                 const RowLds& L, const ContactRows<NA, NF>& cr, const float* applied = nullptr,
+                 PairMask pm = PairMask{}) {
   S.kinematics();
   S.com_crb();
   S.factor();
   S.smooth_forces();
+  pm.hold();
   if (applied) S.add_applied(applied, n, e);
-  return solve_constraints<NA, NF, CON>(S, cbuf, ccount, pmask, n, e, L, cr);
+  return solve_constraints<NA, NF, CON>(S, cbuf, ccount, pmask, n, e, L, cr, pm);
 }
 
 // mj_resetData zeroes d.qfrc_applied: a reset / soft reset of env e clears its row
@@ -379,6 +381,8 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
   }
   // a soft reset moved the env: the collide output no longer applies
   const bool use = S.status == st0 && ccount != nullptr;
+  PairMask pm;
+  if (use) pm.load(pmask, m.npair, n, e);  // (stays zero otherwise: no contact list)
 #ifdef SOARM_PHASE_PROF
   PHASE_T(t1);
   PSTAMP(0);
@@ -392,11 +396,12 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
   PSTAMP(4);
   PHASE_T(t2);
   PSTAMP(5);
+  pm.hold();
   if (AP) S.add_applied(st.qfrc_applied, n, e);
-  int ncon = solve_constraints<NA, NF, true>(S, use ? cbuf : nullptr, use ? ccount : nullptr, pmask, n, e, L, cr);
+  int ncon = solve_constraints<NA, NF, true>(S, use ? cbuf : nullptr, use ? ccount : nullptr, pmask, n, e, L, cr, pm);
 #else
   int ncon = forward<NA, NF, true>(S, use ? cbuf : nullptr, use ? ccount : nullptr, pmask, n, e, L, cr,
-                                   AP ? st.qfrc_applied : nullptr);
+                                   AP ? st.qfrc_applied : nullptr, pm);
 #endif
   if (S.acc_bad()) {
     S.soft_reset(SIM_ST_BADQACC);

@@ -46,7 +46,12 @@ struct Sim {
     for (int b = 1; b < 2 + NA; b++) {
       const int p = b - 1;  // base's parent is the world; chain is serial
       float R[9], t[3], pos[3], q[4];
-      q2m(R, xquat[p]);
+      if (p == 0) {
+        R[0] = R[4] = R[8] = 1.f, R[1] = R[2] = R[3] = R[5] = R[6] = R[7] = 0.f;
+      } else {  // the parent's frame, converted from its final quaternion in its own iteration
+#pragma unroll
+        for (int k = 0; k < 9; k++) R[k] = xmat[p][k];
+      }
       const float bp[3] = {m.body_pos[b][0], m.body_pos[b][1], m.body_pos[b][2]};
       mv(t, R, bp);
       pos[0] = xpos[p][0] + t[0], pos[1] = xpos[p][1] + t[1], pos[2] = xpos[p][2] + t[2];
