@@ -270,17 +270,20 @@ __global__ __launch_bounds__(64) void k_step(const DModel* __restrict__ dm, int 
   if (obs) write_obs(S, obs, e);
 }
 
-// geom world poses from the current qpos (collision input)
+// geom world poses from the current qpos (collision input); GEOM_LPE lanes per env split
+// the geoms (the FK chain runs on each of them)
+constexpr int GEOM_LPE = 4;
 template <int NA, int NF>
 __global__ __launch_bounds__(64) void k_geom(const DModel* __restrict__ dm, int n, sim_state st,
                                              float* __restrict__ gpose) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const int e = blockIdx.x * (64 / GEOM_LPE) + (int)threadIdx.x / GEOM_LPE;
   if (e >= n) return;
   Sim<NA, NF> S(dm, 1.f, -1.f, 1.f);
   load_state(S, st, n, e);
   S.kinematics();
-  write_geom_poses(S, gpose, n, e);
+  write_geom_poses(S, gpose, n, e, (int)threadIdx.x % GEOM_LPE, GEOM_LPE);
 }
+inline dim3 geom_grid(int n) { return dim3((n + 64 / GEOM_LPE - 1) / (64 / GEOM_LPE)); }
 
 // mj_collision, one lane per (env, candidate pair); blockIdx.y = pair
 __global__ __launch_bounds__(256, 3) void k_collide(const DModel* __restrict__ dm, int n,
@@ -432,9 +435,6 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
     write_obs(S, obs, e);
   }
   PSTAMP(13);
-#ifdef SOARM_EXP_NOGPOSE
-  gpose = nullptr;
-#endif
   if (gpose) {
     S.kinematics();
     PSTAMP(14);
@@ -1214,7 +1214,7 @@ int sim_step(sim_batch* b, const sim_state* s, const float* action, int frame_sk
     dispatch_nf(b->model->nf, [&](auto nfc) {
       constexpr int NA = 6, NF = decltype(nfc)::value;
       prof_mark(b, 3, q);
-      hipLaunchKernelGGL((k_geom<NA, NF>), grid_for(b->n), dim3(64), 0, q, b->d_model, b->n, *s,
+      hipLaunchKernelGGL((k_geom<NA, NF>), geom_grid(b->n), dim3(64), 0, q, b->d_model, b->n, *s,
                          b->d_gpose);
       prof_mark(b, -1, q);
       for (int sub = 0; sub < frame_skip; sub++) {
@@ -1294,7 +1294,7 @@ int sim_contacts(sim_batch* b, const sim_state* s, float* out, int32_t* ncon, vo
   const int np = b->model->desc.npair;
   dispatch_nf(b->model->nf, [&](auto nfc) {
     constexpr int NA = 6, NF = decltype(nfc)::value;
-    hipLaunchKernelGGL((k_geom<NA, NF>), grid_for(b->n), dim3(64), 0, st, b->d_model, b->n, *s,
+    hipLaunchKernelGGL((k_geom<NA, NF>), geom_grid(b->n), dim3(64), 0, st, b->d_model, b->n, *s,
                        b->d_gpose);
   });
   if (np > 0)
@@ -1317,7 +1317,7 @@ int sim_collide_profile(sim_batch* b, const sim_state* s, double* cycles, void* 
   HIPCHECK(hipMemsetAsync(d_cyc, 0, 2 * np * sizeof(unsigned long long), st));
   dispatch_nf(b->model->nf, [&](auto nfc) {
     constexpr int NA = 6, NF = decltype(nfc)::value;
-    hipLaunchKernelGGL((k_geom<NA, NF>), grid_for(b->n), dim3(64), 0, st, b->d_model, b->n, *s,
+    hipLaunchKernelGGL((k_geom<NA, NF>), geom_grid(b->n), dim3(64), 0, st, b->d_model, b->n, *s,
                        b->d_gpose);
   });
   launch_collide(b, st, d_cyc);
