@@ -74,12 +74,20 @@ struct PairOut {
 // neighbour while one improves; each step loads all candidates' records together (their
 // coordinates to compare, their neighbour ids for the next step), so a step is one
 // dependent round trip.  Same comparisons, order and result as a CSR walk.
+// (the hull tables are read through global-address-space pointers: the DModel holds them as
+// plain pointers, which would otherwise compile to flat loads)
+template <class T>
+using gptr = const __attribute__((address_space(1))) T*;
+DEVI uint4 ldg(gptr<uint4> p, int i) {  // (dword loads, merged into one 16-B load)
+  const gptr<uint32_t> q = (gptr<uint32_t>)(p + i);
+  return make_uint4(q[0], q[1], q[2], q[3]);
+}
 DEVI float3 hull_support(const DModel& m, int g, const float l[3]) {
-  const uint4* rec = m.hull_rec + 2 * m.geom_hulladr[g];
-  const uint4* lr = m.hull_lutrec + HULL_LUTREC * (m.geom_lutadr[g] + lut_cell(l[0], l[1], l[2]));
-  uint4 r0 = lr[0], r1 = lr[1], nb[8];
+  const gptr<uint4> rec = (gptr<uint4>)m.hull_rec + 2 * m.geom_hulladr[g];
+  const gptr<uint4> lr = (gptr<uint4>)m.hull_lutrec + HULL_LUTREC * (m.geom_lutadr[g] + lut_cell(l[0], l[1], l[2]));
+  uint4 r0 = ldg(lr, 0), r1 = ldg(lr, 1), nb[8];
 #pragma unroll
-  for (int k = 0; k < 8; k++) nb[k] = lr[2 + k];
+  for (int k = 0; k < 8; k++) nb[k] = ldg(lr, 2 + k);
   const int nvert = m.geom_hullnum[g];
   auto dotr = [&](const uint4& r) {
     return l[0] * __uint_as_float(r.x) + l[1] * __uint_as_float(r.y) + l[2] * __uint_as_float(r.z);
@@ -98,7 +106,7 @@ DEVI float3 hull_support(const DModel& m, int g, const float l[3]) {
 #pragma unroll
     for (int k = 0; k < 8; k++)
       if (k == best) u = nb[k].w;
-    r0 = rec[2 * u], r1 = rec[2 * u + 1], cd = nd;
+    r0 = ldg(rec, 2 * u), r1 = ldg(rec, 2 * u + 1), cd = nd;
   }
   for (int guard = 0; guard < nvert; guard++) {
     const uint32_t ids[4] = {r1.x, r1.y, r1.z, r1.w};
@@ -106,7 +114,7 @@ DEVI float3 hull_support(const DModel& m, int g, const float l[3]) {
 #pragma unroll
     for (int k = 0; k < 8; k++) {
       const uint32_t u = (ids[k >> 1] >> (16 * (k & 1))) & 0xffffu;
-      c0[k] = rec[2 * u], c1[k] = rec[2 * u + 1];
+      c0[k] = ldg(rec, 2 * u), c1[k] = ldg(rec, 2 * u + 1);
     }
     float nd = cd;
     int best = -1;
@@ -121,12 +129,12 @@ DEVI float3 hull_support(const DModel& m, int g, const float l[3]) {
       if (k == best) b0 = c0[k], b1 = c1[k];
     const int deg = (int)(r0.w & 255u);
     if (deg > 8) {  // hub vertex (~2%): the rest of its neighbours, 8 per round trip
-      const uint16_t* ov = m.hull_ovf + (r0.w >> 8);
+      const gptr<uint16_t> ov = (gptr<uint16_t>)m.hull_ovf + (r0.w >> 8);
       for (int a = 8; a < deg; a += 8) {
 #pragma unroll
         for (int k = 0; k < 8; k++) {
           const uint32_t u = (a + k < deg) ? ov[a - 8 + k] : ov[a - 8];
-          c0[k] = rec[2 * u], c1[k] = rec[2 * u + 1];
+          c0[k] = ldg(rec, 2 * u), c1[k] = ldg(rec, 2 * u + 1);
         }
 #pragma unroll
         for (int k = 0; k < 8; k++) {
@@ -159,7 +167,7 @@ DEVI float support_ub(const DModel& m, int g, const float l[3]) {
   const float fu = fminf(fmaxf((u + mx) * s, 0.f), (float)HULL_SB_K), fv = fminf(fmaxf((v + mx) * s, 0.f), (float)HULL_SB_K);
   const int i = min((int)fu, HULL_SB_K - 1), j = min((int)fv, HULL_SB_K - 1);
   const float a = fu - i, b = fv - j;
-  const float* t = m.hull_sb + m.geom_sbadr[g] + face * HULL_SB_FACE + i * (HULL_SB_K + 1) + j;
+  const gptr<float> t = (gptr<float>)m.hull_sb + m.geom_sbadr[g] + face * HULL_SB_FACE + i * (HULL_SB_K + 1) + j;
   const float h00 = t[0], h10 = t[HULL_SB_K + 1], h01 = t[1], h11 = t[HULL_SB_K + 2];
   const float q = (a + b <= 1.f) ? (1.f - a - b) * h00 + a * h10 + b * h01
                                  : (a + b - 1.f) * h11 + (1.f - a) * h01 + (1.f - b) * h10;

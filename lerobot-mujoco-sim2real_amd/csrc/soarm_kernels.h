@@ -31,8 +31,12 @@
 // those of an earlier access, so no per-lane address stays live between the two
 template <class T>
 DEVI T* launder(T* p) {
-  asm volatile("" : "+s"(p));
-  return p;
+  // laundered as a global-address-space pointer, so address-space inference still emits
+  // global (not flat) accesses through the result: a flat store counts against lgkmcnt as
+  // well, and every later LDS / scalar-load wait would then also wait for it to land
+  auto g = (__attribute__((address_space(1))) T*)p;
+  asm volatile("" : "+s"(g));
+  return (T*)g;
 }
 template <class T>
 DEVI T& soa(T* p, int r, int n, int e) {

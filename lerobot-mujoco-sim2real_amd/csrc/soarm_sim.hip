@@ -414,9 +414,8 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
   }
   PSTAMP(10);
   if constexpr (NF == 1) {  // reload (laundered pointers: not CSE'd with the first load)
-    const float* qp = st.qpos;
-    const float* qv = st.qvel;
-    asm volatile("" : "+s"(qp), "+s"(qv));
+    const float* qp = launder(st.qpos);
+    const float* qv = launder(st.qvel);
 #pragma unroll
     for (int i = 0; i < Sim<NA, NF>::NQ; i++) S.qpos[i] = soa(qp, i, n, e);
 #pragma unroll

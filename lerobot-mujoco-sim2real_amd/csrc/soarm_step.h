@@ -35,7 +35,11 @@ struct Sim {
   float fsmooth[NV], qacc_s[NV], qacc[NV], fcon[NV];
 
   DEVI Sim(const DModel* m_, float ms, float fr, float ds) : mp(m_), mscale(ms), fric(fr), dscale(ds) {}
-  DEVI void relaunder() { asm volatile("" : "+s"(mp)); }
+  DEVI void relaunder() {  // (through the constant address space: the model stays scalar-loaded)
+    auto c = (__attribute__((address_space(4))) const DModel*)mp;
+    asm volatile("" : "+s"(c));
+    mp = (const DModel*)c;
+  }
 
   // ---------------------------------------------------------------- mj_kinematics
   DEVI void kinematics() {
