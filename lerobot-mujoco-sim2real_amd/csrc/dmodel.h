@@ -51,6 +51,11 @@ struct DModel {
   int pair_slot[MAXP];  // first contact slot of the pair in the collide output
   int pair_body1[MAXP], pair_body2[MAXP];  // geom_bodyid of the pair's geoms
   int pair_cap[MAXP];                      // contact slots of the pair (1 or PAIR_MAXCON)
+  // multi-contact pairs (cap > 1, at most 16): index q into the collide output's count word,
+  // which holds (contacts - 1) in bits 2q, 2q+1 (-1: single-contact pair, a set mask bit is
+  // its one contact); the count word follows the presence words in pmask
+  int pair_cq[MAXP];
+  int ncq;
   int nslot;            // total contact slots (sum of per-pair capacities)
   int free_diag;        // every free body has ipos = 0 and iquat = 1: its 6x6 M block is diagonal
 
@@ -85,6 +90,9 @@ struct DModel {
   const float* hull_sb;
   int geom_sbadr[MAXG];
 };
+
+// words per env of the collide output's pair mask: presence bits, then the count word
+__host__ __device__ inline int pmask_words(const DModel& m) { return ((m.npair + 31) >> 5) + (m.ncq > 0 ? 1 : 0); }
 
 // Support-point start table: a cube map of HULL_LUT_K x HULL_LUT_K cells per
 // face; each cell holds the hull's argmax vertex for the cell-centre

@@ -150,17 +150,25 @@ struct RowLds {
 // collide launch) so their round trip overlaps the smooth dynamics instead of starting the
 // contact-row build; `hold` pins them (the loads stay above, the registers are not sunk).
 // Zero (no contacts) unless loaded.
+// cw: the count word of the multi-contact pairs (DModel::pair_cq), so the contact list needs
+// no per-pair count load.
 struct PairMask {
   static constexpr int MAXW = (SIM_MAXPAIR + 31) / 32;
-  uint32_t w[MAXW] = {};
-  DEVI void load(const uint32_t* __restrict__ pmask, int npair, int n, int e) {
-    const int nw = (npair + 31) >> 5;
+  uint32_t w[MAXW] = {}, cw = 0u;
+  DEVI void load(const uint32_t* __restrict__ pmask, const DModel& m, int n, int e) {
+    const int nw = (m.npair + 31) >> 5;
 #pragma unroll
     for (int k = 0; k < MAXW; k++) w[k] = k < nw ? soa(pmask, k, n, e) : 0u;
+    if (m.ncq > 0) cw = soa(pmask, nw, n, e);
   }
   DEVI void hold() {
 #pragma unroll
     for (int k = 0; k < MAXW; k++) asm volatile("" : "+v"(w[k]));
+    asm volatile("" : "+v"(cw));
+  }
+  DEVI int count(const DModel& m, int p) const {
+    const int cq = m.pair_cq[p];
+    return cq < 0 ? 1 : (int)((cw >> (2 * cq)) & 3u) + 1;
   }
 };
 
@@ -512,7 +520,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
         while (bits) {
           const int p = 32 * w + __builtin_ctz(bits);
           bits &= bits - 1;
-          const int cnt = soa(ccount, p, n, e);
+          const int cnt = pm.count(m, p);
           for (int k = 0; k < cnt; k++) {
             if (ncon >= SIM_MAXCON) {
               S.status |= SIM_ST_CONOVERFLOW;
@@ -557,7 +565,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
           // the pair's constants and every slot it may fill (cap <= PAIR_MAXCON; a set mask
           // bit means at least one contact, and slots past the count are never used)
           RP_MARK(3);
-          const int cnt = soa(ccount, p, n, e);
+          const int cnt = pm.count(m, p);
           const int s0 = m.pair_slot[p], cap = m.pair_cap[p];
           const int b1 = m.pair_body1[p], b2 = m.pair_body2[p];
           const float mu = S.fric >= 0.f ? S.fric : m.pair_friction[p];

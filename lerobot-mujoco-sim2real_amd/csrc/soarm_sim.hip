@@ -302,7 +302,11 @@ __global__ __launch_bounds__(256, 3) void k_collide(const DModel* __restrict__ d
   PairOut o{cbuf, n, e, m.pair_slot[p], m.pair_cap[p], 0};
   collide_pair(m, p, P1, P2, o);
   soa(ccount, p, n, e) = o.n;
-  if (o.n > 0) atomicOr(&pmask[(size_t)(p >> 5) * n + e], 1u << (p & 31));
+  if (o.n > 0) {
+    atomicOr(&pmask[(size_t)(p >> 5) * n + e], 1u << (p & 31));
+    const int cq = m.pair_cq[p];
+    if (cq >= 0) atomicOr(&pmask[(size_t)((m.npair + 31) >> 5) * n + e], (uint32_t)(o.n - 1) << (2 * cq));
+  }
   if (pcyc && (threadIdx.x & 63) == 0) {
     const unsigned long long dt = (unsigned long long)(clock64() - t0);
     atomicAdd(&pcyc[p], dt);
@@ -385,7 +389,7 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
   // a soft reset moved the env: the collide output no longer applies
   const bool use = S.status == st0 && ccount != nullptr;
   PairMask pm;
-  if (use) pm.load(pmask, m.npair, n, e);  // (stays zero otherwise: no contact list)
+  if (use) pm.load(pmask, m, n, e);  // (stays zero otherwise: no contact list)
 #ifdef SOARM_PHASE_PROF
   PHASE_T(t1);
   PSTAMP(0);
@@ -422,7 +426,7 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
     for (int i = 0; i < Sim<NA, NF>::NV; i++) S.qvel[i] = soa(qv, i, n, e);
   }
   if (pmask)  // consumed: clear for the next collide
-    for (int w = 0; w < (m.npair + 31) >> 5; w++) soa(pmask, w, n, e) = 0u;
+    for (int w = 0; w < pmask_words(m); w++) soa(pmask, w, n, e) = 0u;
   const float ee[3] = {S.ee[0], S.ee[1], S.ee[2]};
   PSTAMP(11);
   S.integrate();
@@ -502,7 +506,7 @@ __global__ __launch_bounds__(64) void k_gather(const DModel* __restrict__ dm, in
                                                float* __restrict__ out, int* __restrict__ nout) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
-  for (int w = 0; w < (dm->npair + 31) >> 5; w++) soa(pmask, w, n, e) = 0u;
+  for (int w = 0; w < pmask_words(*dm); w++) soa(pmask, w, n, e) = 0u;
   __shared__ float s_con[SIM_MAXCON * 8][64];
   const ConLds C{s_con, (int)threadIdx.x};
   int status = 0;
@@ -864,9 +868,11 @@ static int validate_and_build(const sim_model_desc& d, sim_model* M) {
     const int cap = (t2 == SIM_GEOM_BOX && (t1 == SIM_GEOM_BOX || t1 == SIM_GEOM_PLANE)) ? 4 : 1;
     m.pair_slot[p] = m.nslot;
     m.pair_cap[p] = cap;
+    m.pair_cq[p] = cap > 1 ? m.ncq++ : -1;
     m.pair_body1[p] = d.geom_bodyid[g1], m.pair_body2[p] = d.geom_bodyid[g2];
     m.nslot += cap;
   }
+  if (m.ncq > 16) return fail(SIM_E_MODEL, "more than 16 box-box / plane-box pairs");
   // free bodies: the kernels use a diagonal 6x6 mass block, which needs the inertia frame at
   // the body frame (ipos = 0, iquat = identity) — true for the build-defined cube
   m.free_diag = 1;
@@ -1134,7 +1140,7 @@ int sim_batch_create(const sim_model* m, int n_envs, int device, sim_batch** out
     HIPCHECK(hipMalloc(&B->d_gpose, (size_t)m->desc.ngeom * 12 * n_envs * sizeof(float)));
     HIPCHECK(hipMalloc(&B->d_cbuf, (size_t)(m->dm.nslot > 0 ? m->dm.nslot : 1) * 7 * n_envs * sizeof(float)));
     HIPCHECK(hipMalloc(&B->d_ccount, (size_t)(m->desc.npair > 0 ? m->desc.npair : 1) * n_envs * sizeof(int)));
-    const size_t nw = (size_t)((m->desc.npair + 31) / 32 > 0 ? (m->desc.npair + 31) / 32 : 1);
+    const size_t nw = (size_t)std::max(pmask_words(m->dm), 1);
     HIPCHECK(hipMalloc(&B->d_pmask, nw * n_envs * sizeof(uint32_t)));
     HIPCHECK(hipMemset(B->d_pmask, 0, nw * n_envs * sizeof(uint32_t)));
   }
@@ -1320,7 +1326,7 @@ int sim_collide_profile(sim_batch* b, const sim_state* s, double* cycles, void* 
                        b->d_gpose);
   });
   launch_collide(b, st, d_cyc);
-  HIPCHECK(hipMemsetAsync(b->d_pmask, 0, (size_t)((np + 31) / 32) * b->n * sizeof(uint32_t), st));
+  HIPCHECK(hipMemsetAsync(b->d_pmask, 0, (size_t)pmask_words(b->model->dm) * b->n * sizeof(uint32_t), st));
   std::vector<unsigned long long> h(2 * np);
   HIPCHECK(hipMemcpyAsync(h.data(), d_cyc, 2 * np * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
   HIPCHECK(hipStreamSynchronize(st));
