@@ -13,18 +13,24 @@ Per frame k of a T-frame reference ``state_all_ref = [cartesian xyz, joint angle
 :class:`KoopmanMPCTracking` runs that loop for n envs on one GPU with no host round trip:
 ``sim_bias`` writes ``qfrc_applied`` in place, the reference is lifted and turned into per-frame
 feedforward terms once (the reference recomputes the same lifted rows every frame), then each
-frame is ``sim_bias`` + ``sim_koopman_mpc_step`` + ``sim_step``.  The viewer drawing, the
-return-to-home playback after the last frame (:137-175) and the ZMQ send to the robot (:186-190)
-are out of scope.
+frame is ``sim_bias`` + ``sim_koopman_mpc_step`` + ``sim_step``.  With a ``communicator``
+(``utility.ZMQ.ZMQCommunicator``) each frame also publishes env ``stream_env_id``'s joint angles
+as real-robot targets, as the reference does after its step (:186-190).  The viewer drawing
+and the return-to-home playback after the last frame (:137-175) are out of scope.
 """
 from .sim import BatchSim
+from .utility.ZMQ import stream_env
 
 
 class KoopmanMPCTracking:
     """n envs tracking their own reference trajectories with one MPCController."""
 
-    def __init__(self, controller, model, cartesian_points, joint_angle_traj, device=0, sim=None):
+    def __init__(self, controller, model, cartesian_points, joint_angle_traj, device=0, sim=None,
+                 communicator=None, stream_env_id=0):
         import torch
+
+        self.communicator = communicator
+        self.stream_env_id = stream_env_id
 
         self.torch = torch
         self.ctl = controller
@@ -61,6 +67,8 @@ class KoopmanMPCTracking:
         self.sim.bias(out=self.sim.qfrc_applied)
         self.ctl.step(self.state, self.ff[k], self.u_prev, self.action)
         self.state = self.sim.step(self.action)
+        if self.communicator is not None:  # sim -> real (Koopman_MPC.py:186-190)
+            stream_env(self.sim, self.communicator, self.stream_env_id)
         self.traj_index += 1
         return self.state
 

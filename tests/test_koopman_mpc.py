@@ -15,12 +15,17 @@ Weights are random (the reference's checkpoint is not used: DESIGN.md §9 record
 the reference's initialisers (control/koopman.py).
 """
 import ctypes as C
+import json
+import math
 
 import numpy as np
 import pytest
 
 import koopman_mpc as KO
 from oracle import Oracle
+
+import soarm_pkg  # noqa: F401
+from lerobot_mujoco_sim2real_amd.utility.ZMQ import ZMQCommunicator, real_targets, sim_to_real
 
 RNG = np.random.default_rng(11)
 LAYERS = [8, 64, 64, 64, 64, 24]
@@ -241,7 +246,8 @@ def test_tracking_loop_matches_oracle(gpu_lib, arm_model):
     cart = np.stack([0.3 + 0.0 * t[:, None] + 0 * phase, 0.1 * np.cos(t[:, None] + phase),
                      0.15 + 0.05 * np.sin(t[:, None] + phase)], -1)
     jq = RNG.uniform(-0.3, 0.3, (1, n, 5)) + 0.1 * np.sin(t[:, None, None] + phase[None, :, None])
-    run = KoopmanMPCTracking(ctl, arm_model, cart, jq)
+    sent = _Sink()
+    run = KoopmanMPCTracking(ctl, arm_model, cart, jq, communicator=ZMQCommunicator(socket=sent), stream_env_id=3)
     sref = run.state_all_ref.cpu().numpy().astype(np.float64)
     zref = KO.encode(layers, sref.reshape(T * n, 8)).reshape(T, n, -1)
     orc = Oracle(arm_model)
@@ -261,4 +267,43 @@ def test_tracking_loop_matches_oracle(gpu_lib, arm_model):
         oc = orc.step(st, run.action.cpu().numpy().astype(np.float64), applied=applied)
         err = np.abs(obs - oc)
         assert np.median(err) < 2e-6 and err.max() < 1e-3, (k, np.median(err), err.max())
+        # sim -> real: env 3's qpos[:6] after the step, degrees minus joint_offsets (:186-190)
+        q = run.sim.qpos[:6, 3].double().cpu().numpy()
+        assert json.loads(sent.msgs[-1]) == real_targets(q) and len(sent.msgs) == k + 1
     assert int(run.sim.status.abs().sum()) == 0
+
+
+class _Sink:
+    """Stands in for the PUB socket: records what would be published."""
+
+    def __init__(self):
+        self.msgs = []
+
+    def send_string(self, s):
+        self.msgs.append(s)
+
+
+def test_sim_to_real_payload():
+    """The published list equals the reference's conversion (Koopman_MPC.py:16-27,186-189):
+    degrees(qpos[:6]) - joint_offsets, JSON-encoded by send_data (utility/ZMQ.py:36-51)."""
+    q = [0.1, -0.2, 0.3, 0.0, 1.0, -0.5]
+    expect = [math.degrees(v) - o for v, o in zip(q, [0, 0, 0, 0, 0, -41.97])]
+    assert real_targets(q) == expect
+    assert sim_to_real([10.0, 0, 0, 0, 0, 0.0]) == [10.0, 0, 0, 0, 0, 41.97]
+    sink = _Sink()
+    c = ZMQCommunicator(socket=sink)
+    c.send_data(expect)
+    assert sink.msgs == [json.dumps(expect)]
+    c.cleanup()
+    c.send_data(expect)  # no socket: nothing sent (the reference prints and returns)
+    assert len(sink.msgs) == 1
+
+
+def test_zmq_transport_fails_loudly_without_pyzmq():
+    try:
+        import zmq  # noqa: F401
+    except ImportError:
+        with pytest.raises(ImportError, match="pyzmq"):
+            ZMQCommunicator("tcp://127.0.0.1:5555")
+    else:
+        pytest.skip("pyzmq present")
