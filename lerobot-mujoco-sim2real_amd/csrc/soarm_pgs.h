@@ -1025,7 +1025,8 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   // (j = sub: the contact's own 3x3 Gram block), full 3x3 per j
   float yo[3] = {0.f, 0.f, 0.f}, xr[QUAD ? FC : 1][9];
   // quad mode, packed: this lane's contact's 4 edge residuals r_e = y_0 + s_e y_t(e) + R f_e
-  // (pairs (r0, r1), (r2, r3)); the sweep broadcasts them instead of y
+  // (pairs (r0, r1), (r2, r3)), held scaled by -1/ARdiag_e (see sA10 below); the sweep
+  // broadcasts them instead of y
   f2 ro01 = f2{0.f, 0.f}, ro23 = f2{0.f, 0.f};
   // rows of the arm block of M^-1 as dof pairs (packed v_arm updates of the friction rows)
   f2 Mp[NA][NA / 2];
@@ -1105,6 +1106,19 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   // residuals' update per edge of contact j: C_e'e = (1, s'_e' on t(e')) X_sub,j (1, s_e on
   // t(e)) + R delta (own contact), as pairs over e': r_own += C_.e df_e
   f2 qA2030[FC], qA2131[FC], qhd01[FC], qhd23[FC], C01[QUAD ? FC : 1][4], C23[QUAD ? FC : 1][4];
+  // quad mode, packed: the residuals are carried scaled, s_e = -r_e / ARdiag_e, so the projected
+  // step is df = max(s_e, -f_e) with no multiply on the chain; the edge-Gram entries that move
+  // a later edge e' are pre-scaled by -1/ARdiag_e' (sA10 = -A10/ARdiag1, sA32, qA2030, qA2131)
+  float sA10[FC], sA32[FC];
+  // this lane's own block contact (quad mode): -1/ARdiag of its 4 edges as pairs
+  auto own_nia01 = [&]() {
+    return f2{-(sub == 0 ? yia[0][0] : sub == 1 ? yia[1][0] : sub == 2 ? yia[2][0] : yia[3][0]),
+              -(sub == 0 ? yia[0][1] : sub == 1 ? yia[1][1] : sub == 2 ? yia[2][1] : yia[3][1])};
+  };
+  auto own_nia23 = [&]() {
+    return f2{-(sub == 0 ? yia[0][2] : sub == 1 ? yia[1][2] : sub == 2 ? yia[2][2] : yia[3][2]),
+              -(sub == 0 ? yia[0][3] : sub == 1 ? yia[1][3] : sub == 2 ? yia[2][3] : yia[3][3])};
+  };
   auto yblock_consts = [&](auto pk) {
     if constexpr (NF == 1 && CON) {
 #pragma unroll
@@ -1134,7 +1148,9 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
           for (int d = 0; d < ed; d++)
             yA[k][q++] = G[0] + sg(ed) * gt(ed) + sg(d) * gt(d) + sg(ed) * sg(d) * gtt(ed, d);
         if constexpr (QUAD && decltype(pk)::value) {
-          qA2030[k] = f2{yA[k][1], yA[k][3]}, qA2131[k] = f2{yA[k][2], yA[k][4]};
+          sA10[k] = -yia[k][1] * yA[k][0], sA32[k] = -yia[k][3] * yA[k][5];
+          qA2030[k] = f2{-yia[k][2] * yA[k][1], -yia[k][3] * yA[k][3]};
+          qA2131[k] = f2{-yia[k][2] * yA[k][2], -yia[k][3] * yA[k][4]};
           qhd01[k] = f2{yhd[k][0], yhd[k][1]}, qhd23[k] = f2{yhd[k][2], yhd[k][3]};
         }
       }
@@ -1147,6 +1163,8 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
         for (int ed = 0; ed < 4; ed++) fo[ed] = sub == 0 ? cfo[0][ed] : sub == 1 ? cfo[1][ed] : sub == 2 ? cfo[2][ed] : cfo[3][ed];
         ro01 = f2{fmaf(Rpo, fo[0], fmaf(muo, yo[1], yo[0])), fmaf(Rpo, fo[1], fmaf(-muo, yo[1], yo[0]))};
         ro23 = f2{fmaf(Rpo, fo[2], fmaf(muo, yo[2], yo[0])), fmaf(Rpo, fo[3], fmaf(-muo, yo[2], yo[0]))};
+        const f2 nio01 = own_nia01(), nio23 = own_nia23();
+        ro01 = ro01 * nio01, ro23 = ro23 * nio23;  // scaled: s_e = -r_e / ARdiag_e
 #pragma unroll
         for (int k = 0; k < FC; k++) {
           const float mu = ymu[k];
@@ -1163,7 +1181,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
               const float so = (e2 & 1) ? -muo : muo;
               c[e2] = fmaf(so, K[1 + (e2 >> 1)], K[0]) + ((k == sub && e2 == ed) ? Rpo : 0.f);
             }
-            C01[k][ed] = f2{c[0], c[1]}, C23[k][ed] = f2{c[2], c[3]};
+            C01[k][ed] = f2{c[0], c[1]} * nio01, C23[k][ed] = f2{c[2], c[3]} * nio23;
           }
         }
       }
@@ -1176,21 +1194,22 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   auto yblock_contact = [&](const int j, float& improvement, f2& impq, float (&dsel)[4], auto coupled, auto pk) {
     if constexpr (QUAD && decltype(pk)::value) {  // packed residual form; contact j's residuals live in lane j
       const f2 c01 = f2{cfo[j][0], cfo[j][1]}, c23 = f2{cfo[j][2], cfo[j][3]};
-      const f2 r01 = f2{qbcast(ro01.x, j), qbcast(ro01.y, j)};
-      f2 r23 = f2{qbcast(ro23.x, j), qbcast(ro23.y, j)};
-      const float df0 = max_neg(r01.x * -yia[j][0], c01.x);
-      const float r1 = fmaf(yA[j][0], df0, r01.y);
-      r23 = fma2(qA2030[j], splat2(df0), r23);
-      const float df1 = max_neg(r1 * -yia[j][1], c01.y);
-      const f2 r23b = fma2(qA2131[j], splat2(df1), r23);
-      const float df2 = max_neg(r23b.x * -yia[j][2], c23.x);
-      const float r3 = fmaf(yA[j][5], df2, r23b.y);
-      const float df3 = max_neg(r3 * -yia[j][3], c23.y);
+      const f2 s01 = f2{qbcast(ro01.x, j), qbcast(ro01.y, j)};  // scaled residuals of contact j
+      f2 s23 = f2{qbcast(ro23.x, j), qbcast(ro23.y, j)};
+      const float df0 = max_neg(s01.x, c01.x);
+      const float s1 = fmaf(sA10[j], df0, s01.y);
+      s23 = fma2(qA2030[j], splat2(df0), s23);
+      const float df1 = max_neg(s1, c01.y);
+      const f2 s23b = fma2(qA2131[j], splat2(df1), s23);
+      const float df2 = max_neg(s23b.x, c23.x);
+      const float s3 = fmaf(sA32[j], df2, s23b.y);
+      const float df3 = max_neg(s3, c23.y);
       const f2 d01 = f2{df0, df1}, d23 = f2{df2, df3};
       const f2 n01 = c01 + d01, n23 = c23 + d23;
       cfo[j][0] = n01.x, cfo[j][1] = n01.y, cfo[j][2] = n23.x, cfo[j][3] = n23.y;
-      impq = fma2(-d01, fma2(qhd01[j], d01, f2{r01.x, r1}), impq);
-      impq = fma2(-d23, fma2(qhd23[j], d23, f2{r23b.x, r3}), impq);
+      // improvement -df (r + ARdiag df / 2) with r = -ARdiag s = -2 hd s: -(hd df)(df - 2 s)
+      impq = fma2(-(qhd01[j] * d01), fma2(f2{s01.x, s1}, splat2(-2.f), d01), impq);
+      impq = fma2(-(qhd23[j] * d23), fma2(f2{s23b.x, s3}, splat2(-2.f), d23), impq);
       const float dfs[4] = {df0, df1, df2, df3};
 #pragma unroll
       for (int ed = 0; ed < 4; ed++) {  // this lane's residuals take the 4 steps
@@ -1576,9 +1595,10 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
     for (int t = 0; t < 9; t++) xq.xo[t] = EX(E_X + 9 * sub + t);
     xq.muo = sub == 0 ? ymu[0] : sub == 1 ? ymu[1] : sub == 2 ? ymu[2] : ymu[3];
 #pragma unroll
-    for (int qq = 0; qq < 3; qq++) {  // residual form of X_own,E: rows (1, s_e on t(e)) of the own contact
-      xq.qe01[qq] = f2{fmaf(xq.muo, xq.xo[3 + qq], xq.xo[qq]), fmaf(-xq.muo, xq.xo[3 + qq], xq.xo[qq])};
-      xq.qe23[qq] = f2{fmaf(xq.muo, xq.xo[6 + qq], xq.xo[qq]), fmaf(-xq.muo, xq.xo[6 + qq], xq.xo[qq])};
+    for (int qq = 0; qq < 3; qq++) {  // residual form of X_own,E: rows (1, s_e on t(e)) of the own
+                                      // contact, scaled by its -1/ARdiag as the residuals are
+      xq.qe01[qq] = f2{fmaf(xq.muo, xq.xo[3 + qq], xq.xo[qq]), fmaf(-xq.muo, xq.xo[3 + qq], xq.xo[qq])} * own_nia01();
+      xq.qe23[qq] = f2{fmaf(xq.muo, xq.xo[6 + qq], xq.xo[qq]), fmaf(-xq.muo, xq.xo[6 + qq], xq.xo[qq])} * own_nia23();
     }
     xq.fSh01 = f2{-EX(F_SH + 0), -EX(F_SH + 1)}, xq.fSh2 = -EX(F_SH + 2);
   };
