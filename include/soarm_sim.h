@@ -265,7 +265,7 @@ int sim_contacts(sim_batch* b, const sim_state* s, float* out, int32_t* ncon, vo
 int sim_collide_profile(sim_batch* b, const sim_state* s, double* cycles, void* stream);
 
 /* diagnostic: summed wave cycles per phase of the contact substep kernel in a
-   build compiled with -DSOARM_PHASE_PROF (out[61]; the first 19: load, smooth dynamics, rows,
+   build compiled with -DSOARM_PHASE_PROF (out[77]; the first 19: load, smooth dynamics, rows,
    PGS, integrate+output, waves, sum of PGS sweeps over envs, envs, max wave
    cycles, waves on the register fast path, max wave PGS cycles, sum of per-wave
    max sweeps, waves with an active limit / a non-block contact / contact

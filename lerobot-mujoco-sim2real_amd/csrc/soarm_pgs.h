@@ -90,6 +90,9 @@ DEVI float max_neg(float x, float f) {
   asm("v_max_f32_e64 %0, %1, -%2" : "=v"(r) : "v"(x), "v"(f));
   return r;
 }
+// re-define a value in a VGPR (an empty asm): starts a new live range at this point
+DEVI void vpin(float& x) { asm volatile("" : "+v"(x)); }
+DEVI void vpin(f2& x) { asm volatile("" : "+v"(x)); }
 DEVI float qbcast(float x, int j) {
   const int b = __float_as_int(x);
   switch (j) {
@@ -1763,6 +1766,19 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       }
     }
     if constexpr (RETIRE) {
+      // the block-only sweeps hold far fewer values than the sweeps with the arm's rows:
+      // re-define the block's loop constants here (an empty asm per value) so they get
+      // registers of their own for this loop instead of the AGPR homes they were given
+      // under the first loop's pressure (one copy here, not an AGPR read per sweep)
+      if constexpr (PK::value) {
+#pragma unroll
+        for (int k = 0; k < FC; k++) {
+          vpin(qA2030[k]), vpin(qA2131[k]), vpin(qhd01[k]), vpin(qhd23[k]), vpin(sA10[k]), vpin(sA32[k]);
+#pragma unroll
+          for (int ed = 0; ed < 4; ed++) vpin(C01[k][ed]), vpin(C23[k][ed]), vpin(cfo[k][ed]);
+        }
+        vpin(ro01), vpin(ro23);
+      }
       if (!done)
         for (; it < m.iterations; it++) {
           float unused = 0.f;
@@ -1855,7 +1871,8 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
     g_pgs_prof[8 * e + 1] = clock64(), g_pgs_prof[8 * e + 2] = nsweep,
     g_pgs_prof[8 * e + 3] = (ypure ? 0 : yext ? 1 : block_first ? 2 : 3) | (npost > 0 && npost_free ? 16 : 0) |
                             (min(npost, 3) << 8) | (min(nfree_x, 3) << 12) | ((nl > 5) << 16) | ((nlim > 0) << 17) |
-                            ((nl != ncon) << 18) | ((long long)min(armstop, 255) << 20),
+                            ((nl != ncon) << 18) | ((long long)min(armstop, 255) << 20) |
+                            ((long long)(yext ? 4 + 2 * yext2 + ycoupled : 0) << 28),
     g_pgs_prof[8 * e + 4] = nlim, g_pgs_prof[8 * e + 5] = ncon;
 #endif
 

@@ -204,9 +204,12 @@ DEVI void write_obs(const Sim<NA, NF>& S, float* obs, int e) {
 //   [19..22] waves per sweep variant (y-pure, y+arm slot, block-first general, other),
 //   [23..26] max wave cycles per variant, [27] waves with a non-block contact on the free body
 //   [28..42] wave cycles between consecutive fine stamps (g_stamp, see PSTAMP sites)
-__device__ unsigned long long g_phase[61];  // [53..56] contact-row build split (g_rowprof),
+__device__ unsigned long long g_phase[77];  // [53..56] contact-row build split (g_rowprof),
                                             // [57] waves that retired the arm rows, [58] sum of their retire sweeps,
                                             // [59] / [60] max wave cycles of the waves that did not / did retire
+                                            // y+arm slot waves by (F slot, E coupled to the cube) = 2 F + coupled:
+                                            // [61..64] waves, [65..68] max wave cycles, [69..72] sum of PGS
+                                            // cycles, [73..76] sum of the arm-retire sweep (0: not retired)
 #define PHASE_T(v) const long long v = clock64()
 #else
 #define PHASE_T(v)
@@ -495,6 +498,13 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
     const int ast = (int)((g_pgs_prof[8 * e + 3] >> 20) & 255);
     if (ast) atomicAdd(&g_phase[57], 1ull), atomicAdd(&g_phase[58], (unsigned long long)ast);
     atomicMax(&g_phase[ast ? 60 : 59], (unsigned long long)(t5 - t0));
+    const int xv = (int)((g_pgs_prof[8 * e + 3] >> 28) & 7);
+    if (xv >= 4) {
+      atomicAdd(&g_phase[61 + xv - 4], 1ull);
+      atomicMax(&g_phase[65 + xv - 4], (unsigned long long)(t5 - t0));
+      atomicAdd(&g_phase[69 + xv - 4], (unsigned long long)(p1 - p0));
+      atomicAdd(&g_phase[73 + xv - 4], (unsigned long long)ast);
+    }
   }
 #endif
 }
@@ -1338,12 +1348,12 @@ int sim_collide_profile(sim_batch* b, const sim_state* s, double* cycles, void* 
 int sim_phase_profile(double* out, int reset) {
   if (!out) return fail(SIM_E_ARG, "null output");
 #ifdef SOARM_PHASE_PROF
-  unsigned long long h[61];
+  unsigned long long h[77];
   HIPCHECK(hipDeviceSynchronize());
   HIPCHECK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_phase), sizeof(h)));
-  for (int k = 0; k < 61; k++) out[k] = (double)h[k];
+  for (int k = 0; k < 77; k++) out[k] = (double)h[k];
   if (reset) {
-    const unsigned long long z[61] = {};
+    const unsigned long long z[77] = {};
     HIPCHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof(z)));
   }
   return SIM_OK;

@@ -44,7 +44,7 @@ q0 = W.initial_qpos(cm, ids, 0)
 sim.reset(init_qpos=q0[:, :5], extra_qpos=q0, seed=0)
 tab = {k: (torch.as_tensor(v, dtype=torch.float32, device="cuda") if isinstance(v, np.ndarray) else v)
        for k, v in W.chirp_tables(ids, 0).items()}
-out = (ctypes.c_double * 61)()
+out = (ctypes.c_double * 77)()
 res = {}
 every = int(os.environ.get("EVERY", 0))
 starts = set(range(0, T, every)) if every else {0, T // 2, T - 10}
@@ -84,6 +84,10 @@ for t in range(T):
         r["armstop_waves"] = v[57] / max(v[5], 1)
         r["mean_armstop_sweep"] = v[58] / max(v[57], 1)
         r["max_wave_cycles_kept_retired"] = [v[59], v[60]]
+        r["yarm_subvariants"] = {k: {"waves": v[61 + i], "max_cycles": v[65 + i],
+                                     "mean_pgs_cycles": v[69 + i] / max(v[61 + i], 1),
+                                     "mean_retire_sweep": v[73 + i] / max(v[61 + i], 1)}
+                                 for i, k in enumerate(["E", "E_coupled", "EF", "EF_coupled"])}
         res[t] = r
         print(t, json.dumps(r), flush=True)
 json.dump(res, open(os.path.join(ROOT, "gpurun_out", f"phase_prof_{os.environ.get('CONFIG', 'contact')}.json"), "w"), indent=1)
