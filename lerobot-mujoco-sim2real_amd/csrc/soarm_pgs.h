@@ -85,6 +85,13 @@ constexpr int lpe() { return NF == 1 ? SOARM_LPE : SOARM_LPE_ARM; }
 typedef float f2 __attribute__((ext_vector_type(2)));
 DEVI f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 DEVI f2 splat2(float x) { return f2{x, x}; }
+// a * (b.y, b.y) + c: the high half of a pair splatted by op_sel (the compiler copies it to a
+// low half first)
+DEVI f2 fma2_hi(f2 a, f2 b, f2 c) {
+  f2 r;
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[1,1,1]" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
 DEVI float max_neg(float x, float f) {
   float r;
   asm("v_max_f32_e64 %0, %1, -%2" : "=v"(r) : "v"(x), "v"(f));
@@ -1199,26 +1206,28 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       const f2 c01 = f2{cfo[j][0], cfo[j][1]}, c23 = f2{cfo[j][2], cfo[j][3]};
       const f2 s01 = f2{qbcast(ro01.x, j), qbcast(ro01.y, j)};  // scaled residuals of contact j
       f2 s23 = f2{qbcast(ro23.x, j), qbcast(ro23.y, j)};
-      const float df0 = max_neg(s01.x, c01.x);
-      const float s1 = fmaf(sA10[j], df0, s01.y);
-      s23 = fma2(qA2030[j], splat2(df0), s23);
-      const float df1 = max_neg(s1, c01.y);
-      const f2 s23b = fma2(qA2131[j], splat2(df1), s23);
-      const float df2 = max_neg(s23b.x, c23.x);
-      const float s3 = fmaf(sA32[j], df2, s23b.y);
-      const float df3 = max_neg(s3, c23.y);
-      const f2 d01 = f2{df0, df1}, d23 = f2{df2, df3};
+      // the steps are built in their pairs d01, d23 and splatted from a pair half (op_sel),
+      // so no register copy sits between a step and the packed updates that consume it
+      f2 d01, d23;
+      d01.x = max_neg(s01.x, c01.x);
+      const float s1 = fmaf(sA10[j], d01.x, s01.y);
+      s23 = fma2(qA2030[j], d01.xx, s23);
+      d01.y = max_neg(s1, c01.y);
+      const f2 s23b = fma2_hi(qA2131[j], d01, s23);
+      d23.x = max_neg(s23b.x, c23.x);
+      const float s3 = fmaf(sA32[j], d23.x, s23b.y);
+      d23.y = max_neg(s3, c23.y);
       const f2 n01 = c01 + d01, n23 = c23 + d23;
       cfo[j][0] = n01.x, cfo[j][1] = n01.y, cfo[j][2] = n23.x, cfo[j][3] = n23.y;
       // improvement -df (r + ARdiag df / 2) with r = -ARdiag s = -2 hd s: -(hd df)(df - 2 s)
       impq = fma2(-(qhd01[j] * d01), fma2(f2{s01.x, s1}, splat2(-2.f), d01), impq);
       impq = fma2(-(qhd23[j] * d23), fma2(f2{s23b.x, s3}, splat2(-2.f), d23), impq);
-      const float dfs[4] = {df0, df1, df2, df3};
-#pragma unroll
-      for (int ed = 0; ed < 4; ed++) {  // this lane's residuals take the 4 steps
-        ro01 = fma2(C01[j][ed], splat2(dfs[ed]), ro01);
-        ro23 = fma2(C23[j][ed], splat2(dfs[ed]), ro23);
-      }
+      const float dfs[4] = {d01.x, d01.y, d23.x, d23.y};
+      // this lane's residuals take the 4 steps
+      ro01 = fma2(C01[j][0], d01.xx, ro01), ro23 = fma2(C23[j][0], d01.xx, ro23);
+      ro01 = fma2_hi(C01[j][1], d01, ro01), ro23 = fma2_hi(C23[j][1], d01, ro23);
+      ro01 = fma2(C01[j][2], d23.xx, ro01), ro23 = fma2(C23[j][2], d23.xx, ro23);
+      ro01 = fma2_hi(C01[j][3], d23, ro01), ro23 = fma2_hi(C23[j][3], d23, ro23);
       if constexpr (decltype(coupled)::value) {  // y_E moves by X_jE D_j: lane j keeps its own
 #pragma unroll                                   // contact's steps, the quad sums them before E
         for (int ed = 0; ed < 4; ed++) dsel[ed] = sub == j ? dfs[ed] : dsel[ed];
