@@ -1024,8 +1024,8 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   // quad mode: the E/F coefficients preloaded into registers before the sweeps, in the
   // register pairs the packed loop consumes (no memory reads inside the sweep loop)
   struct ExtQ {
-    float eIA[4], fIA[4], muo, eA10, eA32, fA10, fA32, eMu, eRp, fMu, fRp, fJ2[6], fX2[3], eG2[3], xo[9], fSh2;
-    f2 eWp[9], eA2030, eA2131, fA2030, fA2131, eHD01, eHD23, fHD01, fHD23, fJp[6], fWp[9], fXp[3], eGp[3], qe01[3], qe23[3], fSh01;
+    float muo, eA10, eA32, fA10, fA32, eMu, eRp, fMu, fRp, fJ2[6], fX2[3], eG2[3], xo[9], fSh2;
+    f2 eNia01, eNia23, fNia01, fNia23, eWp[9], eA2030, eA2131, fA2030, fA2131, eHD01, eHD23, fHD01, fHD23, fJp[6], fWp[9], fXp[3], eGp[3], qe01[3], qe23[3], fSh01;
   } xq;
   constexpr int NX = FC * (FC - 1) / 2;
   float yb[FC][3], xg[NX > 0 ? NX : 1][9];
@@ -1512,24 +1512,27 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
     }
   };
   // quad mode, packed: one edge chain (pyramid of 4 edges) from y = (a, b, c)
-  auto qchain = [&](float a, float b, float c, float (&f)[4], float mu, float Rp, const float (&ia)[4], float A10,
+  // scaled residuals as in the block (s = -r / ARdiag; nia = -1/ARdiag per edge, the A's
+  // pre-scaled by the -1/ARdiag of the edge they move), steps built in their pairs
+  auto qchain = [&](float a, float b, float c, float (&f)[4], float mu, float Rp, f2 nia01, f2 nia23, float A10,
                     f2 A2030, f2 A2131, float A32, f2 hd01, f2 hd23, f2& imp, float (&df)[4]) {
     const f2 c01 = f2{f[0], f[1]}, c23 = f2{f[2], f[3]};
-    f2 r01 = fma2(splat2(Rp), c01, fma2(f2{mu, -mu}, splat2(b), splat2(a)));
-    f2 r23 = fma2(splat2(Rp), c23, fma2(f2{mu, -mu}, splat2(c), splat2(a)));
-    df[0] = max_neg(r01.x * -ia[0], c01.x);
-    const float r1 = fmaf(A10, df[0], r01.y);
-    r23 = fma2(A2030, splat2(df[0]), r23);
-    df[1] = max_neg(r1 * -ia[1], c01.y);
-    r23 = fma2(A2131, splat2(df[1]), r23);
-    df[2] = max_neg(r23.x * -ia[2], c23.x);
-    const float r3 = fmaf(A32, df[2], r23.y);
-    df[3] = max_neg(r3 * -ia[3], c23.y);
-    const f2 d01 = f2{df[0], df[1]}, d23 = f2{df[2], df[3]};
+    const f2 s01 = fma2(splat2(Rp), c01, fma2(f2{mu, -mu}, splat2(b), splat2(a))) * nia01;
+    f2 s23 = fma2(splat2(Rp), c23, fma2(f2{mu, -mu}, splat2(c), splat2(a))) * nia23;
+    f2 d01, d23;
+    d01.x = max_neg(s01.x, c01.x);
+    const float s1 = fmaf(A10, d01.x, s01.y);
+    s23 = fma2(A2030, d01.xx, s23);
+    d01.y = max_neg(s1, c01.y);
+    s23 = fma2_hi(A2131, d01, s23);
+    d23.x = max_neg(s23.x, c23.x);
+    const float s3 = fmaf(A32, d23.x, s23.y);
+    d23.y = max_neg(s3, c23.y);
+    df[0] = d01.x, df[1] = d01.y, df[2] = d23.x, df[3] = d23.y;
     const f2 n01 = c01 + d01, n23 = c23 + d23;
     f[0] = n01.x, f[1] = n01.y, f[2] = n23.x, f[3] = n23.y;
-    imp = fma2(-d01, fma2(hd01, d01, f2{r01.x, r1}), imp);
-    imp = fma2(-d23, fma2(hd23, d23, f2{r23.x, r3}), imp);
+    imp = fma2(-(hd01 * d01), fma2(f2{s01.x, s1}, splat2(-2.f), d01), imp);
+    imp = fma2(-(hd23 * d23), fma2(f2{s23.x, s3}, splat2(-2.f), d23), imp);
   };
   // v_arm += W D with W as dof pairs (W[q] row pairs)
   auto qvarm = [&](const f2 (&Wp)[9], const float (&D)[3]) {
@@ -1547,7 +1550,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
 #pragma unroll
     for (int i = 0; i < NA; i++) y01 = fma2(xq.fJp[i], splat2(v[i]), y01), y2 = fmaf(xq.fJ2[i], v[i], y2);
     float df[4];
-    qchain(y01.x, y01.y, y2, fF, xq.fMu, xq.fRp, xq.fIA, xq.fA10, xq.fA2030, xq.fA2131, xq.fA32, xq.fHD01, xq.fHD23,
+    qchain(y01.x, y01.y, y2, fF, xq.fMu, xq.fRp, xq.fNia01, xq.fNia23, xq.fA10, xq.fA2030, xq.fA2131, xq.fA32, xq.fHD01, xq.fHD23,
            imp, df);
     famax += (fabsf(df[0]) + fabsf(df[1])) + (fabsf(df[2]) + fabsf(df[3]));
     const float mu = xq.fMu;
@@ -1560,7 +1563,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   };
   auto yext_row_q = [&](f2& imp, auto coupled, float& famax) {
     float df[4];
-    qchain(yE[0], yE[1], yE[2], fE, xq.eMu, xq.eRp, xq.eIA, xq.eA10, xq.eA2030, xq.eA2131, xq.eA32, xq.eHD01, xq.eHD23,
+    qchain(yE[0], yE[1], yE[2], fE, xq.eMu, xq.eRp, xq.eNia01, xq.eNia23, xq.eA10, xq.eA2030, xq.eA2131, xq.eA32, xq.eHD01, xq.eHD23,
            imp, df);
     if constexpr (!decltype(coupled)::value) famax += (fabsf(df[0]) + fabsf(df[1])) + (fabsf(df[2]) + fabsf(df[3]));
     const float mu = xq.eMu;
@@ -1588,12 +1591,15 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
         xq.eWp[3 * q + k] = f2{EX(E_W + 6 * q + 2 * k), EX(E_W + 6 * q + 2 * k + 1)};
         xq.fWp[3 * q + k] = f2{EX(F_W + 6 * q + 2 * k), EX(F_W + 6 * q + 2 * k + 1)};
       }
+    float eia[4], fia[4];  // -1/ARdiag of the E and F edges
 #pragma unroll
-    for (int ed = 0; ed < 4; ed++) xq.eIA[ed] = EX(E_IA + ed), xq.fIA[ed] = EX(F_IA + ed);
-    xq.eA10 = EX(E_A + 0), xq.eA2030 = f2{EX(E_A + 1), EX(E_A + 3)}, xq.eA2131 = f2{EX(E_A + 2), EX(E_A + 4)};
-    xq.eA32 = EX(E_A + 5);
-    xq.fA10 = EX(F_A + 0), xq.fA2030 = f2{EX(F_A + 1), EX(F_A + 3)}, xq.fA2131 = f2{EX(F_A + 2), EX(F_A + 4)};
-    xq.fA32 = EX(F_A + 5);
+    for (int ed = 0; ed < 4; ed++) eia[ed] = -EX(E_IA + ed), fia[ed] = -EX(F_IA + ed);
+    xq.eNia01 = f2{eia[0], eia[1]}, xq.eNia23 = f2{eia[2], eia[3]};
+    xq.fNia01 = f2{fia[0], fia[1]}, xq.fNia23 = f2{fia[2], fia[3]};
+    xq.eA10 = eia[1] * EX(E_A + 0), xq.eA32 = eia[3] * EX(E_A + 5);
+    xq.eA2030 = f2{eia[2] * EX(E_A + 1), eia[3] * EX(E_A + 3)}, xq.eA2131 = f2{eia[2] * EX(E_A + 2), eia[3] * EX(E_A + 4)};
+    xq.fA10 = fia[1] * EX(F_A + 0), xq.fA32 = fia[3] * EX(F_A + 5);
+    xq.fA2030 = f2{fia[2] * EX(F_A + 1), fia[3] * EX(F_A + 3)}, xq.fA2131 = f2{fia[2] * EX(F_A + 2), fia[3] * EX(F_A + 4)};
     xq.eHD01 = f2{EX(E_HD + 0), EX(E_HD + 1)}, xq.eHD23 = f2{EX(E_HD + 2), EX(E_HD + 3)};
     xq.fHD01 = f2{EX(F_HD + 0), EX(F_HD + 1)}, xq.fHD23 = f2{EX(F_HD + 2), EX(F_HD + 3)};
     xq.eMu = EX(E_MU), xq.eRp = EX(E_RP), xq.fMu = EX(F_MUX), xq.fRp = EX(F_RPX);
