@@ -1897,6 +1897,27 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
     S.qacc[i] = v[i];
     S.fcon[i] = 0.f;
   }
+  if constexpr (CON) {
+    // qacc = qacc_smooth + M^-1 J' f, so J' f = M qacc - qfrc_smooth (M qacc_smooth = qfrc_smooth):
+    // the Euler step's right-hand side qfrc_smooth + qfrc_constraint is M qacc.  One 6x6 product
+    // (+ the free bodies' diagonal blocks) instead of J' f over every contact row; equal in exact
+    // arithmetic, fp32 rounding apart (the oracle keeps J' f).
+#pragma unroll
+    for (int i = 0; i < NA; i++) {
+      float sacc = -S.fsmooth[i];
+#pragma unroll
+      for (int k = 0; k < NA; k++) sacc = fmaf(S.MA[i >= k ? i * (i + 1) / 2 + k : k * (k + 1) / 2 + i], v[k], sacc);
+      S.fcon[i] = sacc;
+    }
+#pragma unroll
+    for (int f = 0; f < NF; f++)
+#pragma unroll
+      for (int i = 0; i < 6; i++) {
+        const int d = NA + 6 * f + i;
+        S.fcon[d] = fmaf(S.MF[f][i * (i + 1) / 2 + i], v[d], -S.fsmooth[d]);
+      }
+    return ncon;
+  }
 #pragma unroll
   for (int i = 0; i < NA; i++) S.fcon[i] += ff[i];
   for (int l = 0; l < nlim; l++) {
