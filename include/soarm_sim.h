@@ -51,6 +51,8 @@ extern "C" {
 /* MuJoCo enum values (mjtJoint, mjtGeom) */
 enum { SIM_JNT_FREE = 0, SIM_JNT_BALL = 1, SIM_JNT_SLIDE = 2, SIM_JNT_HINGE = 3 };
 enum { SIM_GEOM_PLANE = 0, SIM_GEOM_SPHERE = 2, SIM_GEOM_BOX = 6, SIM_GEOM_MESH = 7 };
+/* mjtSolver values */
+enum { SIM_SOL_PGS = 0, SIM_SOL_CG = 1, SIM_SOL_NEWTON = 2 };
 
 /* error codes */
 enum {
@@ -82,11 +84,14 @@ typedef struct sim_model_desc {
   double timestep;
   double gravity[3];
   double impratio;
-  double tolerance;      /* solver: stop when the cost improvement is below this */
-  int32_t iterations;    /* solver: max PGS sweeps */
+  double tolerance;      /* solver: stop when the scaled cost improvement is below this */
+  double meaninertia;    /* mjStatistic.meaninertia = trace(M(qpos0)) / nv (mj_setConst): the
+                            solvers' stopping tests scale by 1 / (meaninertia * max(1, nv)) */
+  int32_t iterations;    /* solver: max PGS sweeps / Newton iterations */
   int32_t disable_contact; /* mjDSBL_CONTACT */
   int32_t disable_eulerdamp;
-  int32_t _pad0;
+  int32_t solver;        /* mjtSolver: SIM_SOL_PGS (the kernels) or SIM_SOL_NEWTON (MuJoCo's
+                            default; CPU oracle only — sim_model_create rejects it) */
 
   /* bodies (0 = world) */
   int32_t body_parentid[SIM_MAXBODY];

@@ -12,6 +12,7 @@ MAXGEOM, MAXPAIR, MAXSITE, MAXU, MAXOBSQ = 40, 160, 4, 8, 8
 MAXCON = 16
 
 JNT_FREE, JNT_BALL, JNT_SLIDE, JNT_HINGE = 0, 1, 2, 3
+SOL_PGS, SOL_CG, SOL_NEWTON = 0, 1, 2
 GEOM_PLANE, GEOM_SPHERE, GEOM_BOX, GEOM_MESH = 0, 2, 6, 7
 
 ST_BADQPOS, ST_BADQVEL, ST_BADQACC, ST_CONOVERFLOW = 1, 2, 4, 8
@@ -30,7 +31,8 @@ class ModelDesc(C.Structure):
         ("nbody", i32), ("njnt", i32), ("nq", i32), ("nv", i32), ("nu", i32),
         ("ngeom", i32), ("nsite", i32), ("npair", i32), ("nhullvert", i32), ("nhulladj", i32),
         ("timestep", f64), ("gravity", _a(f64, 3)), ("impratio", f64), ("tolerance", f64),
-        ("iterations", i32), ("disable_contact", i32), ("disable_eulerdamp", i32), ("_pad0", i32),
+        ("meaninertia", f64),
+        ("iterations", i32), ("disable_contact", i32), ("disable_eulerdamp", i32), ("solver", i32),
         # bodies
         ("body_parentid", _a(i32, MAXBODY)), ("body_rootid", _a(i32, MAXBODY)),
         ("body_weldid", _a(i32, MAXBODY)), ("body_jntnum", _a(i32, MAXBODY)),

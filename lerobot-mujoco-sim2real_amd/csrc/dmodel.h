@@ -20,7 +20,7 @@ struct DModel {
   int nq, nv, nu, ngeom, npair, nact, obs_site, obs_nq;
   int obs_qadr[SIM_MAXOBSQ];
   int iterations, disable_contact, eulerdamp, nhullvert;
-  float timestep, impratio, tolerance, _pad0;
+  float timestep, impratio, tolerance, pgs_scale;  // pgs_scale = 1 / (meaninertia * max(1, nv))
   float gravity[4];
 
   // bodies

@@ -736,15 +736,9 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
 #ifdef SOARM_PHASE_PROF
   if (e < 65536) g_pgs_prof[8 * e + 7] = clock64();  // warm start + cost done
 #endif
-  // ---- projected Gauss-Seidel sweeps (MuJoCo improvement criterion, scaled by 1/trace(M))
-  float tr = 0.f;
-#pragma unroll
-  for (int i = 0; i < NA; i++) tr += S.MA[i * (i + 1) / 2 + i];
-#pragma unroll
-  for (int f2 = 0; f2 < NF; f2++)
-#pragma unroll
-    for (int i = 0; i < 6; i++) tr += S.MF[f2][i * (i + 1) / 2 + i];
-  const float scale = 1.f / tr;
+  // ---- projected Gauss-Seidel sweeps (mj_solPGS's improvement criterion, scaled by the model
+  // constant 1 / (meaninertia * max(1, nv)), meaninertia = trace(M(qpos0)) / nv)
+  const float scale = m.pgs_scale;
   if (L.keep) {  // park what only the post-solve stages need (restored below)
     int k = 0;
 #pragma unroll

@@ -770,6 +770,8 @@ static int validate_and_build(const sim_model_desc& d, sim_model* M) {
     nf++;
   }
   if (na != 6 || nf > 1) return fail(SIM_E_MODEL, "kernels are compiled for a 6-hinge arm + <=1 free body");
+  if (d.solver != SIM_SOL_PGS)
+    return fail(SIM_E_MODEL, "the kernels run the PGS solver (north star); Newton is CPU-oracle only");
   if (d.nv != na + 6 * nf || d.nq != na + 7 * nf) return fail(SIM_E_MODEL, "nq/nv mismatch");
   if (d.nu > na) return fail(SIM_E_MODEL, "more actuators than arm hinges");
   for (int a = 0; a < d.nu; a++)
@@ -801,6 +803,7 @@ static int validate_and_build(const sim_model_desc& d, sim_model* M) {
   m.nhullvert = d.nhullvert;
   m.timestep = (float)d.timestep, m.impratio = (float)d.impratio;
   m.tolerance = (float)d.tolerance;
+  m.pgs_scale = (float)(1.0 / ((d.meaninertia > 1e-15 ? d.meaninertia : 1.0) * std::max(1, d.nv)));
   for (int k = 0; k < 3; k++) m.gravity[k] = (float)d.gravity[k];
   for (int b2 = 0; b2 < d.nbody; b2++) {
     for (int k = 0; k < 3; k++) {

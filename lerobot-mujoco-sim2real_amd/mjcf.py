@@ -272,8 +272,13 @@ def _load_hulls(path=None):
 
 def compile_mjcf(xml_path=SCENE_XML, kv=None, disable_contact=False, iterations=100,
                  tolerance=1e-8, obs_site="gripperframe",
-                 obs_joints=("shoulder_pan", "shoulder_lift", "elbow_flex", "wrist_flex", "wrist_roll")):
-    """Compile an MJCF file into a :class:`CompiledModel`."""
+                 obs_joints=("shoulder_pan", "shoulder_lift", "elbow_flex", "wrist_flex", "wrist_roll"),
+                 solver="PGS"):
+    """Compile an MJCF file into a :class:`CompiledModel`.
+
+    solver: "PGS" (what the HIP kernels run, per BASELINE.json north_star) or "Newton"
+    (MuJoCo's default, which the reference scene's missing <option> selects; only the CPU
+    oracle runs it — sim_model_create rejects it)."""
     if not os.path.exists(xml_path):
         raise FileNotFoundError(f"MuJoCo XML file not found: {xml_path}")
     root = _load_tree(xml_path)
@@ -318,6 +323,10 @@ def compile_mjcf(xml_path=SCENE_XML, kv=None, disable_contact=False, iterations=
     d.impratio = float(opt.get("impratio", 1.0))
     d.tolerance = tolerance
     d.iterations = iterations
+    sol = {"pgs": abi.SOL_PGS, "newton": abi.SOL_NEWTON}
+    if str(solver).lower() not in sol:
+        raise ValueError(f"solver must be PGS or Newton, not {solver!r}")
+    d.solver = sol[str(solver).lower()]
     d.disable_contact = int(bool(disable_contact))
 
     # ---- walk bodies depth-first; worldbody sections merged in order
@@ -667,6 +676,8 @@ def compile_mjcf(xml_path=SCENE_XML, kv=None, disable_contact=False, iterations=
     kin.forward_position(q0)
     M = kin.mass_matrix()
     Minv = np.linalg.inv(M) if nv else np.zeros((0, 0))
+    # mjStatistic.meaninertia: mean diagonal of M at qpos0 (armature included)
+    d.meaninertia = float(np.trace(M) / nv) if nv else 1.0
     for bid in range(1, nbody):
         jp, jr = kin.jac(kin.xipos[bid], bid)
         J = np.vstack([jp, jr])

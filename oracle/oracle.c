@@ -6,6 +6,7 @@
 #include "oracle.h"
 
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 #ifdef _OPENMP
 #include <omp.h>
@@ -593,6 +594,12 @@ void orc_solver_stats(double* out, int reset) {
   }
 }
 
+/* stopping-test scale of MuJoCo's solvers: 1 / (mjStatistic.meaninertia * max(1, nv)) */
+static double solver_scale(const sim_model_desc* m) {
+  const double mi = m->meaninertia > MINVAL ? m->meaninertia : 1.0;
+  return 1.0 / (mi * (m->nv > 1 ? m->nv : 1));
+}
+
 /* ------------------------------------------------ PGS dual solver [ext mj_solPGS] */
 static double project(int type, double f, double fl) {
   if (type == ORC_EFC_FRICTION) return f < -fl ? -fl : (f > fl ? fl : f);
@@ -647,10 +654,9 @@ void orc_solve_pgs(const orc_model* om, orc_data* d) {
     for (int r = 0; r < ne; r++) f[r] = 0;
     memcpy(v, d->qacc_smooth, nv * sizeof(double));
   }
-  /* Gauss-Seidel sweeps with projection */
-  double scale = 0;
-  for (int i = 0; i < nv; i++) scale += d->M[i][i];
-  scale = (scale > MINVAL) ? 1.0 / (scale / (nv > 0 ? nv : 1) * (nv > 1 ? nv : 1)) : 1.0;
+  /* Gauss-Seidel sweeps with projection; mj_solPGS stops when the sweep's cost improvement,
+     scaled by 1 / (meaninertia * max(1, nv)) (a model constant, M at qpos0), is below tolerance */
+  const double scale = solver_scale(m);
   int it;
   for (it = 0; it < m->iterations; it++) {
     double improvement = 0;
@@ -684,6 +690,238 @@ void orc_solve_pgs(const orc_model* om, orc_data* d) {
   }
 }
 
+/* ---------------------------------------- primal Newton solver [ext mj_solNewton]
+ * The reference scene has no <option> (SOARM101/SO101/scene_with_table_v.xml:1-32), so the
+ * reference's mj_step (SOARM101_Env.py:131-132) solves the constraint problem with MuJoCo's
+ * default solver: primal Newton, iterations 100, tolerance 1e-8.  Restated from MuJoCo's
+ * published algorithm (engine_solver.c / mj_constraintUpdate):
+ *   minimise  c(a) = 1/2 (a - a0)' M (a - a0) + sum_r s_r(J_r a - aref_r),  a0 = qacc_smooth,
+ *   s_r(x) = x^2 / (2 R_r)                          limits, pyramid edges: x < 0 (else 0)
+ *          = Huber: x^2/(2R) for |x| < R fl, fl |x| - R fl^2 / 2 beyond   frictionloss rows
+ *   force f_r = -s_r'(x);  gradient g = M (a - a0) - J' f;  Hessian H = M + J_q' D J_q over the
+ *   rows in their quadratic zone (D = 1/R);  direction p = -H^-1 g;  line search: exact
+ *   minimiser of the convex piecewise-quadratic c(a + alpha p) (MuJoCo's 1-D Newton search
+ *   with gtol = tolerance * ls_tolerance(0.01) * |p| * meaninertia * nv finds the same point
+ *   to within that tolerance);  stop when scale * (c_old - c) < tol or scale * |g| < tol,
+ *   scale = 1 / (meaninertia * max(1, nv)).
+ *   Warm start: qacc_warmstart if its cost beats qacc_smooth's (mj_fwdConstraint).
+ * The problem is strictly convex (R > 0), so the optimum is unique: with tol <= 0 the loop
+ * runs until the step stops changing the cost (the exact optimum to double precision) — the
+ * reference point the PGS kernels are measured against.
+ * ------------------------------------------------------------------------------- */
+static double row_force(const orc_data* d, int r, double x, int* quad) {
+  const double R = d->efc_R[r];
+  if (d->efc_type[r] == ORC_EFC_FRICTION) {
+    const double fl = d->efc_fl[r];
+    if (x <= -R * fl) {
+      *quad = 0;
+      return fl;
+    }
+    if (x >= R * fl) {
+      *quad = 0;
+      return -fl;
+    }
+    *quad = 1;
+    return -x / R;
+  }
+  *quad = x < 0;
+  return x < 0 ? -x / R : 0.0;
+}
+static double row_cost(const orc_data* d, int r, double x) {
+  const double R = d->efc_R[r];
+  if (d->efc_type[r] == ORC_EFC_FRICTION) {
+    const double fl = d->efc_fl[r];
+    if (x <= -R * fl) return -fl * x - 0.5 * R * fl * fl;
+    if (x >= R * fl) return fl * x - 0.5 * R * fl * fl;
+    return 0.5 * x * x / R;
+  }
+  return x < 0 ? 0.5 * x * x / R : 0.0;
+}
+/* c(a); jar [nefc] = J a - aref */
+static double primal_cost(const sim_model_desc* m, const orc_data* d, const double* a, double* jar) {
+  const int nv = m->nv;
+  double da[SIM_MAXDOF], c = 0;
+  for (int i = 0; i < nv; i++) da[i] = a[i] - d->qacc_smooth[i];
+  for (int i = 0; i < nv; i++)
+    for (int k = 0; k < nv; k++) c += 0.5 * da[i] * d->M[i][k] * da[k];
+  for (int r = 0; r < d->nefc; r++) {
+    double x = -d->efc_aref[r];
+    for (int i = 0; i < nv; i++) x += d->efc_J[r][i] * a[i];
+    jar[r] = x;
+    c += row_cost(d, r, x);
+  }
+  return c;
+}
+/* derivative of c(a + alpha p) at alpha: g0 + alpha pMp - sum_r f_r(jar_r + alpha jv_r) jv_r */
+static double ls_deriv(const orc_data* d, double g0, double pMp, const double* jar, const double* jv,
+                       double alpha, double* curv) {
+  double g = g0 + alpha * pMp, h = pMp;
+  for (int r = 0; r < d->nefc; r++) {
+    int q;
+    const double f = row_force(d, r, jar[r] + alpha * jv[r], &q);
+    g -= f * jv[r];
+    if (q) h += jv[r] * jv[r] / d->efc_R[r];
+  }
+  if (curv) *curv = h;
+  return g;
+}
+static int cmp_double(const void* a, const void* b) {
+  const double x = *(const double*)a, y = *(const double*)b;
+  return x < y ? -1 : (x > y ? 1 : 0);
+}
+/* exact minimiser of the convex piecewise quadratic c(a + alpha p), alpha >= 0 */
+static double line_search(const orc_data* d, double g0, double pMp, const double* jar, const double* jv) {
+  if (ls_deriv(d, g0, pMp, jar, jv, 0.0, NULL) >= 0) return 0.0;
+  double bp[2 * ORC_MAXEFC];
+  int nb = 0;
+  for (int r = 0; r < d->nefc; r++) {
+    if (jv[r] == 0) continue;
+    const double R = d->efc_R[r];
+    double xs[2];
+    int nx = 0;
+    if (d->efc_type[r] == ORC_EFC_FRICTION) {
+      xs[nx++] = -R * d->efc_fl[r];
+      xs[nx++] = R * d->efc_fl[r];
+    } else {
+      xs[nx++] = 0.0;
+    }
+    for (int k = 0; k < nx; k++) {
+      const double al = (xs[k] - jar[r]) / jv[r];
+      if (al > 0) bp[nb++] = al;
+    }
+  }
+  qsort(bp, nb, sizeof(double), cmp_double);
+  double lo = 0.0, glo = ls_deriv(d, g0, pMp, jar, jv, 0.0, NULL);
+  for (int k = 0; k < nb; k++) {
+    const double hi = bp[k];
+    if (hi <= lo) continue;
+    const double ghi = ls_deriv(d, g0, pMp, jar, jv, hi, NULL);
+    if (ghi >= 0) /* the derivative is linear on [lo, hi]: its root */
+      return lo + (hi - lo) * (-glo) / (ghi - glo);
+    lo = hi, glo = ghi;
+  }
+  double h;
+  ls_deriv(d, g0, pMp, jar, jv, lo + 1.0, &h); /* curvature of the last (unbounded) piece */
+  return lo - glo / h;
+}
+/* dense Cholesky solve (H SPD), n <= SIM_MAXDOF */
+static int chol_solve_n(int n, double A[SIM_MAXDOF][SIM_MAXDOF], double* x, const double* b) {
+  double L[SIM_MAXDOF][SIM_MAXDOF];
+  for (int i = 0; i < n; i++)
+    for (int j = 0; j <= i; j++) {
+      double s = A[i][j];
+      for (int k = 0; k < j; k++) s -= L[i][k] * L[j][k];
+      if (i == j) {
+        if (s <= 0) return -1;
+        L[i][i] = sqrt(s);
+      } else {
+        L[i][j] = s / L[j][j];
+      }
+    }
+  double y[SIM_MAXDOF];
+  for (int i = 0; i < n; i++) {
+    double s = b[i];
+    for (int k = 0; k < i; k++) s -= L[i][k] * y[k];
+    y[i] = s / L[i][i];
+  }
+  for (int i = n - 1; i >= 0; i--) {
+    double s = y[i];
+    for (int k = i + 1; k < n; k++) s -= L[k][i] * x[k];
+    x[i] = s / L[i][i];
+  }
+  return 0;
+}
+
+static double newton_stats[3]; /* calls, iterations, line-search steps taken */
+void orc_newton_stats(double* out, int reset) {
+  for (int k = 0; k < 3; k++) {
+    out[k] = newton_stats[k];
+    if (reset) newton_stats[k] = 0;
+  }
+}
+
+void orc_solve_newton(const orc_model* om, orc_data* d, double tol) {
+  const sim_model_desc* m = om->m;
+  const int nv = m->nv, ne = d->nefc;
+  const double scale = solver_scale(m);
+  double a[SIM_MAXDOF], jar[ORC_MAXEFC], jv[ORC_MAXEFC];
+  /* warm start (mj_fwdConstraint): qacc_warmstart unless qacc_smooth costs less */
+  double cw = primal_cost(m, d, d->qacc_warmstart, jar);
+  double cs = primal_cost(m, d, d->qacc_smooth, jar);
+  memcpy(a, cw < cs ? d->qacc_warmstart : d->qacc_smooth, nv * sizeof(double));
+  double cost = primal_cost(m, d, a, jar);
+  int it = 0;
+  for (; it < m->iterations; it++) {
+    /* gradient and Hessian at a */
+    double g[SIM_MAXDOF], H[SIM_MAXDOF][SIM_MAXDOF], da[SIM_MAXDOF];
+    for (int i = 0; i < nv; i++) da[i] = a[i] - d->qacc_smooth[i];
+    for (int i = 0; i < nv; i++) {
+      double s = 0;
+      for (int k = 0; k < nv; k++) {
+        s += d->M[i][k] * da[k];
+        H[i][k] = d->M[i][k];
+      }
+      g[i] = s;
+    }
+    for (int r = 0; r < ne; r++) {
+      int q;
+      const double f = row_force(d, r, jar[r], &q);
+      for (int i = 0; i < nv; i++) g[i] -= d->efc_J[r][i] * f;
+      if (q) {
+        const double D = 1.0 / d->efc_R[r];
+        for (int i = 0; i < nv; i++)
+          for (int k = 0; k < nv; k++) H[i][k] += D * d->efc_J[r][i] * d->efc_J[r][k];
+      }
+    }
+    double gn = 0;
+    for (int i = 0; i < nv; i++) gn += g[i] * g[i];
+    if (tol > 0 && scale * sqrt(gn) < tol) break;
+    if (gn == 0) break;
+    double p[SIM_MAXDOF], mg[SIM_MAXDOF];
+    for (int i = 0; i < nv; i++) mg[i] = -g[i];
+    if (chol_solve_n(nv, H, p, mg)) break;
+    /* exact line search along p */
+    double Mp[SIM_MAXDOF], pMp = 0, g0 = 0;
+    for (int i = 0; i < nv; i++) {
+      double s = 0;
+      for (int k = 0; k < nv; k++) s += d->M[i][k] * p[k];
+      Mp[i] = s;
+    }
+    for (int i = 0; i < nv; i++) pMp += p[i] * Mp[i], g0 += da[i] * Mp[i];
+    for (int r = 0; r < ne; r++) {
+      double s = 0;
+      for (int i = 0; i < nv; i++) s += d->efc_J[r][i] * p[i];
+      jv[r] = s;
+    }
+    const double alpha = line_search(d, g0, pMp, jar, jv);
+    if (!(alpha > 0)) break;
+    double an[SIM_MAXDOF], jn[ORC_MAXEFC];
+    for (int i = 0; i < nv; i++) an[i] = a[i] + alpha * p[i];
+    const double cn = primal_cost(m, d, an, jn);
+    newton_stats[2] += 1;
+    if (!(cn <= cost)) break; /* rounding-level: no further progress */
+    const double improvement = scale * (cost - cn);
+    memcpy(a, an, nv * sizeof(double));
+    memcpy(jar, jn, ne * sizeof(double));
+    cost = cn;
+    if (tol > 0 ? improvement < tol : improvement == 0) {
+      it++;
+      break;
+    }
+  }
+  newton_stats[0] += 1;
+  newton_stats[1] += it;
+  d->solver_iter = it;
+  d->flops += it * (2.0 * ne * nv * nv + (double)nv * nv * nv / 3.0);
+  memcpy(d->qacc, a, nv * sizeof(double));
+  for (int i = 0; i < nv; i++) d->qfrc_constraint[i] = 0;
+  for (int r = 0; r < ne; r++) {
+    int q;
+    d->efc_force[r] = row_force(d, r, jar[r], &q);
+    for (int i = 0; i < nv; i++) d->qfrc_constraint[i] += d->efc_J[r][i] * d->efc_force[r];
+  }
+}
+
 /* --------------------------------------------------------- mj_forward [ext] */
 void orc_forward(const orc_model* om, orc_data* d) {
   const sim_model_desc* m = om->m;
@@ -704,7 +942,10 @@ void orc_forward(const orc_model* om, orc_data* d) {
   orc_solve_m(om, d, d->qacc_smooth, d->qfrc_smooth);
   orc_make_constraint(om, d);
   if (d->nefc) {
-    orc_solve_pgs(om, d);
+    if (m->solver == SIM_SOL_NEWTON)
+      orc_solve_newton(om, d, m->tolerance); /* tolerance <= 0: to the exact optimum */
+    else
+      orc_solve_pgs(om, d);
   } else {
     memcpy(d->qacc, d->qacc_smooth, nv * sizeof(double));
     memset(d->qfrc_constraint, 0, sizeof(d->qfrc_constraint));

@@ -102,6 +102,10 @@ void orc_passive_actuation(const orc_model* om, orc_data* d);
 void orc_collision(const orc_model* om, orc_data* d);
 void orc_make_constraint(const orc_model* om, orc_data* d);
 void orc_solve_pgs(const orc_model* om, orc_data* d);
+/* MuJoCo's default primal Newton solver; tol <= 0 iterates to the exact optimum */
+void orc_solve_newton(const orc_model* om, orc_data* d, double tol);
+void orc_newton_stats(double* out /*[3] calls, iterations, line searches*/, int reset);
+void orc_solver_stats(double* out /*[3] PGS calls, sweeps, rows*/, int reset);
 void orc_forward(const orc_model* om, orc_data* d);
 void orc_step(const orc_model* om, orc_data* d);
 void orc_jac(const orc_model* om, const orc_data* d, const double p[3], int body, double* jacp,

@@ -50,8 +50,21 @@ def lib():
         L.orc_ik_dls.restype = None
         L.orc_hull_support_flat.argtypes = [vp] * 4 + [C.c_int, vp, C.c_int, C.c_int, vp]
         L.orc_hull_support_flat.restype = C.c_int
+        L.orc_newton_stats.argtypes = [vp, C.c_int]
+        L.orc_newton_stats.restype = None
+        L.orc_solver_stats.argtypes = [vp, C.c_int]
+        L.orc_solver_stats.restype = None
         _lib = L
     return _lib
+
+
+def solver_stats(reset=True):
+    """(PGS calls, sweeps, rows), (Newton calls, iterations, line searches) since the last reset
+    (single-threaded oracle calls only: the counters are not atomic)."""
+    a, b = np.zeros(3), np.zeros(3)
+    lib().orc_solver_stats(_p(a), int(reset))
+    lib().orc_newton_stats(_p(b), int(reset))
+    return a, b
 
 
 def _p(a):
@@ -61,10 +74,20 @@ def _p(a):
 class Oracle:
     """Batched float64 oracle over a compiled model (row-major [n][...] state)."""
 
-    def __init__(self, cm):
+    def __init__(self, cm, solver=None, tolerance=None):
+        """solver: None (the compiled model's, PGS) or "PGS" / "Newton" (MuJoCo's default, the
+        solver the reference's scene runs); tolerance: override (Newton with tolerance 0
+        iterates to the exact optimum of the constraint problem)."""
         self.cm = cm
         self.desc = cm.desc
-        self._desc_p = C.cast(C.pointer(cm.desc), C.c_void_p)
+        if solver is not None or tolerance is not None:
+            from lerobot_mujoco_sim2real_amd import abi
+            self.desc = type(cm.desc).from_buffer_copy(cm.desc)
+            if solver is not None:
+                self.desc.solver = {"pgs": abi.SOL_PGS, "newton": abi.SOL_NEWTON}[solver.lower()]
+            if tolerance is not None:
+                self.desc.tolerance = tolerance
+        self._desc_p = C.cast(C.pointer(self.desc), C.c_void_p)
         self.hv = np.ascontiguousarray(cm.hull_vert, np.float32)
         self.hadr = np.ascontiguousarray(cm.hull_adr, np.int32)
         self.hadj = np.ascontiguousarray(cm.hull_adj, np.int32)
