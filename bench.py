@@ -6,13 +6,15 @@ SO-ARM101 envs per GPU with contacts (config 3: the build-defined pick scene,
 table + cube, PGS, chirp actions).  One step = one ``SOARM101Env.step()`` for
 every env = 10 physics substeps of 2 ms (``SOARM101_Env.py:39-40,131-132``).
 
-    python bench.py [--gpus N --steps K --warmup W --config contact|nocontact|dr]
+    python bench.py [--gpus N --steps K --warmup W --config contact|nocontact|dr|rollout|mpc|plumbing]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 One process per GPU; envs shard by global env id (rank r owns
 [r*n, (r+1)*n)), there is no per-step collective (``scaling: weak``); the
 timed region is bracketed by barrier + synchronize and the max over ranks is
-used.  Rank 0 prints one JSON line.
+used.  Rank 0 prints one JSON line.  ``--gpus N`` without a torchrun
+environment starts the N rank processes itself (before any GPU call) and exits
+with their status; under torchrun, ``--gpus`` must equal WORLD_SIZE.
 """
 import argparse
 import json
@@ -34,13 +36,57 @@ def parse():
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--envs", type=int, default=None, help="envs per GPU (default 4096; 8192 for dr)")
-    p.add_argument("--config", default="contact", choices=["contact", "nocontact", "dr", "rollout", "mpc"])
+    p.add_argument("--config", default="contact",
+                   choices=["contact", "nocontact", "dr", "rollout", "mpc", "plumbing"])
     p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal on one GPU)")
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-profile", action="store_true")
+    p.add_argument("--no-steady", action="store_true", help="skip the steps 20-120 steady-state window")
+    p.add_argument("--launcher-check", action="store_true",
+                   help="exercise the rank launcher / process group / max-over-ranks timing with an empty "
+                        "timed region (no GPU; CPU tests)")
     return p.parse_args()
+
+
+def launch_ranks(args):
+    """`--gpus N` without a torchrun environment: start N rank processes of this script (one per
+    GPU) with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, wait, return the worst exit status.
+    Called before anything touches the GPU (this process never initialises HIP)."""
+    import socket
+    import subprocess
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   SOARM_BENCH_LAUNCHER="bench.py --gpus")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    # a rank that fails leaves the others blocked in a collective: stop them (these exact
+    # child processes) once one exits with an error
+    import time as _t
+    rcs = [None] * len(procs)
+    while any(rc is None for rc in rcs):
+        for i, pr in enumerate(procs):
+            if rcs[i] is None:
+                rcs[i] = pr.poll()
+        if any(rc not in (None, 0) for rc in rcs):
+            for i, pr in enumerate(procs):
+                if rcs[i] is None:
+                    pr.terminate()
+                    try:
+                        rcs[i] = pr.wait(timeout=30)
+                    except subprocess.TimeoutExpired:
+                        pr.kill()
+                        rcs[i] = pr.wait()
+            break
+        _t.sleep(0.05)
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
 
 
 def cpu_baseline(cfg_name, seconds, seed):
@@ -101,6 +147,17 @@ def cpu_baseline(cfg_name, seconds, seed):
             orc.step(st, a, params=prm, nthreads=nthreads)
         return n * T
 
+    if cfg_name == "plumbing":  # config 1: one env, zero action, 1000 env-steps on one core
+        t0 = time.perf_counter()
+        st = orc.new_state(1)
+        q = W.initial_qpos(cm, np.arange(1), seed)
+        orc.reset(st, init_qpos=q[:, :5], extra_qpos=q)
+        for _ in range(1000):
+            orc.step(st, np.zeros((1, 5)), nthreads=1)
+        dt = time.perf_counter() - t0
+        return {"value": 1000 / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
+                "sample": f"1 env x 1000 env-steps (zero action) of the float64 C oracle on 1 thread, {dt:.2f} s",
+                "nproc": os.cpu_count()}
     n = 256
     done, chunk, t0 = 0, 0, time.perf_counter()
     while time.perf_counter() - t0 < seconds:
@@ -142,15 +199,24 @@ def _mpc_net(seed):
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
+    if world != args.gpus:
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
+    launcher = os.environ.get("SOARM_BENCH_LAUNCHER", "torchrun" if world > 1 else "single process")
     import numpy as np
     import torch
     import torch.distributed as dist
 
+    if args.launcher_check:
+        return launcher_check(args, rank, world, launcher)
+
     import soarm_pkg  # noqa: F401
-    from lerobot_mujoco_sim2real_amd import build, workloads as W
+    from lerobot_mujoco_sim2real_amd import build, shard, workloads as W
     from lerobot_mujoco_sim2real_amd.sim import BatchSim
 
     build.ensure_built(local)
@@ -162,10 +228,13 @@ def main():
             dist.init_process_group("nccl", init_method="env://", device_id=dev)
         else:
             dist.init_process_group(args.dist_backend, init_method="env://")
+        if dist.get_world_size() != args.gpus:
+            print(f"bench: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}", file=sys.stderr)
+            sys.exit(2)
 
     name = args.config
     cfg = W.CONFIGS[name]
-    n = args.envs or (8192 if name == "dr" else 4096)
+    n = args.envs or cfg.get("envs", 4096)
     ids = np.arange(rank * n, (rank + 1) * n)
     cm = W.model(name)
     sim = BatchSim(cm, n, gpu)
@@ -177,7 +246,7 @@ def main():
            for k, v in W.chirp_tables(ids, args.seed).items()}
     gen = torch.Generator(device=dev)
     gen.manual_seed(args.seed * 1000003 + rank)
-    act = torch.empty((n, 5), dtype=torch.float32, device=dev)
+    act = sim.action_buffer()  # the step reads its action from here (stable address: graph replay)
 
     mpc = cfg["action"] == "koopman_mpc"
     if mpc:
@@ -194,24 +263,27 @@ def main():
         run.runBefore()
 
     rollout = cfg["action"] == "ik_fig8"
+    qstar = None
     if rollout:
         # config 5: DLS-IK toward each env's Fig8 target, action = clip((q* - q)/dt), rows
         # [u | obs] recorded on device for every timed step, gathered to rank 0 at the end
         phase = torch.as_tensor(W.ik_phase(ids, args.seed), dtype=torch.float32, device=dev)
         qstar = sim.qpos.clone()
         rows = torch.empty((args.steps + 1, n, 13), dtype=torch.float32, device=dev)
-        rec = {"i": -1}
+    rec = {"i": -1}
 
     def one_step(t):
+        nonlocal qstar
         if mpc:
             run.runFunc()
             return
         if rollout:
-            nonlocal qstar
             qstar, _, _ = sim.ik(W.fig8_targets(float(t), phase, lib=torch), q=qstar)
             act.copy_(W.ik_action(qstar[:5].T, sim.obs[:, 3:8], lib=torch))
         elif cfg["action"] == "chirp":
             act.copy_(W.chirp_action(tab, float(t), lib=torch))
+        elif cfg["action"] == "zero":
+            act.zero_()
         else:
             torch.rand((n, 5), generator=gen, device=dev, out=act)
             act.sub_(0.5)
@@ -221,32 +293,52 @@ def main():
             rows[rec["i"] + 1, :, 5:] = obs
             rec["i"] += 1
 
-    def gather_rows():
-        """Rollout rows of every rank to rank 0 (RCCL gather over xGMI)."""
-        if world == 1:
-            return
-        src = rows if args.dist_backend == "nccl" else rows.cpu()
-        bufs = [torch.empty_like(src) for _ in range(world)] if rank == 0 else None
-        dist.gather(src, bufs, dst=0)
+    def snapshot():
+        """Everything the step loop reads; restore() replays from this point exactly."""
+        st = [x.clone() for x in (sim.qpos, sim.qvel, sim.qacc_warmstart, sim.ctrl, sim.status, sim.obs)]
+        g = gen.get_state()
+        qs = qstar.clone() if rollout else None
+        mp_ = (run.u_prev.clone(), run.traj_index, run.state is sim.obs) if mpc else None
 
-    t = 0
-    for _ in range(args.warmup):
-        one_step(t)
-        t += 1
-    sim.ncon.zero_()
+        def restore():
+            nonlocal qstar
+            for dst, src in zip((sim.qpos, sim.qvel, sim.qacc_warmstart, sim.ctrl, sim.status, sim.obs), st):
+                dst.copy_(src)
+            gen.set_state(g)
+            if rollout:
+                qstar = qs.clone()
+            if mpc:
+                run.u_prev.copy_(mp_[0])
+                run.traj_index = mp_[1]
+                run.state = sim.obs if mp_[2] else run.state_all_ref[0]
+        return restore
 
     def sync():
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
 
-    # snapshot of everything the timed steps read, so the profiled pass below replays
-    # exactly the timed region's work (same states, same actions)
-    snap_t = t
-    snap = [x.clone() for x in (sim.qpos, sim.qvel, sim.qacc_warmstart, sim.ctrl, sim.status, sim.obs)]
-    snap_gen = gen.get_state()
-    snap_qstar = qstar.clone() if rollout else None
-    snap_mpc = (run.u_prev.clone(), run.traj_index, run.state is sim.obs) if mpc else None
+    def max_over_ranks(*vals):
+        if world == 1:
+            return vals
+        x = torch.tensor(vals, dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
+        dist.all_reduce(x, op=dist.ReduceOp.MAX)
+        return tuple(float(v) for v in x)
+
+    def sum_over_ranks(*vals):
+        if world == 1:
+            return vals
+        x = torch.tensor(vals, dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
+        dist.all_reduce(x, op=dist.ReduceOp.SUM)
+        return tuple(float(v) for v in x)
+
+    restore_t0 = snapshot()
+    t = 0
+    for _ in range(args.warmup):
+        one_step(t)
+        t += 1
+    sim.ncon.zero_()
+    snap_t, restore_timed = t, snapshot()
     sync()
     t0 = time.perf_counter()
     if rollout:
@@ -255,25 +347,26 @@ def main():
     for _ in range(args.steps):
         one_step(t)
         t += 1
+    gather_s = None
     if rollout:
         rec["i"] = -1
-        gather_rows()
+        if world > 1:  # rollout rows of every rank to rank 0 (RCCL gather over xGMI)
+            torch.cuda.synchronize()
+            tg = time.perf_counter()
+            shard.gather_rollouts(rows if args.dist_backend == "nccl" else rows.cpu(), dst=0)
+            torch.cuda.synchronize()
+            gather_s = time.perf_counter() - tg
     sync()
     dt = time.perf_counter() - t0
-    ncon = float(sim.ncon.sum().item())
-    if world > 1:
-        x = torch.tensor([dt, ncon], dtype=torch.float64, device=dev)
-        mx = x.clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        dist.all_reduce(x, op=dist.ReduceOp.SUM)
-        dt, ncon = float(mx[0]), float(x[1])
+    (dt,) = max_over_ranks(dt)
+    if gather_s is not None:
+        (gather_s,) = max_over_ranks(gather_s)
+    (ncon,) = sum_over_ranks(float(sim.ncon.sum().item()))
     # validity of what was timed: states finite, soft resets (mj_checkPos/Vel/Acc status bits) counted
     finite = bool(torch.isfinite(sim.obs).all() and torch.isfinite(sim.qpos).all() and torch.isfinite(sim.qvel).all())
     nbad = int((sim.status != 0).sum().item())
-    if world > 1:
-        v = torch.tensor([0 if finite else 1, nbad], dtype=torch.float64, device=dev)
-        dist.all_reduce(v, op=dist.ReduceOp.SUM)
-        finite, nbad = v[0].item() == 0, int(v[1].item())
+    nonfinite, nbad = sum_over_ranks(0.0 if finite else 1.0, float(nbad))
+    finite, nbad = nonfinite == 0, int(nbad)
     total_envs = n * world
     value = total_envs * args.steps / dt
     contacts = ncon / (total_envs * args.steps * 10)
@@ -284,15 +377,7 @@ def main():
     cost = json.load(open(os.path.join(ROOT, "profiles", "algorithmic_cost.json")))[name]
     if not args.no_profile:
         kp = args.steps
-        for dst, src in zip((sim.qpos, sim.qvel, sim.qacc_warmstart, sim.ctrl, sim.status, sim.obs), snap):
-            dst.copy_(src)
-        gen.set_state(snap_gen)
-        if rollout:
-            qstar = snap_qstar
-        if mpc:
-            run.u_prev.copy_(snap_mpc[0])
-            run.traj_index = snap_mpc[1]
-            run.state = sim.obs if snap_mpc[2] else run.state_all_ref[0]
+        restore_timed()
         t = snap_t
         sync()
         sim.profile_begin()
@@ -317,15 +402,39 @@ def main():
         lanes = 4 if kind == "substep" else 1
         waves = -(-n * lanes // 64)
         capped = PEAK_FP32_TFLOPS * min(1.0, waves / 1024)
-        roof = {"bound": "mfma", "achieved": achieved, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+        roof = {"bound": "valu", "achieved": achieved, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                 "frac": achieved / PEAK_FP32_TFLOPS, "traffic": traffic,
-                "lanes_per_env": lanes, "waves_per_launch": waves, "occupancy_capped_peak": capped, "frac_of_capped": achieved / capped,
+                "lanes_per_env": lanes, "waves_per_launch": waves, "occupancy_capped_peak": capped,
+                "frac_of_capped": achieved / capped,
                 "kernel": kind, "avg_launch_ms": avg_ms, "launches": cnt,
                 "flops_per_launch": per_launch,
                 "kernel_ms_per_step": {k: v[0] / kp for k, v in prof.items()},
                 "hbm_gbs_algorithmic": cost["hbm_bytes_per_env_step"] * n * world / (dt / args.steps) / 1e9,
                 "hbm_peak_gbs": PEAK_HBM_GBS,
-                "note": "FP32 VALU-bound per-env algebra (no MFMA); peak = FP32 vector = FP32 MFMA rate"}
+                "note": "bound = FP32 VALU (per-env 6x6 / 12-dof algebra, no MFMA, HBM < 0.1% of peak); "
+                        "peak = MI355X FP32 vector rate; the kernel is latency-bound on each env's "
+                        "Gauss-Seidel chain (DESIGN.md §4)"}
+
+    # steady state: the same workload timed over env-steps 20..120 (from the reset), the window
+    # where arm-cube / arm-table contacts are present (the driver's short window is not)
+    steady = None
+    if not args.no_steady and not (rollout or mpc) and (args.warmup, args.steps) != (20, 100):
+        restore_t0()
+        t = 0
+        for _ in range(20):
+            one_step(t)
+            t += 1
+        sync()
+        ts = time.perf_counter()
+        for _ in range(100):
+            one_step(t)
+            t += 1
+        sync()
+        (dts,) = max_over_ranks(time.perf_counter() - ts)
+        steady = {"window": "env-steps 20-120", "value": total_envs * 100 / dts, "ms_per_step": dts / 100 * 1e3}
+    elif (args.warmup, args.steps) == (20, 100):
+        steady = {"window": "env-steps 20-120", "value": value, "ms_per_step": dt / args.steps * 1e3,
+                  "note": "= the timed window"}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -339,8 +448,12 @@ def main():
             "data": "synthetic (Philox-keyed initial states / chirp inputs per global env id)",
             "config": {"workload": cfg["desc"], "config": name, "envs_per_gpu": n, "global_envs": total_envs,
                        "frame_skip": 10, "substeps_per_s": value * 10,
-                       "contacts_per_env_substep": contacts, "solver": "PGS (iterations 100, tol 1e-8)",
+                       "contacts_per_env_substep": contacts,
+                       "solver": "PGS (iterations 100, tol 1e-8, scale 1/(meaninertia nv))",
                        "parallelism": f"env-sharded x{world} (no per-step collective)"},
+            "steady_state": steady,
+            "dist": {"world_size": world, "backend": (args.dist_backend if world > 1 else None),
+                     "launcher": launcher, "rollout_gather_s": gather_s},
             "roofline": roof, "cpu_baseline": cpu,
             "validity": {"state_finite": finite, "envs_status_nonzero": nbad,
                          "library": build.library_info()},
@@ -353,6 +466,32 @@ def main():
         dist.destroy_process_group()
     if not finite:
         sys.exit(3)
+
+
+def launcher_check(args, rank, world, launcher):
+    """The multi-rank plumbing of main() with an empty timed region (no GPU, no simulator)."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo", init_method="env://")
+        assert dist.get_world_size() == args.gpus
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    time.sleep(0.01 * (rank + 1))
+    if world > 1:
+        dist.barrier()
+    dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "n_gpus": world, "steps": args.steps,
+                          "ms_per_step": float(dt[0]) * 1e3, "dist": {"world_size": world, "backend": "gloo",
+                                                                       "launcher": launcher},
+                          "launcher_check": True}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -191,6 +191,7 @@ typedef struct sim_ik_opts {
   int32_t site;               /* site id */
   int32_t ndof;               /* number of leading dofs moved (5) */
   int32_t _pad;
+  double rot_weight;          /* 0.5: weight of |err_rot| in the error norm (pose targets) */
 } sim_ik_opts;
 
 /* Env state: caller-owned DEVICE buffers, SoA [field][n_envs]. */
@@ -249,6 +250,13 @@ int sim_reset(sim_batch* b, const sim_state* s, const float* init_qpos, const fl
 int sim_step(sim_batch* b, const sim_state* s, const float* action, int frame_skip, float* obs,
              void* stream);
 
+/* keyed uniform draws of the rollout loop's input streams (replaces the reference's serial
+   np.random.rand draws, SOARM101_DataCollection.py:115,132): out [N][k] row-major, out[i][j] =
+   lo + (hi - lo) u, u from Philox4x32-10 keyed by (seed, env_offset + i, counter, j): the same
+   env gets the same draws for any batch split or GPU count.  k <= 64. */
+int sim_rand_uniform(sim_batch* b, uint64_t seed, int64_t env_offset, uint32_t counter, int k, float lo,
+                     float hi, float* out, void* stream);
+
 /* one plain mj_step-equivalent on the current ctrl, no obs (frame_skip substeps) */
 int sim_substeps(sim_batch* b, const sim_state* s, int nsub, void* stream);
 
@@ -291,6 +299,10 @@ int sim_profile_end(sim_batch* b, double* ms, int32_t* launches);
    target [N][3], q [nq][N] SoA in/out (warm start), ok [N] (1 = converged), iters [N] or NULL */
 int sim_ik_dls(sim_batch* b, const float* target, float* q, int32_t* ok, int32_t* iters,
                const sim_ik_opts* opts, void* stream);
+/* replaces dm_control qpos_from_site_pose with target_quat (control/TrajectoryGenerator.py:96-107,
+   rot_weight 0.5): target_quat [N][4] (w, x, y, z) or NULL (= sim_ik_dls) */
+int sim_ik_dls_pose(sim_batch* b, const float* target, const float* target_quat, float* q, int32_t* ok,
+                    int32_t* iters, const sim_ik_opts* opts, void* stream);
 
 #ifdef __cplusplus
 }

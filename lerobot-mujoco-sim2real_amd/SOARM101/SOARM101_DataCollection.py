@@ -18,6 +18,7 @@ Action sources (``input_type``):
   per env a Fig8/Circle Cartesian target stream (random phase), batched DLS-IK
   gives q*, action = clip((q* - q) / dt, +-max_speed).
 """
+import json
 import os
 
 import numpy as np
@@ -71,6 +72,15 @@ class SineInputGenerator:
         u[m] = v[m]
         return u
 
+    def rows(self, lo, hi):
+        """The generator of trajectories [lo, hi) (their table rows; same draws as the full one)."""
+        g = object.__new__(SineInputGenerator)
+        g.traj_num, g.udim, g.mode = hi - lo, self.udim, self.mode
+        g.freq_start, g.freq_end = self.freq_start, self.freq_end
+        g.freq_table, g.amp_table = self.freq_table[lo:hi], self.amp_table[lo:hi]
+        g.phase_table, g.sine_mask = self.phase_table[lo:hi], self.sine_mask[lo:hi]
+        return g
+
     def batch(self, t, T_total=200):
         """All trajectories at step t: [traj_num, udim] float64."""
         v = self.amp_table * np.sin(2 * np.pi * self.freq(t, T_total) * t + self.phase_table)
@@ -122,11 +132,11 @@ def stream_seed(seed, stream):
     """32-bit seed of rollout stream `stream` under the user seed (splitmix64 finaliser).
 
     The reference draws every dataset from ONE advancing ``np.random`` stream
-    (``SOARM101_DataCollection.py:97-132``), so train / val / test splits and
-    successive chunks are independent draws.  Here each rollout call takes the
-    next stream index and derives its reset key, action generator and sine
-    tables from ``stream_seed(seed, index)``: distinct calls never share initial
-    states or inputs, and a fixed (seed, call order) reproduces the dataset."""
+    (``SOARM101_DataCollection.py:97-132``), so train / val / test splits are independent
+    draws.  Here every split has a stream of its own, keyed by the split's identity
+    (:data:`SPLIT_STREAM`), never by call order: regenerating one missing file of a
+    partially cached dataset reproduces exactly that split, and no two splits share initial
+    states or inputs."""
     m = (1 << 64) - 1
     z = (int(seed) * 0x9E3779B97F4A7C15 + (int(stream) + 1) * 0xBF58476D1CE4E5B9) & m
     z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & m
@@ -134,24 +144,59 @@ def stream_seed(seed, stream):
     return int((z ^ (z >> 31)) & 0xFFFFFFFF)
 
 
-class SOARM101DataGenerator:
-    """Reference ``SOARM101DataGenerator`` (``:77-205``) with a batched GPU rollout."""
+# stream index of each dataset split of generate_and_save_data (SOARM101_DataCollection.py:138-181)
+SPLIT_STREAM = {"train": 0, "val": 1, "test_random": 2, "test_sin": 3, "test_chirp": 4}
+# counter words of the keyed draws (sim_rand_uniform): step i of the random input stream uses
+# counter i; the IK phase uses PHASE_COUNTER
+PHASE_COUNTER = 0xFFFFFFFF
 
-    def __init__(self, args: Args = None, device: int = 0, max_envs: int = 65536, model=None):
+
+def _dist():
+    """(rank, world) of an initialised torch.distributed job, else (0, 1)."""
+    try:
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized():
+            return dist.get_rank(), dist.get_world_size()
+    except ImportError:
+        pass
+    return 0, 1
+
+
+class SOARM101DataGenerator:
+    """Reference ``SOARM101DataGenerator`` (``:77-205``) with a batched GPU rollout.
+
+    Multi-GPU: under ``torchrun`` (one process per GPU, torch.distributed
+    initialised) every dataset shards by global trajectory id — rank r rolls out
+    ``shard.shard_range(traj_num, world, r)`` on its own GPU — and either gathers the rows to
+    rank 0 (RCCL over xGMI) or writes per-rank ``.npy`` shards plus a manifest
+    (``shard_files=True``).  Every draw (reset state, random inputs, sine tables, IK phase)
+    is keyed by (split seed, global trajectory id), so the concatenated shards equal the
+    single-GPU dataset bit for bit."""
+
+    def __init__(self, args: Args = None, device: int = None, max_envs: int = 65536, model=None,
+                 shard_files: bool = False):
         self.args = args if args is not None else Args()
         self.udim, self.xdim = self.args.u_dim, self.args.x_dim
+        rank, world = _dist()
+        if device is None:
+            device = int(os.environ.get("LOCAL_RANK", rank)) if world > 1 else 0
         self.device_index = device
         self.max_envs = max_envs
         self.model = model
+        self.shard_files = shard_files
         self.collate_fn = Collater(self.args.x_dim, self.args.u_dim, self.args.device)
         self._envs = {}
-        self._stream = 0  # advances per rollout call (one np.random stream in the reference)
+        self._stream = 100  # ad-hoc rollout calls: streams after the named splits
 
     def next_seed(self):
-        """Seed of the next rollout stream (see :func:`stream_seed`)."""
+        """Seed of the next ad-hoc rollout stream (see :func:`stream_seed`)."""
         s = stream_seed(self.args.seed, self._stream)
         self._stream += 1
         return s
+
+    def split_seed(self, split):
+        """Seed of a named dataset split (:data:`SPLIT_STREAM`)."""
+        return stream_seed(self.args.seed, SPLIT_STREAM[split])
 
     def _env(self, n):
         if n not in self._envs:
@@ -165,18 +210,19 @@ class SOARM101DataGenerator:
                        sine=None, env_offset=0):
         """Rollout of `n` envs for `steps` env-steps; returns a device tensor [steps+1, n, 13] fp32.
 
+        Env i is global trajectory ``env_offset + i``: its reset state, random inputs and IK
+        phase are keyed by (seed, that id), and ``sine`` (a :class:`SineInputGenerator` over
+        these n trajectories) holds its table rows.
         actions: optional [steps+1, n, 5] (row i = u_i) to replay a fixed input sequence.
-        seed: key of the reset draw, action generator and sine tables; None takes the
-        generator's next stream (:meth:`next_seed`), so successive calls are independent."""
+        seed: None takes the generator's next ad-hoc stream (:meth:`next_seed`)."""
         import torch
 
         env = self._env(n)
         env._env_offset = env_offset
-        dev = env.sim.device
+        sim = env.sim
+        dev = sim.device
         if seed is None:
             seed = self.next_seed()
-        gen = torch.Generator(device=dev)
-        gen.manual_seed(seed)
         if input_type in ("sin", "chirp") and actions is None:
             sine = sine or SineInputGenerator(n, self.udim, (0.0025, 0.05), (-0.5, 0.5), mode=input_type,
                                               rng=np.random.default_rng(seed))
@@ -184,21 +230,21 @@ class SOARM101DataGenerator:
         ik = input_type.startswith("ik_") and actions is None
         if ik:
             kind = "Fig8" if input_type == "ik_fig8" else "Circle"
-            phase = torch.rand(n, generator=gen, device=dev, dtype=torch.float64) * 2 * np.pi
+            phase = sim.rand_uniform(seed, PHASE_COUNTER, 1, 0.0, 2 * np.pi, env_offset)[:, 0].double()
             qstar = None
 
         def u_at(i, obs):
             nonlocal qstar
             if actions is not None:
                 return torch.as_tensor(actions[i], dtype=torch.float32, device=dev)
-            if input_type == "random":
-                return (torch.rand((n, self.udim), generator=gen, device=dev) - 0.5) * 2 * 0.5
+            if input_type == "random":  # (rand(5) - 0.5) * 2 * 0.5, keyed by (seed, traj id, step)
+                return sim.rand_uniform(seed, i, self.udim, -0.5, 0.5, env_offset)
             if input_type in ("sin", "chirp"):
                 return dsine(i)
             if ik:
                 t = 1.6 + 0.02 * (i + 1) + phase
                 tgt = cartesian_targets(kind, t).float()
-                qstar, ok, _ = env.sim.ik(tgt, q=qstar if qstar is not None else env.sim.qpos.clone())
+                qstar, ok, _ = sim.ik(tgt, q=qstar if qstar is not None else sim.qpos.clone())
                 q = obs[:, 3:8]
                 return torch.clamp((qstar[:5].T - q) / env.dt, -env.max_speed, env.max_speed)
             raise ValueError(input_type)
@@ -206,6 +252,7 @@ class SOARM101DataGenerator:
         out = torch.empty((steps + 1, n, self.udim + self.xdim), dtype=torch.float32, device=dev)
         opts = None if init_qpos is None else {"initial_state": np.concatenate(
             [np.asarray(init_qpos), np.zeros_like(init_qpos)], axis=1)}
+        # reset draw keyed by (seed, global id): SOARM101VecEnv keys it by (seed, call index 0)
         s, _ = env.reset(seed=seed, options=opts)
         u = u_at(0, s)
         out[0, :, :self.udim] = u
@@ -217,38 +264,84 @@ class SOARM101DataGenerator:
             out[i, :, self.udim:] = s
         return out
 
-    def generate_physics_based_data(self, traj_num, steps, input_type, **kw):
-        """Same contract as the reference (``:90-136``): ndarray[traj, steps+1, 13] float64."""
-        chunks = []
-        for s0 in range(0, traj_num, self.max_envs):
-            n = min(self.max_envs, traj_num - s0)
-            r = self.rollout_device(n, steps, input_type, env_offset=s0, **kw)
-            chunks.append(r.transpose(0, 1).double().cpu().numpy())
-        return np.concatenate(chunks, axis=0)
+    def _rollout_ids(self, traj_num, steps, input_type, seed, lo, hi, **kw):
+        """Rows of global trajectories [lo, hi) as a device tensor [steps+1, hi-lo, 13], in chunks of
+        at most max_envs envs; the sine tables are the full dataset's rows lo..hi."""
+        import torch
+
+        sine_all = None
+        if input_type in ("sin", "chirp") and "actions" not in kw:
+            sine_all = SineInputGenerator(traj_num, self.udim, (0.0025, 0.05), (-0.5, 0.5), mode=input_type,
+                                          rng=np.random.default_rng(seed))
+        parts = []
+        for s0 in range(lo, hi, self.max_envs):
+            n = min(self.max_envs, hi - s0)
+            sine = sine_all.rows(s0, s0 + n) if sine_all is not None else None
+            parts.append(self.rollout_device(n, steps, input_type, seed=seed, sine=sine, env_offset=s0, **kw))
+        if not parts:
+            return torch.empty((steps + 1, 0, self.udim + self.xdim), dtype=torch.float32,
+                               device=torch.device("cuda", self.device_index))
+        return parts[0] if len(parts) == 1 else torch.cat(parts, dim=1)
+
+    def generate_physics_based_data(self, traj_num, steps, input_type, seed=None, rank=None, world=None,
+                                    gather=True, **kw):
+        """Same contract as the reference (``:90-136``): ndarray[traj, steps+1, 13] float64.
+
+        Multi-GPU (torch.distributed initialised, or explicit rank/world): this rank rolls
+        out its shard of trajectory ids; with ``gather`` rank 0 receives the whole dataset
+        (other ranks return None), otherwise every rank returns its own shard's rows."""
+        from .. import shard
+
+        if seed is None:
+            seed = self.next_seed()
+        drank, dworld = _dist()
+        rank = drank if rank is None else rank
+        world = dworld if world is None else world
+        lo, hi = shard.shard_range(traj_num, world, rank)
+        local = self._rollout_ids(traj_num, steps, input_type, seed, lo, hi, **kw)
+        if world > 1 and gather and dworld > 1:
+            full = shard.gather_rollouts(local, dst=0)
+            return None if full is None else full.transpose(0, 1).double().cpu().numpy()
+        return local.transpose(0, 1).double().cpu().numpy()
+
+    def _split(self, path, split, samples, steps, input_type):
+        """One dataset file: load it if cached, else generate (sharded under torch.distributed)."""
+        from .. import shard
+
+        rank, world = _dist()
+        if os.path.exists(path):
+            return np.load(path)
+        seed = self.split_seed(split)
+        if world > 1 and self.shard_files:
+            base = path[:-4] if path.endswith(".npy") else path
+            mine = f"{base}.rank{rank}-of-{world}.npy"
+            if os.path.exists(mine):  # resume from this rank's shard
+                return np.load(mine)
+            part = self.generate_physics_based_data(samples, steps, input_type, seed=seed, gather=False)
+            np.save(mine, part)
+            if rank == 0:
+                man = {"file": os.path.basename(path), "shape": [samples, steps + 1, self.udim + self.xdim],
+                       "dtype": "float64", "seed": seed, "input_type": input_type,
+                       "shards": [{"file": os.path.basename(f"{base}.rank{r}-of-{world}.npy"),
+                                   "traj": list(shard.shard_range(samples, world, r))} for r in range(world)]}
+                with open(f"{base}.manifest.json", "w") as f:
+                    json.dump(man, f, indent=1)
+            return part
+        data = self.generate_physics_based_data(samples, steps, input_type, seed=seed)
+        if rank == 0:
+            np.save(path, data)
+        return data
 
     def generate_and_save_data(self):
-        """File cache / resume exactly as the reference (``:138-181``)."""
+        """File cache / resume as the reference (``:138-181``); each split keyed by its name."""
         a = self.args
         os.makedirs(a.data_dir_save, exist_ok=True)
-        if os.path.exists(a.data_dir_load_train):
-            self.train_data = np.load(a.data_dir_load_train)
-        else:
-            self.train_data = self.generate_physics_based_data(a.train_samples, a.train_steps, "random")
-            np.save(a.data_dir_load_train, self.train_data)
-        if os.path.exists(a.data_dir_load_val):
-            self.val_data = np.load(a.data_dir_load_val)
-        else:
-            self.val_data = self.generate_physics_based_data(a.test_samples, a.test_steps, "random")
-            np.save(a.data_dir_load_val, self.val_data)
+        self.train_data = self._split(a.data_dir_load_train, "train", a.train_samples, a.train_steps, "random")
+        self.val_data = self._split(a.data_dir_load_val, "val", a.test_samples, a.test_steps, "random")
         self.test_data_dict = {}
         for t in ["random", "sin", "chirp"]:
             p = os.path.join(a.data_dir_save, f"test_data_{t}_{a.test_samples}_{a.test_steps}.npy")
-            if os.path.exists(p):
-                d = np.load(p)
-            else:
-                d = self.generate_physics_based_data(a.test_samples, a.test_steps, t)
-                np.save(p, d)
-            self.test_data_dict[t] = d
+            self.test_data_dict[t] = self._split(p, f"test_{t}", a.test_samples, a.test_steps, t)
 
     def get_train_loader(self):
         import torch

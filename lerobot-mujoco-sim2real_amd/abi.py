@@ -86,7 +86,7 @@ class IkOpts(C.Structure):
     _fields_ = [
         ("tol", f64), ("regularization_threshold", f64), ("regularization_strength", f64),
         ("max_update_norm", f64), ("progress_thresh", f64),
-        ("max_steps", i32), ("site", i32), ("ndof", i32), ("_pad", i32),
+        ("max_steps", i32), ("site", i32), ("ndof", i32), ("_pad", i32), ("rot_weight", f64),
     ]
 
 
@@ -119,7 +119,7 @@ EXPORTS = [
     "sim_last_error", "sim_version", "sim_model_create", "sim_model_free",
     "sim_batch_create", "sim_batch_free", "sim_batch_set_params", "sim_reset",
     "sim_step", "sim_substeps", "sim_bias", "sim_observe", "sim_contacts", "sim_collide_profile", "sim_phase_profile", "sim_ik_dls",
-    "sim_profile_begin", "sim_profile_end",
+    "sim_profile_begin", "sim_profile_end", "sim_rand_uniform", "sim_ik_dls_pose",
     # include/koopman_mpc.h
     "sim_koopman_create", "sim_koopman_free", "sim_koopman_encode", "sim_koopman_feedforward",
     "sim_koopman_mpc_step",
@@ -160,6 +160,8 @@ def load_lib(path=None):
     lib.sim_profile_begin.argtypes = [vp]
     lib.sim_profile_end.argtypes = [vp, vp, vp]
     lib.sim_ik_dls.argtypes = [vp, vp, vp, vp, vp, C.POINTER(IkOpts), vp]
+    lib.sim_ik_dls_pose.argtypes = [vp, vp, vp, vp, vp, vp, C.POINTER(IkOpts), vp]
+    lib.sim_rand_uniform.argtypes = [vp, C.c_uint64, C.c_int64, C.c_uint32, ip, C.c_float, C.c_float, vp, vp]
     lib.sim_koopman_create.argtypes = [C.POINTER(KoopmanDesc), vp, vp, ip, C.POINTER(vp)]
     lib.sim_koopman_free.argtypes = [vp]
     lib.sim_koopman_free.restype = None

@@ -3,9 +3,10 @@
 Reference: ``control/TrajectoryGenerator.py:10-210``.  Same constructor and
 ``generate(traj_name, target_orientation) -> (xyz [N,3], q [N,num_joints], t [N])``.
 The reference solves the N points serially with dm_control's
-``qpos_from_site_pose`` (``:96-107``, position-only at the ``Koopman_MPC.py:252``
-call site), warm-starting each point from the previous solution and repeating
-the last good solution on failure (``:180-205``).  Here the warm-started chain
+``qpos_from_site_pose`` (``:96-107``: pose IK with ``rot_weight=0.5`` toward the default
+``target_orientation=[1, 0, 0, 0]`` (``:118``); ``None`` — what the ``Koopman_MPC.py:252``
+call site passes — is position-only), warm-starting each point from the previous solution
+and repeating the last good solution on failure (``:180-205``).  Here the warm-started chain
 runs point by point through ``sim_ik_dls`` (one lane), and
 :meth:`solve_batch` solves many independent targets at once (one lane each).
 """
@@ -16,7 +17,7 @@ from ..SOARM101.SOARM101_DataCollection import cartesian_targets
 from ..sim import BatchSim
 
 IK_DEFAULTS = dict(tol=1e-6, regularization_threshold=0.1, regularization_strength=1e-2,
-                   max_update_norm=2.0, progress_thresh=20.0, max_steps=100)
+                   max_update_norm=2.0, progress_thresh=20.0, max_steps=100, rot_weight=0.5)
 
 
 class CartesianTrajectoryGenerator:
@@ -43,8 +44,9 @@ class CartesianTrajectoryGenerator:
         t_param = 1.6 + 0.02 * np.linspace(0, self.time_horizon * 5, len(self.time_vector))
         return cartesian_targets(traj_name, t_param, self.idx, self.traj_scale)
 
-    def solve_batch(self, targets, q0=None, **opts):
-        """Independent targets [N,3] (one lane each); returns q [N, nq], ok [N], iters [N]."""
+    def solve_batch(self, targets, q0=None, target_quat=None, **opts):
+        """Independent targets [N,3] (one lane each; target_quat [N,4] / [4] or None = position
+        only); returns q [N, nq], ok [N], iters [N]."""
         import torch
 
         o = dict(IK_DEFAULTS, **opts)
@@ -53,14 +55,14 @@ class CartesianTrajectoryGenerator:
         q = None
         if q0 is not None:
             q = torch.as_tensor(np.asarray(q0, np.float32).T.copy(), device=sim.device)
-        q, ok, it = sim.ik(targets, q=q, ndof=self.num_joints, **o)
+        q, ok, it = sim.ik(targets, q=q, ndof=self.num_joints, target_quat=target_quat, **o)
         return q.T.cpu().numpy(), ok.cpu().numpy().astype(bool), it.cpu().numpy()
 
-    def generate(self, traj_name="Fig8", target_orientation=None):
-        if target_orientation is not None:
-            raise NotImplementedError("orientation targets: only target_quat=None is on the hot path "
-                                      "(Koopman_MPC.py:252)")
+    def generate(self, traj_name="Fig8", target_orientation=np.array([1.0, 0.0, 0.0, 0.0])):
+        """The reference's default pose target [1, 0, 0, 0] (w, x, y, z) is kept; None = position only."""
         import torch
+
+        tq = None if target_orientation is None else np.asarray(target_orientation, np.float32).reshape(1, 4)
 
         xyz = self.cartesian_path(traj_name)
         sim = self._sim(1)
@@ -68,7 +70,8 @@ class CartesianTrajectoryGenerator:
         traj = []
         for i, pos in enumerate(xyz):
             last = q.clone()
-            qn, ok, _ = sim.ik(pos[None].astype(np.float32), q=q, ndof=self.num_joints, **IK_DEFAULTS)
+            qn, ok, _ = sim.ik(pos[None].astype(np.float32), q=q, ndof=self.num_joints, target_quat=tq,
+                               **IK_DEFAULTS)
             if bool(ok[0]):
                 traj.append(qn[: self.num_joints, 0].cpu().numpy().copy())
                 q = qn

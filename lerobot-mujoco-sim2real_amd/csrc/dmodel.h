@@ -62,6 +62,7 @@ struct DModel {
   // sites
   int site_bodyid[SIM_MAXSITE];
   float site_pos[SIM_MAXSITE][3];
+  float site_quat[SIM_MAXSITE][4];  // unit (w, x, y, z): site frame in its body frame
 
   // actuators (actuator a drives dof a; checked on the host)
   int act_ctrllimited[MAXU], act_forcelimited[MAXU];

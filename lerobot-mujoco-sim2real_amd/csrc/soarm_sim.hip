@@ -570,6 +570,25 @@ __global__ __launch_bounds__(64) void k_reset(const DModel* __restrict__ dm, int
   if (obs) write_obs(S, obs, e);
 }
 
+// Keyed uniform draws for the rollout's action / phase streams: out[e][j] = lo + width u, u from
+// Philox4x32-10 keyed by `seed`, counter (gid, gid >> 32, counter, 1 + j / 4) — sim_reset's draws
+// use the 4th word 0, so the streams never overlap.  Keyed by global env id, so a dataset is the
+// same for any env chunking / GPU count.  Host mirror: workloads.keyed_uniform.
+__global__ __launch_bounds__(64) void k_rand(int n, uint32_t k0, uint32_t k1, long long env_offset,
+                                             uint32_t counter, int k, float lo, float width,
+                                             float* __restrict__ out) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const unsigned long long gid = (unsigned long long)(env_offset + e);
+  for (int b = 0; 4 * b < k; b++) {
+    const u4 r = philox(u4{(uint32_t)gid, (uint32_t)(gid >> 32), counter, 1u + (uint32_t)b}, k0, k1);
+    const uint32_t rr[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+      if (4 * b + j < k) out[(size_t)e * k + 4 * b + j] = uniform_range(lo, width, u01(rr[j]));
+  }
+}
+
 // qfrc_bias at the current state (mj_comVel + mj_rne with flg_acc = 0, as left by mj_forward)
 template <int NA, int NF>
 __global__ __launch_bounds__(64) void k_bias(const DModel* __restrict__ dm, int n, sim_state st,
@@ -598,18 +617,23 @@ __global__ __launch_bounds__(64) void k_observe(const DModel* __restrict__ dm, i
 }
 
 // ------------------------------------------------------------ DLS site IK
-// dm_control qpos_from_site_pose, position only (target_quat=None at
-// Koopman_MPC.py:252), joints = the first `ndof` arm hinges:
-//   err = target - site_xpos;  stop (success) if |err| < tol
-//   J = site jacobian (3 x ndof);  reg = strength if |err| > threshold else 0
-//   dq = J' (J J' + reg I)^-1 err  (== (J'J + reg I)^-1 J' err; reg = 0 -> min-norm)
-//   stop (fail) if |err| / |dq| > progress_thresh;  clip |dq| <= max_update_norm
+// dm_control qpos_from_site_pose (control/TrajectoryGenerator.py:96-107), joints = the first
+// `ndof` arm hinges; tq (target quaternions [N][4], w x y z) null = position only
+// (target_quat=None at Koopman_MPC.py:252):
+//   err = [target - site_xpos ; quat2vel(target_quat * conj(site_xquat))]   (3 or 6 rows)
+//   err_norm = |err_pos| + rot_weight |err_rot|;  stop (success) if err_norm < tol
+//   J = site jacobian [jacp; jacr];  reg = strength if err_norm > threshold else 0
+//   position only: dq = J' (J J' + reg I)^-1 err  (== (J'J + reg I)^-1 J' err; reg = 0 -> min-norm)
+//   pose: dq = (J'J + reg I)^-1 J' err  (6 rows over 5 dofs: J'J is regular away from singular
+//         poses; where its LDL' meets a non-positive pivot the solve stops as failed, where
+//         dm_control's lstsq would drop the direction)
+//   stop (fail) if err_norm / |dq| > progress_thresh;  clip |dq| <= max_update_norm
 //   q += dq  (hinges: mj_integratePos is plain addition; joint ranges not enforced)
 template <int NA>
 __global__ __launch_bounds__(64) void k_ik(const DModel* __restrict__ dm, int n,
-                                           const float* __restrict__ target, float* __restrict__ q,
-                                           int32_t* __restrict__ ok, int32_t* __restrict__ iters,
-                                           sim_ik_opts o) {
+                                           const float* __restrict__ target, const float* __restrict__ tq,
+                                           float* __restrict__ q, int32_t* __restrict__ ok,
+                                           int32_t* __restrict__ iters, sim_ik_opts o) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
   const DModel& m = *dm;
@@ -617,18 +641,43 @@ __global__ __launch_bounds__(64) void k_ik(const DModel* __restrict__ dm, int n,
 #pragma unroll
   for (int i = 0; i < NA; i++) S.qpos[i] = q[(size_t)i * n + e];
   const float tx = target[3 * (size_t)e], ty = target[3 * (size_t)e + 1], tz = target[3 * (size_t)e + 2];
+  float tqt[4] = {1.f, 0.f, 0.f, 0.f};
+  if (tq)
+#pragma unroll
+    for (int k = 0; k < 4; k++) tqt[k] = tq[4 * (size_t)e + k];
+  const int sb = m.site_bodyid[m.obs_site];
   int success = 0, it = 0;
   for (; it < o.max_steps; it++) {
     S.kinematics();
-    const float err[3] = {tx - S.ee[0], ty - S.ee[1], tz - S.ee[2]};
-    const float en = sqrtf(dot3(err, err));
+    float err[6] = {tx - S.ee[0], ty - S.ee[1], tz - S.ee[2], 0.f, 0.f, 0.f};
+    float en = sqrtf(dot3(err, err));
+    if (tq) {
+      // site quaternion = body quaternion * site quaternion; err quat = target * conj(site)
+      float bq[4] = {1.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int b = 1; b < Sim<NA, 0>::NB; b++)
+        if (b == sb) bq[0] = S.xquat[b][0], bq[1] = S.xquat[b][1], bq[2] = S.xquat[b][2], bq[3] = S.xquat[b][3];
+      const float sq_[4] = {m.site_quat[m.obs_site][0], m.site_quat[m.obs_site][1], m.site_quat[m.obs_site][2],
+                            m.site_quat[m.obs_site][3]};
+      float sq[4], eq[4];
+      qmul(sq, bq, sq_);
+      qnormalize(sq);
+      const float cq[4] = {sq[0], -sq[1], -sq[2], -sq[3]};
+      qmul(eq, tqt, cq);
+      const float s = sqrtf(eq[1] * eq[1] + eq[2] * eq[2] + eq[3] * eq[3]);  // mju_quat2Vel, dt = 1
+      if (s >= 1e-15f) {
+        float speed = 2.f * atan2f(s, eq[0]);
+        if (speed > 3.14159265358979f) speed -= 6.28318530717959f;
+        err[3] = eq[1] / s * speed, err[4] = eq[2] / s * speed, err[5] = eq[3] / s * speed;
+      }
+      en += (float)o.rot_weight * sqrtf(err[3] * err[3] + err[4] * err[4] + err[5] * err[5]);
+    }
     if (en < (float)o.tol) {
       success = 1;
       break;
     }
     // site jacobian: hinge i moves the site iff its body is an ancestor of the site body
-    const int sb = m.site_bodyid[m.obs_site];
-    float J[3][NA];
+    float J[6][NA];
 #pragma unroll
     for (int i = 0; i < NA; i++) {
       float r[3] = {S.ee[0] - S.anchor[i][0], S.ee[1] - S.anchor[i][1], S.ee[2] - S.anchor[i][2]};
@@ -636,30 +685,55 @@ __global__ __launch_bounds__(64) void k_ik(const DModel* __restrict__ dm, int n,
       cross(c, S.axis[i], r);
       const bool use = (i < o.ndof) && (sb >= i + 2);
 #pragma unroll
-      for (int k = 0; k < 3; k++) J[k][i] = use ? c[k] : 0.f;
+      for (int k = 0; k < 3; k++) J[k][i] = use ? c[k] : 0.f, J[3 + k][i] = use ? S.axis[i][k] : 0.f;
     }
     const float reg = en > (float)o.regularization_threshold ? (float)o.regularization_strength : 0.f;
-    // A = J J' + reg I (3x3 SPD), solve A y = err, dq = J' y
-    float A[6];
-    A[0] = reg, A[1] = 0, A[2] = reg, A[3] = 0, A[4] = 0, A[5] = reg;  // packed lower: 00,10,11,20,21,22
-#pragma unroll
-    for (int i = 0; i < NA; i++) {
-      A[0] += J[0][i] * J[0][i];
-      A[1] += J[1][i] * J[0][i];
-      A[2] += J[1][i] * J[1][i];
-      A[3] += J[2][i] * J[0][i];
-      A[4] += J[2][i] * J[1][i];
-      A[5] += J[2][i] * J[2][i];
-    }
-    float Ad[3], y[3];
-    ldl_factor<3>(A, Ad);
-    ldl_solve<3>(A, Ad, y, err);
     float dq[NA], dn2 = 0.f;
+    if (!tq) {
+      // A = J J' + reg I (3x3 SPD), solve A y = err, dq = J' y
+      float A[6];
+      A[0] = reg, A[1] = 0, A[2] = reg, A[3] = 0, A[4] = 0, A[5] = reg;  // packed lower: 00,10,11,20,21,22
 #pragma unroll
-    for (int i = 0; i < NA; i++) {
-      dq[i] = J[0][i] * y[0] + J[1][i] * y[1] + J[2][i] * y[2];
-      dn2 += dq[i] * dq[i];
+      for (int i = 0; i < NA; i++) {
+        A[0] += J[0][i] * J[0][i];
+        A[1] += J[1][i] * J[0][i];
+        A[2] += J[1][i] * J[1][i];
+        A[3] += J[2][i] * J[0][i];
+        A[4] += J[2][i] * J[1][i];
+        A[5] += J[2][i] * J[2][i];
+      }
+      float Ad[3], y[3];
+      ldl_factor<3>(A, Ad);
+      ldl_solve<3>(A, Ad, y, err);
+#pragma unroll
+      for (int i = 0; i < NA; i++) dq[i] = J[0][i] * y[0] + J[1][i] * y[1] + J[2][i] * y[2];
+    } else {
+      // H = J'J + reg I over the joints (unused joints: identity rows, zero right-hand side)
+      float H[NA * (NA + 1) / 2], g[NA], Hd[NA];
+#pragma unroll
+      for (int a = 0; a < NA; a++) {
+        float ga = 0.f;
+#pragma unroll
+        for (int k = 0; k < 6; k++) ga += J[k][a] * err[k];
+        g[a] = ga;
+#pragma unroll
+        for (int b = 0; b <= a; b++) {
+          float h = 0.f;
+#pragma unroll
+          for (int k = 0; k < 6; k++) h += J[k][a] * J[k][b];
+          const bool used = a < o.ndof && sb >= a + 2;
+          H[a * (a + 1) / 2 + b] = a == b ? (used ? h + reg : 1.f) : h;
+        }
+      }
+      ldl_factor<NA>(H, Hd);
+      bool spd = true;  // a non-positive pivot: J'J singular to fp32 (singular pose) -> fail
+#pragma unroll
+      for (int a = 0; a < NA; a++) spd &= Hd[a] > 0.f && Hd[a] < 3.0e38f;
+      if (!spd) break;
+      ldl_solve<NA>(H, Hd, dq, g);
     }
+#pragma unroll
+    for (int i = 0; i < NA; i++) dn2 += dq[i] * dq[i];
     const float dn = sqrtf(dn2);
     if (en / dn > (float)o.progress_thresh) break;
     if (dn > (float)o.max_update_norm) {
@@ -898,6 +972,9 @@ static int validate_and_build(const sim_model_desc& d, sim_model* M) {
   for (int s = 0; s < d.nsite; s++) {
     m.site_bodyid[s] = d.site_bodyid[s];
     for (int k = 0; k < 3; k++) m.site_pos[s][k] = (float)d.site_pos[s][k];
+    double qn = 0;
+    for (int k = 0; k < 4; k++) qn += d.site_quat[s][k] * d.site_quat[s][k];
+    for (int k = 0; k < 4; k++) m.site_quat[s][k] = (float)(qn > 0 ? d.site_quat[s][k] / std::sqrt(qn) : k == 0);
   }
   for (int a = 0; a < d.nu; a++) {
     m.act_ctrllimited[a] = d.actuator_ctrllimited[a];
@@ -1367,6 +1444,16 @@ int sim_phase_profile(double* out, int reset) {
 #endif
 }
 
+int sim_rand_uniform(sim_batch* b, uint64_t seed, int64_t env_offset, uint32_t counter, int k, float lo,
+                     float hi, float* out, void* stream) {
+  if (!b || !out) return fail(SIM_E_ARG, "null argument");
+  if (k < 1 || k > 64) return fail(SIM_E_ARG, "k must be in [1, 64]");
+  hipLaunchKernelGGL(k_rand, grid_for(b->n), dim3(64), 0, (hipStream_t)stream, b->n, (uint32_t)seed,
+                     (uint32_t)(seed >> 32), (long long)env_offset, counter, k, lo, hi - lo, out);
+  HIPCHECK(hipGetLastError());
+  return SIM_OK;
+}
+
 int sim_substeps(sim_batch* b, const sim_state* s, int nsub, void* stream) {
   return sim_step(b, s, nullptr, nsub, nullptr, stream);
 }
@@ -1397,15 +1484,20 @@ int sim_observe(sim_batch* b, const sim_state* s, float* obs, void* stream) {
   return SIM_OK;
 }
 
-int sim_ik_dls(sim_batch* b, const float* target, float* q, int32_t* ok, int32_t* iters,
-               const sim_ik_opts* opts, void* stream) {
+int sim_ik_dls_pose(sim_batch* b, const float* target, const float* target_quat, float* q, int32_t* ok,
+                    int32_t* iters, const sim_ik_opts* opts, void* stream) {
   if (!b || !target || !q || !opts) return fail(SIM_E_ARG, "null argument");
   if (opts->ndof < 1 || opts->ndof > 6 || opts->max_steps < 0) return fail(SIM_E_ARG, "bad ik options");
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL((k_ik<6>), grid_for(b->n), dim3(64), 0, st, b->d_model, b->n, target, q, ok,
+  hipLaunchKernelGGL((k_ik<6>), grid_for(b->n), dim3(64), 0, st, b->d_model, b->n, target, target_quat, q, ok,
                      iters, *opts);
   HIPCHECK(hipGetLastError());
   return SIM_OK;
+}
+
+int sim_ik_dls(sim_batch* b, const float* target, float* q, int32_t* ok, int32_t* iters,
+               const sim_ik_opts* opts, void* stream) {
+  return sim_ik_dls_pose(b, target, nullptr, q, ok, iters, opts, stream);
 }
 
 }  // extern "C"

@@ -778,6 +778,11 @@ class NumpyKinematics:
         b = d.site_bodyid[s]
         return self.xpos[b] + self.xmat[b] @ np.array(d.site_pos[s])
 
+    def site_xquat(self, s):
+        """site frame orientation (w, x, y, z) = body quaternion * site quaternion"""
+        d = self.d
+        return quat_normalize(quat_mul(self.xquat[d.site_bodyid[s]], np.array(d.site_quat[s])))
+
     def geom_pose(self, g):
         d = self.d
         b = d.geom_bodyid[g]

@@ -121,6 +121,7 @@ class BatchSim:
         self.qfrc_applied = None  # [nv, n] once enable_qfrc_applied() is called
         self._bind_state()
         self._params = None
+        self._act = None
 
     def _bind_state(self):
         self._state = abi.SimState(_ptr(self.qpos), _ptr(self.qvel), _ptr(self.qacc_warmstart),
@@ -187,14 +188,39 @@ class BatchSim:
                                                _ptr(mk), _ptr(self.obs), self._stream()))
         return self.obs
 
+    def action_buffer(self):
+        """The staging buffer [n, nact] float32 that :meth:`step` reads the action from: a caller
+        that writes its actions here directly (``step(sim.action_buffer())``) skips the copy."""
+        if self._act is None:
+            self._act = self.torch.zeros((self.n, self.nact), dtype=self.torch.float32, device=self.device)
+        return self._act
+
     def step(self, action, frame_skip=None):
-        """ctrl[:nact] = action ([n, nact]); frame_skip x mj_step; returns obs [n, obs_dim]."""
-        a = self._dev(action, (self.n, self.nact))
-        self._keep_a = a
+        """ctrl[:nact] = action ([n, nact]); frame_skip x mj_step; returns obs [n, obs_dim].
+
+        The action is staged into one persistent device buffer (:meth:`action_buffer`): the
+        contact env-step replays a hipGraph keyed by the addresses of the buffers it reads
+        (soarm_sim.hip sim_step), so a fresh tensor per call (a strided view, a numpy array,
+        a new torch expression) would otherwise recapture the graph."""
+        a = self.action_buffer()
+        if action is not a:
+            src = action if isinstance(action, self.torch.Tensor) else self.torch.as_tensor(
+                np.asarray(action, dtype=np.float32))
+            a.copy_(src.reshape(self.n, self.nact))
         abi.check(self.lib, self.lib.sim_step(self._batch, C.byref(self._state), _ptr(a),
                                               int(frame_skip or self.frame_skip), _ptr(self.obs),
                                               self._stream()))
         return self.obs
+
+    def rand_uniform(self, seed, counter, k, lo, hi, env_offset=0, out=None):
+        """[n, k] float32 U[lo, hi) keyed by (seed, env_offset + i, counter) (sim_rand_uniform;
+        host mirror: workloads.keyed_uniform)."""
+        if out is None:
+            out = self.torch.empty((self.n, k), dtype=self.torch.float32, device=self.device)
+        abi.check(self.lib, self.lib.sim_rand_uniform(self._batch, C.c_uint64(seed), C.c_int64(env_offset),
+                                                      C.c_uint32(counter & 0xFFFFFFFF), int(k), C.c_float(lo),
+                                                      C.c_float(hi), _ptr(out), self._stream()))
+        return out
 
     def substeps(self, nsub):
         abi.check(self.lib, self.lib.sim_substeps(self._batch, C.byref(self._state), int(nsub),
@@ -242,17 +268,25 @@ class BatchSim:
         return (cyc[:npair], cyc[npair:2 * npair]) if with_max else cyc[:npair]
 
     def ik(self, target, q=None, tol=1e-6, regularization_threshold=0.1, regularization_strength=1e-2,
-           max_update_norm=2.0, progress_thresh=20.0, max_steps=100, ndof=5):
-        """Batched position-only DLS IK of the observed site.  target [n, 3];
+           max_update_norm=2.0, progress_thresh=20.0, max_steps=100, ndof=5, target_quat=None,
+           rot_weight=0.5):
+        """Batched DLS IK of the observed site (dm_control qpos_from_site_pose).  target [n, 3];
+        target_quat [n, 4] or [4] (w, x, y, z; pose IK) or None (position only);
         q [nq, n] warm start (SoA, modified in place) or None (qpos0)."""
         t = self._dev(target, (self.n, 3))
+        tq = None
+        if target_quat is not None:
+            tq = self.torch.as_tensor(np.asarray(target_quat, np.float32) if not isinstance(
+                target_quat, self.torch.Tensor) else target_quat, dtype=self.torch.float32, device=self.device)
+            tq = tq.expand(self.n, 4).contiguous()
         if q is None:
             q = self.torch.zeros((self.nq, self.n), dtype=self.torch.float32, device=self.device)
             q[:] = self._dev(self.cm.qpos0()).reshape(-1, 1)
         ok = self.torch.zeros(self.n, dtype=self.torch.int32, device=self.device)
         it = self.torch.zeros(self.n, dtype=self.torch.int32, device=self.device)
         o = abi.IkOpts(tol, regularization_threshold, regularization_strength, max_update_norm,
-                       progress_thresh, int(max_steps), int(self.cm.desc.obs_site), int(ndof), 0)
-        abi.check(self.lib, self.lib.sim_ik_dls(self._batch, _ptr(t), _ptr(q), _ptr(ok), _ptr(it),
-                                                C.byref(o), self._stream()))
+                       progress_thresh, int(max_steps), int(self.cm.desc.obs_site), int(ndof), 0, rot_weight)
+        self._keep_ik = (t, tq)
+        abi.check(self.lib, self.lib.sim_ik_dls_pose(self._batch, _ptr(t), _ptr(tq), _ptr(q), _ptr(ok), _ptr(it),
+                                                     C.byref(o), self._stream()))
         return q, ok, it

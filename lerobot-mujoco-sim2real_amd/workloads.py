@@ -4,6 +4,8 @@ Every random draw is Philox4x32-10 keyed by (seed, global env id), so the
 same env gets the same initial state, inputs and DR parameters whether the
 batch runs on 1 or 8 GPUs.
 
+* ``plumbing`` (config 1): one env of the reference scene, zero action, qpos ~ U(-0.3, 0.3)^5
+  (``SOARM101_Env.py:77-142`` driven by hand); its CPU leg is the oracle on one core.
 * ``nocontact`` (config 2): arm on the table, collision disabled (frictionloss
   and joint limits on), qpos ~ U(-0.3, 0.3)^5, random actions U[-0.5, 0.5)^5
   every env-step (``SOARM101_DataCollection.py:132``).
@@ -32,11 +34,14 @@ from .mjcf import CUBE_SCENE_XML, SCENE_XML, compile_mjcf
 from .sim import philox4x32
 
 CONFIGS = {
+    "plumbing": dict(xml=SCENE_XML, disable_contact=False, action="zero", dr=False, envs=1,
+                     desc="1 SO-ARM101 env, reference scene (arm + table, contacts on), zero action "
+                          "(config 1: SOARM101_Env plumbing)"),
     "nocontact": dict(xml=SCENE_XML, disable_contact=True, action="random", dr=False,
                       desc="4096 SO-ARM101 envs, contact-free arm dynamics (config 2)"),
     "contact": dict(xml=CUBE_SCENE_XML, disable_contact=False, action="chirp", dr=False,
                     desc="4096 SO-ARM101 envs, tabletop+cube contacts, PGS (config 3, pick scene)"),
-    "dr": dict(xml=CUBE_SCENE_XML, disable_contact=False, action="chirp", dr=True,
+    "dr": dict(xml=CUBE_SCENE_XML, disable_contact=False, action="chirp", dr=True, envs=8192,
                desc="SO-ARM101 pick scene with per-env mass/friction/damping DR (config 4)"),
     "rollout": dict(xml=SCENE_XML, disable_contact=False, action="ik_fig8", dr=False,
                     desc="SOARM101_DataCollection rollout: batched DLS-IK actions toward Fig8 targets, "
@@ -57,6 +62,22 @@ def philox_uniform(seed, ids, k):
         blocks.append(philox4x32(ctr, key))
     r = np.concatenate(blocks, 1)[:, :k]
     return (r >> 8).astype(np.float32) * np.float32(1.0 / 16777216.0)
+
+
+def keyed_uniform(seed, ids, counter, k, lo, hi):
+    """Host mirror of ``sim_rand_uniform`` (bit-exact): [n, k] float32 lo + (hi - lo) u, u from
+    Philox4x32-10 keyed by `seed`, counter (id, id >> 32, counter, 1 + j // 4)."""
+    ids = np.asarray(ids, dtype=np.uint64)
+    key = (int(seed) & 0xFFFFFFFF, (int(seed) >> 32) & 0xFFFFFFFF)
+    blocks = []
+    for b in range((k + 3) // 4):
+        ctr = np.stack([ids & 0xFFFFFFFF, ids >> np.uint64(32), np.full_like(ids, int(counter) & 0xFFFFFFFF),
+                        np.full_like(ids, 1 + b)], 1)
+        blocks.append(philox4x32(ctr, key))
+    r = np.concatenate(blocks, 1)[:, :k]
+    u = (r >> 8).astype(np.float32) * np.float32(1.0 / 16777216.0)
+    lo32 = np.float32(lo)
+    return lo32 + (np.float32(hi) - lo32) * u
 
 
 def model(name, **kw):

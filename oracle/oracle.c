@@ -1209,19 +1209,20 @@ int orc_debug_forward(const sim_model_desc* m, const float* hv, const int32_t* h
 }
 
 /* ---------------------------------------------------------------------------
- * dm_control utils.inverse_kinematics.qpos_from_site_pose, position only
- * [ext; restated from its published algorithm], as called at
- * control/TrajectoryGenerator.py:96-107 (tol 1e-6, regularization_strength 1e-2,
- * regularization_threshold 0.1, max_update_norm 2, progress_thresh 20,
- * max_steps 100; joints = the first `ndof` hinges):
- *   err = target - site_xpos; success if |err| < tol
- *   J = mj_jacSite translational columns of the joints
- *   reg = strength if |err| > threshold else 0
+ * dm_control utils.inverse_kinematics.qpos_from_site_pose [ext; restated from its published
+ * algorithm], as called at control/TrajectoryGenerator.py:96-107 (tol 1e-6, rot_weight 0.5,
+ * regularization_strength 1e-2, regularization_threshold 0.1, max_update_norm 2,
+ * progress_thresh 20, max_steps 100; joints = the first `ndof` hinges):
+ *   err_pos = target_pos - site_xpos
+ *   err_rot = quat2vel(target_quat * conj(site_xquat), 1)       (target_quat given)
+ *   err_norm = |err_pos| + rot_weight |err_rot|;  success if err_norm < tol
+ *   J = mj_jacSite rows [jacp; jacr] of the joints (3 or 6 rows; rot_weight weighs only the norm)
+ *   reg = strength if err_norm > threshold else 0
  *   dq = solve(J'J + reg I, J'err)   (reg > 0)
- *   dq = lstsq(J'J, J'err)           (reg = 0: minimum-norm, = J'(JJ')^-1 err)
- *   halt if |err|/|dq| > progress_thresh; clip |dq| <= max_update_norm
+ *   dq = lstsq(J'J, J'err)           (reg = 0: pseudo-inverse, cutoff eps * largest eigenvalue)
+ *   halt if err_norm/|dq| > progress_thresh; clip |dq| <= max_update_norm
  *   mj_integratePos(q, dq, 1); joint limits are NOT enforced.
- * q is [n][nq] row-major in/out.
+ * q is [n][nq] row-major in/out; target_quat [n][4] (w, x, y, z) or NULL (position only).
  * ------------------------------------------------------------------------- */
 static int chol_solve(int n, double A[8][8], double* x, const double* b) {
   double L[8][8] = {{0}};
@@ -1250,9 +1251,67 @@ static int chol_solve(int n, double A[8][8], double* x, const double* b) {
   return 0;
 }
 
-void orc_ik_dls(const sim_model_desc* m, int n, const double* target, double* q, int32_t* ok,
-                int32_t* iters, double tol, double reg_thresh, double reg_strength,
-                double max_update, double progress_thresh, int max_steps, int site, int ndof) {
+/* numpy.linalg.lstsq(A, b, rcond=-1) for symmetric PSD A (n <= 8): eigen-decomposition by
+   cyclic Jacobi rotations, pseudo-inverse with the cutoff eps * largest eigenvalue */
+static void sym_lstsq(int n, double A[8][8], double* x, const double* b) {
+  double a[8][8], V[8][8];
+  for (int i = 0; i < n; i++)
+    for (int j = 0; j < n; j++) a[i][j] = A[i][j], V[i][j] = i == j;
+  for (int sweep = 0; sweep < 60; sweep++) {
+    double off = 0;
+    for (int p = 0; p < n; p++)
+      for (int q = p + 1; q < n; q++) off += a[p][q] * a[p][q];
+    if (off < 1e-300) break;
+    for (int p = 0; p < n; p++)
+      for (int q = p + 1; q < n; q++) {
+        if (fabs(a[p][q]) < 1e-300) continue;
+        const double th = (a[q][q] - a[p][p]) / (2 * a[p][q]);
+        const double t = (th >= 0 ? 1.0 : -1.0) / (fabs(th) + sqrt(th * th + 1));
+        const double c = 1 / sqrt(t * t + 1), s = t * c;
+        for (int k = 0; k < n; k++) {
+          const double akp = a[k][p], akq = a[k][q];
+          a[k][p] = c * akp - s * akq, a[k][q] = s * akp + c * akq;
+        }
+        for (int k = 0; k < n; k++) {
+          const double apk = a[p][k], aqk = a[q][k];
+          a[p][k] = c * apk - s * aqk, a[q][k] = s * apk + c * aqk;
+        }
+        for (int k = 0; k < n; k++) {
+          const double vkp = V[k][p], vkq = V[k][q];
+          V[k][p] = c * vkp - s * vkq, V[k][q] = s * vkp + c * vkq;
+        }
+      }
+  }
+  double lmax = 0;
+  for (int i = 0; i < n; i++) lmax = fmax(lmax, fabs(a[i][i]));
+  const double cut = 2.220446049250313e-16 * n * lmax;
+  for (int i = 0; i < n; i++) x[i] = 0;
+  for (int e = 0; e < n; e++) {
+    if (fabs(a[e][e]) <= cut) continue;
+    double c = 0;
+    for (int k = 0; k < n; k++) c += V[k][e] * b[k];
+    c /= a[e][e];
+    for (int k = 0; k < n; k++) x[k] += c * V[k][e];
+  }
+}
+
+/* MuJoCo mju_quat2Vel(res, quat, dt = 1) */
+static void quat2vel(double res[3], const double q[4]) {
+  double ax[3] = {q[1], q[2], q[3]};
+  const double s = sqrt(dot3(ax, ax));
+  if (s < MINVAL) {
+    res[0] = res[1] = res[2] = 0;
+    return;
+  }
+  double speed = 2 * atan2(s, q[0]);
+  if (speed > M_PI) speed -= 2 * M_PI;
+  for (int k = 0; k < 3; k++) res[k] = ax[k] / s * speed;
+}
+
+void orc_ik_dls(const sim_model_desc* m, int n, const double* target, const double* target_quat, double* q,
+                int32_t* ok, int32_t* iters, double tol, double rot_weight, double reg_thresh,
+                double reg_strength, double max_update, double progress_thresh, int max_steps, int site,
+                int ndof) {
   orc_model om;
   make_om(&om, m, NULL, NULL, NULL, NULL);
 #ifdef _OPENMP
@@ -1263,18 +1322,31 @@ void orc_ik_dls(const sim_model_desc* m, int n, const double* target, double* q,
     orc_reset_data(&om, &d);
     for (int i = 0; i < m->nq; i++) d.qpos[i] = q[e * m->nq + i];
     const double* tg = target + 3 * e;
+    const double* tq = target_quat ? target_quat + 4 * e : NULL;
+    const int nr = tq ? 6 : 3;
     int success = 0, it;
     for (it = 0; it < max_steps; it++) {
       orc_kinematics(&om, &d);
-      double err[3];
+      double err[6] = {0};
       for (int k = 0; k < 3; k++) err[k] = tg[k] - d.site_xpos[site][k];
       double en = sqrt(err[0] * err[0] + err[1] * err[1] + err[2] * err[2]);
+      if (tq) {
+        /* site frame quaternion = body quaternion * site quaternion (mju_mat2Quat of site_xmat, up
+           to a sign that quat2vel's > pi branch makes irrelevant) */
+        double sq[4], cq[4], eq[4];
+        quat_mul(sq, d.xquat[m->site_bodyid[site]], m->site_quat[site]);
+        quat_normalize(sq);
+        cq[0] = sq[0], cq[1] = -sq[1], cq[2] = -sq[2], cq[3] = -sq[3];
+        quat_mul(eq, tq, cq);
+        quat2vel(err + 3, eq);
+        en += rot_weight * sqrt(err[3] * err[3] + err[4] * err[4] + err[5] * err[5]);
+      }
       if (en < tol) {
         success = 1;
         break;
       }
       /* site Jacobian columns of the hinges that are ancestors of the site body */
-      double J[3][8] = {{0}};
+      double J[6][8] = {{0}};
       int sb = m->site_bodyid[site];
       for (int j = 0; j < ndof; j++) {
         int b = m->jnt_bodyid[j], anc = 0;
@@ -1286,18 +1358,25 @@ void orc_ik_dls(const sim_model_desc* m, int n, const double* target, double* q,
         double c[3] = {d.xaxis[j][1] * r[2] - d.xaxis[j][2] * r[1],
                        d.xaxis[j][2] * r[0] - d.xaxis[j][0] * r[2],
                        d.xaxis[j][0] * r[1] - d.xaxis[j][1] * r[0]};
-        for (int k = 0; k < 3; k++) J[k][j] = c[k];
+        for (int k = 0; k < 3; k++) J[k][j] = c[k], J[3 + k][j] = d.xaxis[j][k];
       }
       double reg = en > reg_thresh ? reg_strength : 0.0;
       double dq[8] = {0};
-      if (reg > 0) {
+      if (reg > 0 || tq) {
         double H[8][8], g[8];
         for (int a = 0; a < ndof; a++) {
-          g[a] = J[0][a] * err[0] + J[1][a] * err[1] + J[2][a] * err[2];
-          for (int b = 0; b < ndof; b++)
-            H[a][b] = J[0][a] * J[0][b] + J[1][a] * J[1][b] + J[2][a] * J[2][b] + (a == b ? reg : 0);
+          g[a] = 0;
+          for (int k = 0; k < nr; k++) g[a] += J[k][a] * err[k];
+          for (int b = 0; b < ndof; b++) {
+            double h = 0;
+            for (int k = 0; k < nr; k++) h += J[k][a] * J[k][b];
+            H[a][b] = h + (a == b ? reg : 0);
+          }
         }
-        chol_solve(ndof, H, dq, g);
+        if (reg > 0)
+          chol_solve(ndof, H, dq, g);
+        else
+          sym_lstsq(ndof, H, dq, g);
       } else {
         double A[8][8], y[3];
         for (int a = 0; a < 3; a++)

@@ -145,9 +145,10 @@ int orc_debug_forward(const sim_model_desc* m, const float* hv, const int32_t* h
 int orc_collide_geoms(const sim_model_desc* m, const float* hv, const int32_t* hadr,
                       const int32_t* hadj, const double* qpos, int g1, int g2, double* out,
                       int maxout);
-void orc_ik_dls(const sim_model_desc* m, int n, const double* target, double* q, int32_t* ok,
-                int32_t* iters, double tol, double reg_thresh, double reg_strength,
-                double max_update, double progress_thresh, int max_steps, int site, int ndof);
+void orc_ik_dls(const sim_model_desc* m, int n, const double* target, const double* target_quat, double* q,
+                int32_t* ok, int32_t* iters, double tol, double rot_weight, double reg_thresh,
+                double reg_strength, double max_update, double progress_thresh, int max_steps, int site,
+                int ndof);
 #ifdef __cplusplus
 }
 #endif

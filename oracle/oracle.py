@@ -46,7 +46,7 @@ def lib():
         L.orc_debug_forward.restype = C.c_int
         L.orc_collide_geoms.argtypes = [vp] * 5 + [C.c_int, C.c_int, vp, C.c_int]
         L.orc_collide_geoms.restype = C.c_int
-        L.orc_ik_dls.argtypes = [vp, C.c_int, vp, vp, vp, vp] + [C.c_double] * 5 + [C.c_int] * 3
+        L.orc_ik_dls.argtypes = [vp, C.c_int, vp, vp, vp, vp, vp] + [C.c_double] * 6 + [C.c_int] * 3
         L.orc_ik_dls.restype = None
         L.orc_hull_support_flat.argtypes = [vp] * 4 + [C.c_int, vp, C.c_int, C.c_int, vp]
         L.orc_hull_support_flat.restype = C.c_int
@@ -156,13 +156,17 @@ class Oracle:
                     geom_xpos=gx.reshape(-1, 3)[: d.ngeom], efc_force=efc[: nefc.value])
 
     def ik(self, target, q, tol=1e-6, regularization_threshold=0.1, regularization_strength=1e-2,
-           max_update_norm=2.0, progress_thresh=20.0, max_steps=100, ndof=5):
-        """dm_control qpos_from_site_pose restated; target [n,3], q [n,nq] (copied)."""
+           max_update_norm=2.0, progress_thresh=20.0, max_steps=100, ndof=5, target_quat=None,
+           rot_weight=0.5):
+        """dm_control qpos_from_site_pose restated; target [n,3], target_quat [n,4] (w,x,y,z) or
+        None (position only), q [n,nq] (copied)."""
         t = np.ascontiguousarray(target, np.float64).reshape(-1, 3)
+        tq = None if target_quat is None else np.ascontiguousarray(
+            np.broadcast_to(np.asarray(target_quat, np.float64), (len(t), 4)))
         q = np.array(q, dtype=np.float64, order="C").reshape(len(t), -1)
         ok = np.zeros(len(t), np.int32)
         it = np.zeros(len(t), np.int32)
-        lib().orc_ik_dls(self._desc_p, len(t), _p(t), _p(q), _p(ok), _p(it), tol,
+        lib().orc_ik_dls(self._desc_p, len(t), _p(t), _p(tq), _p(q), _p(ok), _p(it), tol, rot_weight,
                          regularization_threshold, regularization_strength, max_update_norm,
                          progress_thresh, max_steps, int(self.desc.obs_site), ndof)
         return q, ok.astype(bool), it

@@ -473,6 +473,62 @@ def test_ik_matches_oracle(gpu_lib, arm_model):
         assert np.linalg.norm(ee - tgt[e]) < 1e-5
 
 
+def test_pose_ik_matches_oracle(gpu_lib, arm_model):
+    """qpos_from_site_pose with target_quat (TrajectoryGenerator.py:96-107, rot_weight 0.5): reachable
+    poses from perturbed starts, and the reference's default orientation [1, 0, 0, 0] over Fig8."""
+    import torch
+    from lerobot_mujoco_sim2real_amd import mjcf
+    from lerobot_mujoco_sim2real_amd.SOARM101.SOARM101_DataCollection import cartesian_targets
+    cm = arm_model
+    kin = mjcf.NumpyKinematics(cm)
+    s = cm.desc.obs_site
+    n = 512
+    qt = np.zeros((n, 6))
+    qt[:, :5] = RNG.uniform(-0.8, 0.8, (n, 5))
+    tp = np.array([kin.forward_position(q).site_xpos(s) for q in qt]).astype(np.float32)
+    tq = np.array([kin.forward_position(q).site_xquat(s) for q in qt]).astype(np.float32)
+    q0 = (qt + np.c_[RNG.uniform(-0.15, 0.15, (n, 5)), np.zeros(n)]).astype(np.float32)
+    S, orc = make_sim(cm, n), Oracle(cm)
+    qg, okg, _ = S.ik(tp, q=torch.as_tensor(q0.T.copy(), device=S.device), target_quat=tq)
+    qg, okg = to_np(qg).T, to_np(okg).astype(bool)
+    qc, okc, _ = orc.ik(tp.astype(np.float64), q0.astype(np.float64), target_quat=tq.astype(np.float64))
+    assert okc.mean() > 0.9 and (okg == okc).mean() > 0.9, (okg.mean(), okc.mean(), (okg == okc).mean())
+    both = okg & okc
+    np.testing.assert_allclose(qg[both][:, :5], qc[both][:, :5], atol=2e-3)
+    # the default orientation over the reference's Fig8 path (a 5-dof arm: some points fail)
+    tpf = cartesian_targets("Fig8", 1.6 + 0.02 * np.linspace(0, 300, 300)).astype(np.float32)
+    S2 = make_sim(cm, 300)
+    qf, okf, _ = S2.ik(tpf, q=None, target_quat=np.array([1.0, 0, 0, 0], np.float32))
+    qcf, okcf, _ = orc.ik(tpf.astype(np.float64), np.zeros((300, 6)), target_quat=np.array([1.0, 0, 0, 0]))
+    okf = to_np(okf).astype(bool)
+    assert (okf == okcf).mean() > 0.95
+    b2 = okf & okcf
+    np.testing.assert_allclose(to_np(qf).T[b2][:, :5], qcf[b2][:, :5], atol=2e-3)
+
+
+def test_rand_uniform_matches_host_mirror(gpu_lib, arm_model):
+    """sim_rand_uniform (the rollout's keyed input draws) == workloads.keyed_uniform bit for bit."""
+    from lerobot_mujoco_sim2real_amd import workloads as W
+    n = 1000
+    S = make_sim(arm_model, n)
+    for seed, ctr, k, lo, hi, off in ((7, 0, 5, -0.5, 0.5, 0), (2 ** 40 + 3, 123, 9, 0.0, 2 * np.pi, 5000)):
+        d = S.rand_uniform(seed, ctr, k, lo, hi, env_offset=off).cpu().numpy()
+        np.testing.assert_array_equal(d, W.keyed_uniform(seed, np.arange(off, off + n), ctr, k, lo, hi))
+
+
+def test_sharded_rollouts_bit_identical(gpu_lib, arm_model):
+    """§8e: a dataset built as two env shards (ranks 0 and 1 of 2, each its own batch) equals the
+    single-batch build bit for bit, for every input type (draws keyed by global trajectory id)."""
+    from lerobot_mujoco_sim2real_amd.args import Args
+    from lerobot_mujoco_sim2real_amd.SOARM101.SOARM101_DataCollection import SOARM101DataGenerator
+    g = SOARM101DataGenerator(Args([]), model=arm_model, max_envs=128)
+    for kind in ("random", "sin", "chirp", "ik_fig8"):
+        full = g.generate_physics_based_data(301, 6, kind, seed=11)
+        parts = [g.generate_physics_based_data(301, 6, kind, seed=11, rank=r, world=2, gather=False) for r in range(2)]
+        np.testing.assert_array_equal(np.concatenate(parts), full, err_msg=kind)
+        assert full.shape == (301, 7, 13)
+
+
 def test_bad_state_soft_reset(gpu_lib, arm_model_nocontact):
     import torch
     from lerobot_mujoco_sim2real_amd import abi
@@ -519,6 +575,21 @@ def test_datacollection_layout_and_replay(gpu_lib, arm_model_nocontact):
     np.testing.assert_allclose(r[:, :, :5], acts, atol=0)
     s1 = orc.step(st, acts[0].astype(np.float64))
     np.testing.assert_allclose(r[1, :, 5:], s1, atol=5e-4)
+    # sin / chirp (SineInputGenerator, :31-74): the device generator's inputs equal the reference
+    # formula over t = 0..200 (float32 of the float64 value), and the rows replay on the oracle
+    from lerobot_mujoco_sim2real_amd.SOARM101.SOARM101_DataCollection import DeviceSine, SineInputGenerator
+    for mode in ("sin", "chirp"):
+        sg = SineInputGenerator(n, 5, (0.0025, 0.05), (-0.5, 0.5), mode=mode, rng=np.random.default_rng(3))
+        ds = DeviceSine(sg, gen._env(n).sim.device)
+        for t in range(201):
+            f = sg.freq_table + ((0.05 - 0.0025) * (t / 200) if mode == "chirp" else 0.0)
+            ref = sg.amp_table * np.sin(2 * np.pi * f * t + sg.phase_table)  # :57-74
+            np.testing.assert_allclose(to_np(ds(t)), ref.astype(np.float32), rtol=0, atol=1e-7)
+        r = to_np(gen.rollout_device(n, T, mode, init_qpos=iq, sine=sg, seed=5))
+        np.testing.assert_allclose(r[:, :, :5], np.stack([sg.batch(t) for t in range(T + 1)]), atol=1e-7)
+        st = orc.new_state(n)
+        orc.reset(st, init_qpos=iq.astype(np.float32).astype(np.float64))
+        np.testing.assert_allclose(r[1, :, 5:], orc.step(st, r[0, :, :5].astype(np.float64)), atol=5e-4)
 
 
 def test_vecenv_api(gpu_lib):

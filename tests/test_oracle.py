@@ -183,6 +183,47 @@ def test_ik_converges_on_fig8(arm_model):
         assert np.linalg.norm(kin.site_xpos(arm_model.desc.obs_site) - p) < 1e-6
 
 
+def test_pose_ik_converges(arm_model):
+    """dm_control qpos_from_site_pose with target_quat (TrajectoryGenerator.py:96-107, rot_weight 0.5):
+    poses the arm itself reaches (5 dofs) are recovered from a perturbed start."""
+    orc = Oracle(arm_model)
+    s = arm_model.desc.obs_site
+    kin = mjcf.NumpyKinematics(arm_model)
+    n = 40
+    qt = np.zeros((n, 6))
+    qt[:, :5] = RNG.uniform(-0.8, 0.8, (n, 5))
+    tp = np.array([kin.forward_position(q).site_xpos(s) for q in qt])
+    tq = np.array([kin.forward_position(q).site_xquat(s) for q in qt])
+    q0 = qt + np.c_[RNG.uniform(-0.15, 0.15, (n, 5)), np.zeros(n)]
+    qn, ok, it = orc.ik(tp, q0, target_quat=tq)
+    assert ok.mean() > 0.9
+    for e in np.nonzero(ok)[0]:
+        k = kin.forward_position(qn[e])
+        assert np.linalg.norm(k.site_xpos(s) - tp[e]) < 1e-6
+        assert min(np.abs(k.site_xquat(s) - tq[e]).max(), np.abs(k.site_xquat(s) + tq[e]).max()) < 4e-6
+    # a quaternion target of the opposite sign is the same rotation (quat2vel's > pi branch)
+    qm, okm, _ = orc.ik(tp, q0, target_quat=-tq)
+    np.testing.assert_array_equal(okm, ok)
+    np.testing.assert_allclose(qm[ok], qn[ok], atol=1e-9)
+
+
+def test_pose_ik_reference_default_orientation(arm_model):
+    """generate()'s default target_orientation [1, 0, 0, 0] (TrajectoryGenerator.py:118) over the
+    Fig8 path: a 5-dof arm cannot hold an arbitrary orientation, so points fail and generate()
+    repeats the last good solution (:193-205); the ones that succeed meet both criteria."""
+    from lerobot_mujoco_sim2real_amd.SOARM101.SOARM101_DataCollection import cartesian_targets
+    orc = Oracle(arm_model)
+    tp = 1.6 + 0.02 * np.linspace(0, 300, 300)
+    xyz = cartesian_targets("Fig8", tp)
+    q, ok, it = orc.ik(xyz, np.zeros((300, 6)), target_quat=np.array([1.0, 0, 0, 0]))
+    kin = mjcf.NumpyKinematics(arm_model)
+    s = arm_model.desc.obs_site
+    for e in np.nonzero(ok)[0][:20]:
+        k = kin.forward_position(q[e])
+        assert np.linalg.norm(k.site_xpos(s) - xyz[e]) < 1e-6
+    assert (it[~ok] < 100).all() or (~ok).sum() == 0  # failures are progress stalls, not the cap
+
+
 def test_golden_regression(arm_model_nocontact):
     """Committed fixtures (tests/golden/make_golden.py) — the oracle must keep reproducing them."""
     import os

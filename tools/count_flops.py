@@ -81,6 +81,8 @@ def main():
             elif c["action"] == "ik_fig8":  # IK flops are not counted: physics only
                 qstar, _, _ = orc.ik(W.fig8_targets(t, phase), qstar)
                 a = W.ik_action(qstar[:, :5], st["qpos"][:, :5])
+            elif c["action"] == "zero":
+                a = np.zeros((N, 5))
             else:
                 a = rng.uniform(-0.5, 0.5, (N, 5))
             orc.step(st, a, params=prm, nthreads=8)
