@@ -600,6 +600,22 @@ static double solver_scale(const sim_model_desc* m) {
   return 1.0 / (mi * (m->nv > 1 ? m->nv : 1));
 }
 
+/* identity of a constraint row across substeps (experiment harness, pgs_warm = 1) */
+static int row_key(const orc_data* d, int r) {
+  const int id = d->efc_id[r];
+  if (d->efc_type[r] == ORC_EFC_FRICTION) return 1000000 + id;
+  if (d->efc_type[r] == ORC_EFC_LIMIT) {
+    double s = 0;
+    for (int i = 0; i < SIM_MAXDOF; i++) s += d->efc_J[r][i];
+    return 2000000 + 2 * id + (s > 0 ? 0 : 1);
+  }
+  int k = 0; /* k-th contact of its pair */
+  for (int c = 0; c < id; c++) k += d->contact[c].pair == d->contact[id].pair;
+  int e = 0; /* edge within the contact */
+  for (int q = r - 1; q >= 0 && d->efc_type[q] == ORC_EFC_CONTACT && d->efc_id[q] == id; q--) e++;
+  return d->contact[id].pair * 64 + k * 4 + e;
+}
+
 /* ------------------------------------------------ PGS dual solver [ext mj_solPGS] */
 static double project(int type, double f, double fl) {
   if (type == ORC_EFC_FRICTION) return f < -fl ? -fl : (f > fl ? fl : f);
@@ -636,6 +652,15 @@ void orc_solve_pgs(const orc_model* om, orc_data* d) {
       f[r] = jar < 0 ? -D * jar : 0;
     }
   }
+  if (om->pgs_warm == 1) /* experiment: persisting rows restart from their previous force */
+    for (int r = 0; r < ne; r++) {
+      const int key = row_key(d, r);
+      for (int q = 0; q < d->prev_n; q++)
+        if (d->prev_key[q] == key) {
+          f[r] = project(d->efc_type[r], d->prev_f[q], d->efc_fl[r]);
+          break;
+        }
+    }
   /* keep the warm start only if its dual cost beats f = 0 */
   memcpy(v, d->qacc_smooth, nv * sizeof(double));
   for (int r = 0; r < ne; r++)
@@ -678,6 +703,10 @@ void orc_solve_pgs(const orc_model* om, orc_data* d) {
     }
   }
   d->solver_iter = it;
+  if (om->pgs_warm == 1) {
+    d->prev_n = ne;
+    for (int r = 0; r < ne; r++) d->prev_key[r] = row_key(d, r), d->prev_f[r] = f[r];
+  }
   orc_stats[0] += 1;
   orc_stats[1] += it;
   orc_stats[2] += ne;
@@ -1041,6 +1070,7 @@ static void make_om(orc_model* om, const sim_model_desc* m, const float* hv, con
   om->mass_scale = params ? params[0] : 1.0;
   om->friction = params ? params[1] : -1.0;
   om->damping_scale = params ? params[2] : 1.0;
+  om->pgs_warm = 0;
 }
 
 static void write_obs(const sim_model_desc* m, const orc_data* d, double* obs) {
@@ -1399,5 +1429,62 @@ void orc_ik_dls(const sim_model_desc* m, int n, const double* target, const doub
     for (int i = 0; i < m->nq; i++) q[e * m->nq + i] = d.qpos[i];
     if (ok) ok[e] = success;
     if (iters) iters[e] = it;
+  }
+}
+
+/* ---------------------------------------------------------------------------
+ * Experiment harness (tools/pgs_warm_exp.py; test infrastructure): n envs for T env-steps of
+ * `nsub` substeps with per-step actions [T][n][nact], persistent per-env data, PGS with warm
+ * start `mode` (orc_model.pgs_warm).  Per env-step and env: out_sweeps = mean PGS sweeps per
+ * substep, out_gap[.][2] = max over the step's substeps of |qacc_PGS - qacc_Newton-exact| on
+ * the arm dofs / the free dofs, for the same constraint problem (same rows).
+ * ------------------------------------------------------------------------- */
+void orc_experiment_pgs(const sim_model_desc* m, const float* hv, const int32_t* hadr, const int32_t* hadj,
+                        int n, const double* qpos, const double* qvel, const double* warm, const double* actions,
+                        int T, int nsub, int mode, int nthreads, double* out_sweeps, double* out_gap,
+                        double* qpos_out) {
+  int32_t seeds[SIM_MAXGEOM * ORC_NSEED];
+  if (hv) orc_hull_seeds(m, hv, seeds);
+#ifdef _OPENMP
+  if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel for num_threads(nthreads) schedule(dynamic, 1)
+#endif
+  for (int e = 0; e < n; e++) {
+    orc_model om;
+    make_om(&om, m, hv, hadr, hadj, NULL);
+    om.hull_seed = hv ? seeds : NULL;
+    om.pgs_warm = mode;
+    orc_model ex = om;
+    sim_model_desc mx = *m;
+    mx.solver = SIM_SOL_NEWTON;
+    mx.tolerance = 0;
+    ex.m = &mx;
+    orc_data* d = (orc_data*)calloc(1, sizeof(orc_data));
+    orc_data* t = (orc_data*)calloc(1, sizeof(orc_data));
+    for (int i = 0; i < m->nq; i++) d->qpos[i] = qpos[e * m->nq + i];
+    for (int i = 0; i < m->nv; i++) d->qvel[i] = qvel[e * m->nv + i], d->qacc_warmstart[i] = warm[e * m->nv + i];
+    for (int s = 0; s < T; s++) {
+      for (int i = 0; i < m->nact; i++) d->ctrl[i] = actions[((size_t)s * n + e) * m->nact + i];
+      double sw = 0, ga = 0, gf = 0;
+      for (int k = 0; k < nsub; k++) {
+        orc_step(&om, d);
+        sw += d->solver_iter;
+        /* the exact optimum of this substep's problem: rebuild the same rows from the state
+           the step started at is not kept, so re-solve from d's rows (kept by orc_step) */
+        memcpy(t, d, sizeof(orc_data));
+        if (t->nefc) orc_solve_newton(&ex, t, 0.0);
+        for (int i = 0; i < m->nv; i++) {
+          const double g = fabs(t->qacc[i] - d->qacc[i]);
+          if (i < 6) ga = fmax(ga, g); else gf = fmax(gf, g);
+        }
+      }
+      out_sweeps[(size_t)s * n + e] = sw / nsub;
+      out_gap[((size_t)s * n + e) * 2] = ga;
+      out_gap[((size_t)s * n + e) * 2 + 1] = gf;
+    }
+    if (qpos_out)
+      for (int i = 0; i < m->nq; i++) qpos_out[e * m->nq + i] = d->qpos[i];
+    free(d);
+    free(t);
   }
 }

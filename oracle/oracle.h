@@ -36,6 +36,9 @@ typedef struct orc_model {
   double mass_scale;
   double friction; /* <0: use geom_friction */
   double damping_scale;
+  int pgs_warm; /* experiment (tools/pgs_warm_exp.py): 0 = mj_solPGS's warm start from qacc_warmstart,
+                   1 = the previous substep's forces for rows that persist (same dof / limit / pair
+                   contact slot and edge), the implied force for new rows */
 } orc_model;
 
 typedef struct orc_contact {
@@ -79,6 +82,10 @@ typedef struct orc_data {
   double efc_R[ORC_MAXEFC], efc_diag[ORC_MAXEFC], efc_fl[ORC_MAXEFC];
   double efc_force[ORC_MAXEFC];
   int solver_iter;
+  /* previous substep's rows (pgs_warm = 1): key per row and its force */
+  int prev_n;
+  int prev_key[ORC_MAXEFC];
+  double prev_f[ORC_MAXEFC];
   /* flop counter (SURVEY.md §8d binding procedure) */
   double flops;
   double cflops; /* the collision share of flops */
