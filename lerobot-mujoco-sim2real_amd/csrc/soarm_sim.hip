@@ -15,6 +15,7 @@
 #include <type_traits>
 #include <mutex>
 #include <thread>
+#include <dlfcn.h>
 #include <sched.h>
 #include <vector>
 
@@ -37,6 +38,40 @@ int soarm_set_error(int code, const std::string& msg) { return fail(code, msg); 
     hipError_t e_ = (x);                                                              \
     if (e_ != hipSuccess) return fail(SIM_E_HIP, std::string(#x ": ") + hipGetErrorString(e_)); \
   } while (0)
+
+// ------------------------------------------------------------------ tracing
+// roctx ranges (SURVEY.md §5 tracing): with SOARM_ROCTX=1 every ABI call, and each stage of the
+// contact env-step (geom poses, collide, substep, per substep), is bracketed by a roctx range
+// that `rocprofv3 --marker-trace` records beside the kernel trace.  The roctx library is opened
+// at run time, so the product has no link dependency on the profiler; the env-step is then
+// launched stage by stage (no hipGraph replay) so that the ranges bracket real launches.
+struct Roctx {
+  int (*push)(const char*) = nullptr;
+  int (*pop)() = nullptr;
+  Roctx() {
+    const char* on = getenv("SOARM_ROCTX");
+    if (!on || on[0] != '1') return;
+    void* h = dlopen("librocprofiler-sdk-roctx.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("libroctx64.so.4", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) return;
+    push = (int (*)(const char*))dlsym(h, "roctxRangePushA");
+    pop = (int (*)())dlsym(h, "roctxRangePop");
+    if (!push || !pop) push = nullptr, pop = nullptr;
+  }
+};
+static const Roctx& roctx() {
+  static const Roctx r;
+  return r;
+}
+struct TraceRange {
+  const bool on;
+  explicit TraceRange(const char* name) : on(roctx().push != nullptr) {
+    if (on) roctx().push(name);
+  }
+  ~TraceRange() {
+    if (on) roctx().pop();
+  }
+};
 
 // read-only model data on one device (constants, hull records, support LUT):
 // uploaded by the first batch created on that device, shared by every later
@@ -1269,6 +1304,7 @@ static int check_state(const sim_batch* b, const sim_state* s) {
 int sim_reset(sim_batch* b, const sim_state* s, const float* init_qpos, const float* init_qvel,
               const float* extra_qpos, uint64_t seed, int64_t env_offset, const uint8_t* mask,
               float* obs, void* stream) {
+  const TraceRange tr_("sim_reset");
   if (int rc = check_state(b, s)) return rc;
   hipStream_t st = (hipStream_t)stream;
   dispatch_nf(b->model->nf, [&](auto nfc) {
@@ -1284,6 +1320,7 @@ int sim_reset(sim_batch* b, const sim_state* s, const float* init_qpos, const fl
 
 int sim_step(sim_batch* b, const sim_state* s, const float* action, int frame_skip, float* obs,
              void* stream) {
+  const TraceRange tr_("sim_step");
   if (int rc = check_state(b, s)) return rc;
   if (frame_skip < 1) return fail(SIM_E_ARG, "frame_skip must be >= 1");
   hipStream_t st = (hipStream_t)stream;
@@ -1309,16 +1346,21 @@ int sim_step(sim_batch* b, const sim_state* s, const float* action, int frame_sk
     dispatch_nf(b->model->nf, [&](auto nfc) {
       constexpr int NA = 6, NF = decltype(nfc)::value;
       prof_mark(b, 3, q);
-      hipLaunchKernelGGL((k_geom<NA, NF>), geom_grid(b->n), dim3(64), 0, q, b->d_model, b->n, *s,
-                         b->d_gpose);
+      {
+        const TraceRange tr_("geom_poses");
+        hipLaunchKernelGGL((k_geom<NA, NF>), geom_grid(b->n), dim3(64), 0, q, b->d_model, b->n, *s,
+                           b->d_gpose);
+      }
       prof_mark(b, -1, q);
       for (int sub = 0; sub < frame_skip; sub++) {
         if (np > 0) {
           prof_mark(b, 1, q);
+          const TraceRange tr_("collide");
           launch_collide(b, q, nullptr);
           prof_mark(b, -1, q);
         }
         const bool last = sub == frame_skip - 1;
+        const TraceRange tr_("substep");
         prof_mark(b, 2, q);
         auto kern = s->qfrc_applied ? k_substep<NA, NF, true> : k_substep<NA, NF, false>;
         hipLaunchKernelGGL(kern, dim3((b->n + 64 / lpe<NF>() - 1) / (64 / lpe<NF>())), dim3(64), 0, q,
@@ -1330,7 +1372,7 @@ int sim_step(sim_batch* b, const sim_state* s, const float* action, int frame_sk
       }
     });
   };
-  if (b->prof || !b->use_graphs) {  // profiling brackets every launch with events: no graph
+  if (b->prof || !b->use_graphs || roctx().push) {  // profiling / tracing brackets every launch: no graph
     enqueue(st);
     HIPCHECK(hipGetLastError());
     return SIM_OK;
@@ -1382,6 +1424,7 @@ int sim_profile_end(sim_batch* b, double* ms, int32_t* launches) {
 }
 
 int sim_contacts(sim_batch* b, const sim_state* s, float* out, int32_t* ncon, void* stream) {
+  const TraceRange tr_("sim_contacts");
   if (int rc = check_state(b, s)) return rc;
   if (!out || !ncon) return fail(SIM_E_ARG, "null output");
   if (b->model->desc.disable_contact) return fail(SIM_E_ARG, "model compiled with contacts disabled");
@@ -1446,6 +1489,7 @@ int sim_phase_profile(double* out, int reset) {
 
 int sim_rand_uniform(sim_batch* b, uint64_t seed, int64_t env_offset, uint32_t counter, int k, float lo,
                      float hi, float* out, void* stream) {
+  const TraceRange tr_("sim_rand_uniform");
   if (!b || !out) return fail(SIM_E_ARG, "null argument");
   if (k < 1 || k > 64) return fail(SIM_E_ARG, "k must be in [1, 64]");
   hipLaunchKernelGGL(k_rand, grid_for(b->n), dim3(64), 0, (hipStream_t)stream, b->n, (uint32_t)seed,
@@ -1459,6 +1503,7 @@ int sim_substeps(sim_batch* b, const sim_state* s, int nsub, void* stream) {
 }
 
 int sim_bias(sim_batch* b, const sim_state* s, float* qfrc_bias, void* stream) {
+  const TraceRange tr_("sim_bias");
   if (int rc = check_state(b, s)) return rc;
   if (!qfrc_bias) return fail(SIM_E_ARG, "qfrc_bias is null");
   hipStream_t st = (hipStream_t)stream;
@@ -1472,6 +1517,7 @@ int sim_bias(sim_batch* b, const sim_state* s, float* qfrc_bias, void* stream) {
 }
 
 int sim_observe(sim_batch* b, const sim_state* s, float* obs, void* stream) {
+  const TraceRange tr_("sim_observe");
   if (int rc = check_state(b, s)) return rc;
   if (!obs) return fail(SIM_E_ARG, "obs is null");
   hipStream_t st = (hipStream_t)stream;
@@ -1486,6 +1532,7 @@ int sim_observe(sim_batch* b, const sim_state* s, float* obs, void* stream) {
 
 int sim_ik_dls_pose(sim_batch* b, const float* target, const float* target_quat, float* q, int32_t* ok,
                     int32_t* iters, const sim_ik_opts* opts, void* stream) {
+  const TraceRange tr_("sim_ik_dls");
   if (!b || !target || !q || !opts) return fail(SIM_E_ARG, "null argument");
   if (opts->ndof < 1 || opts->ndof > 6 || opts->max_steps < 0) return fail(SIM_E_ARG, "bad ik options");
   hipStream_t st = (hipStream_t)stream;
