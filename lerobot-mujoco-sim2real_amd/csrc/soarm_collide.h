@@ -474,27 +474,61 @@ DEVI void plane_convex(const DModel& m, int gp, int g, const GeomPose& Pp, const
   emit(o, dist, pos, n);
 }
 
-DEVI int clip_poly(const float in[][3], int n, float out[][3], const float o[3], const float a[3], float lim) {
+// Polygon clipping and box-box face selection keep every array in registers: loops over the
+// (at most 8) polygon slots are unrolled, and lane-varying indices (the polygon size, the
+// wrap-around neighbour, the next output slot, the reference face / incident axis) pick their
+// element by selects over compile-time indices.  A dynamically indexed private array would
+// live in scratch memory (k_collide had 656 B of scratch per lane).
+// (value selects, v_cndmask: a conditional store `if (j == k) out[j] = x` is merged by the
+// optimizer into one store through a computed index, which sends the array to scratch)
+DEVI void put8(float out[8][3], int k, const float x[3]) {
+#pragma unroll
+  for (int j = 0; j < 8; j++)
+#pragma unroll
+    for (int c = 0; c < 3; c++) out[j][c] = j == k ? x[c] : out[j][c];
+}
+template <int R>
+DEVI void row3(const float M[R][3], int i, float out[3]) {
+#pragma unroll
+  for (int c = 0; c < 3; c++) out[c] = M[0][c];
+#pragma unroll
+  for (int j = 1; j < R; j++)
+#pragma unroll
+    for (int c = 0; c < 3; c++) out[c] = j == i ? M[j][c] : out[c];
+}
+DEVI float pick3(const float* h, int i) { return i == 0 ? h[0] : (i == 1 ? h[1] : h[2]); }
+
+// one Sutherland-Hodgman step: keep the part of polygon in[0..n) with (x - o).a <= lim
+DEVI int clip_poly8(const float in[8][3], int n, float out[8][3], const float o[3], const float a[3], float lim) {
+  float sd[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    float r[3];
+    sub(r, in[i], o);
+    sd[i] = dot3(r, a) - lim;
+  }
   int k = 0;
-  for (int i = 0; i < n; i++) {
-    const float* P = in[i];
-    const float* Q = in[(i + 1) % n];
-    float rp[3], rq[3];
-    sub(rp, P, o);
-    sub(rq, Q, o);
-    const float sp = dot3(rp, a) - lim, sq = dot3(rq, a) - lim;
-    if (sp <= 0.f) {
-      out[k][0] = P[0], out[k][1] = P[1], out[k][2] = P[2];
-      k++;
-    }
-    if ((sp < 0.f && sq > 0.f) || (sp > 0.f && sq < 0.f)) {
-      const float t = sp / (sp - sq);
-      out[k][0] = P[0] + t * (Q[0] - P[0]), out[k][1] = P[1] + t * (Q[1] - P[1]),
-      out[k][2] = P[2] + t * (Q[2] - P[2]);
-      k++;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    if (i < n) {
+      const bool wrap = i + 1 >= n;
+      const float sp = sd[i], sq = wrap ? sd[0] : sd[(i + 1) & 7];
+      const float Q[3] = {wrap ? in[0][0] : in[(i + 1) & 7][0], wrap ? in[0][1] : in[(i + 1) & 7][1],
+                          wrap ? in[0][2] : in[(i + 1) & 7][2]};
+      if (sp <= 0.f) {
+        put8(out, k, in[i]);
+        k++;
+      }
+      if ((sp < 0.f && sq > 0.f) || (sp > 0.f && sq < 0.f)) {
+        const float t = sp / (sp - sq);
+        const float X[3] = {in[i][0] + t * (Q[0] - in[i][0]), in[i][1] + t * (Q[1] - in[i][1]),
+                            in[i][2] + t * (Q[2] - in[i][2])};
+        put8(out, k, X);
+        k++;
+      }
     }
   }
-  return k;
+  return k < 8 ? k : 8;
 }
 
 DEVI void box_box(const DModel& m, int g1, int g2, const GeomPose& P1, const GeomPose& P2, PairOut& o) {
@@ -538,18 +572,22 @@ DEVI void box_box(const DModel& m, int g1, int g2, const GeomPose& P1, const Geo
   if (bcode < 6) {
     const bool ref1 = bcode < 3;
     const int fa = ref1 ? bcode : bcode - 3;
-    const float* cr = ref1 ? P1.p : P2.p;
-    const float* ci = ref1 ? P2.p : P1.p;
-    const float(*Ar)[3] = ref1 ? A : B;
-    const float(*Ai)[3] = ref1 ? B : A;
+    float Ar[3][3], Ai[3][3], cr[3], ci[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      cr[k] = ref1 ? P1.p[k] : P2.p[k], ci[k] = ref1 ? P2.p[k] : P1.p[k];
+#pragma unroll
+      for (int e = 0; e < 3; e++) Ar[k][e] = ref1 ? A[k][e] : B[k][e], Ai[k][e] = ref1 ? B[k][e] : A[k][e];
+    }
     const float* hr = ref1 ? h1 : h2;
     const float* hi = ref1 ? h2 : h1;
     float nr[3];
 #pragma unroll
     for (int k = 0; k < 3; k++) nr[k] = ref1 ? bn[k] : -bn[k];
+    const float hfa = pick3(hr, fa);
     float fc[3];
 #pragma unroll
-    for (int k = 0; k < 3; k++) fc[k] = cr[k] + nr[k] * hr[fa];
+    for (int k = 0; k < 3; k++) fc[k] = cr[k] + nr[k] * hfa;
     int ia = 0;
     float bd = 0.f;
 #pragma unroll
@@ -557,27 +595,37 @@ DEVI void box_box(const DModel& m, int g1, int g2, const GeomPose& P1, const Geo
       const float dd = fabsf(dot3(Ai[k], nr));
       if (dd > bd) bd = dd, ia = k;
     }
-    const float s = dot3(Ai[ia], nr) > 0.f ? -1.f : 1.f;
+    float aia[3], au[3], av[3];
     const int u = (ia + 1) % 3, v = (ia + 2) % 3;
-    float poly[16][3], tmp[16][3];
+    row3<3>(Ai, ia, aia);
+    row3<3>(Ai, u, au);
+    row3<3>(Ai, v, av);
+    const float s = dot3(aia, nr) > 0.f ? -1.f : 1.f;
+    const float hia = pick3(hi, ia), hu = pick3(hi, u), hv = pick3(hi, v);
+    float poly[8][3], tmp[8][3] = {};
     const float su[4] = {1, -1, -1, 1}, sv[4] = {1, 1, -1, -1};
 #pragma unroll
     for (int q = 0; q < 4; q++)
 #pragma unroll
-      for (int k = 0; k < 3; k++)
-        poly[q][k] = ci[k] + s * hi[ia] * Ai[ia][k] + su[q] * hi[u] * Ai[u][k] + sv[q] * hi[v] * Ai[v][k];
+      for (int k = 0; k < 3; k++) poly[q][k] = ci[k] + s * hia * aia[k] + su[q] * hu * au[k] + sv[q] * hv * av[k];
+#pragma unroll
+    for (int q = 4; q < 8; q++) poly[q][0] = poly[q][1] = poly[q][2] = 0.f;
+    const int ra = (fa + 1) % 3, rb = (fa + 2) % 3;
+    float ara[3], arb[3];
+    row3<3>(Ar, ra, ara);
+    row3<3>(Ar, rb, arb);
+    const float hra = pick3(hr, ra), hrb = pick3(hr, rb);
     {
       // fast path (cube resting on the table): the incident face lies inside the reference
       // face's side slabs, so clipping is the identity; emit penetrating corners deepest first
       // (the same stable order as the general path), all with compile-time indices.
-      const int ra = (fa + 1) % 3, rb = (fa + 2) % 3;
       bool inside = true;
       float dep[4];
 #pragma unroll
       for (int q = 0; q < 4; q++) {
         float rel[3];
         sub(rel, poly[q], fc);
-        inside = inside && fabsf(dot3(rel, Ar[ra])) <= hr[ra] && fabsf(dot3(rel, Ar[rb])) <= hr[rb];
+        inside = inside && fabsf(dot3(rel, ara)) <= hra && fabsf(dot3(rel, arb)) <= hrb;
         dep[q] = dot3(rel, nr);
       }
       if (inside) {
@@ -603,39 +651,48 @@ DEVI void box_box(const DModel& m, int g1, int g2, const GeomPose& P1, const Geo
       }
     }
     int n = 4;
-    const int ra = (fa + 1) % 3, rb = (fa + 2) % 3;
     float na[3];
-    n = clip_poly(poly, n, tmp, fc, Ar[ra], hr[ra]);
-    na[0] = -Ar[ra][0], na[1] = -Ar[ra][1], na[2] = -Ar[ra][2];
-    n = clip_poly(tmp, n, poly, fc, na, hr[ra]);
-    n = clip_poly(poly, n, tmp, fc, Ar[rb], hr[rb]);
-    na[0] = -Ar[rb][0], na[1] = -Ar[rb][1], na[2] = -Ar[rb][2];
-    n = clip_poly(tmp, n, poly, fc, na, hr[rb]);
-    float dep[16];
-    int idx[16], mcnt = 0;
-    for (int q = 0; q < n; q++) {
+    n = clip_poly8(poly, n, tmp, fc, ara, hra);
+    na[0] = -ara[0], na[1] = -ara[1], na[2] = -ara[2];
+    n = clip_poly8(tmp, n, poly, fc, na, hra);
+    n = clip_poly8(poly, n, tmp, fc, arb, hrb);
+    na[0] = -arb[0], na[1] = -arb[1], na[2] = -arb[2];
+    n = clip_poly8(tmp, n, poly, fc, na, hrb);
+    // penetrating vertices, deepest first (stable: ties keep polygon order), at most 4
+    float dep[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
       float rel[3];
       sub(rel, poly[q], fc);
       const float sd = dot3(rel, nr);
-      if (sd < 0.f) dep[mcnt] = sd, idx[mcnt] = q, mcnt++;
+      dep[q] = (q < n && sd < 0.f) ? sd : 0.f;
     }
-    for (int a = 1; a < mcnt; a++)
-      for (int b = a; b > 0 && dep[b] < dep[b - 1]; b--) {
-        const float td = dep[b];
-        dep[b] = dep[b - 1], dep[b - 1] = td;
-        const int ti = idx[b];
-        idx[b] = idx[b - 1], idx[b - 1] = ti;
-      }
-    for (int q = 0; q < mcnt && q < 4; q++) {
-      const float* pp = poly[idx[q]];
-      const float pos[3] = {pp[0] - 0.5f * dep[q] * nr[0], pp[1] - 0.5f * dep[q] * nr[1],
-                            pp[2] - 0.5f * dep[q] * nr[2]};
-      emit(o, dep[q], pos, bn);
+    unsigned used = 0;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      int best = -1;
+      float bdep = 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; q++)
+        if (!((used >> q) & 1u) && dep[q] < bdep) bdep = dep[q], best = q;
+      if (best < 0) break;
+      used |= 1u << best;
+      float pos[3] = {0, 0, 0};
+#pragma unroll
+      for (int q = 0; q < 8; q++)
+        if (q == best)
+#pragma unroll
+          for (int k = 0; k < 3; k++) pos[k] = poly[q][k] - 0.5f * bdep * nr[k];
+      emit(o, bdep, pos, bn);
     }
     return;
   }
-  // edge-edge
+  // edge-edge (the edge rows picked by selects: a computed index into A / B would put them in scratch)
   const int ea = (bcode - 6) / 3, eb = (bcode - 6) % 3;
+  float aea[3], beb[3];
+  row3<3>(A, ea, aea);
+  row3<3>(B, eb, beb);
+  const float h1a = pick3(h1, ea), h2b = pick3(h2, eb);
   float p1[3] = {P1.p[0], P1.p[1], P1.p[2]}, p2[3] = {P2.p[0], P2.p[1], P2.p[2]};
 #pragma unroll
   for (int k = 0; k < 3; k++) {
@@ -652,15 +709,15 @@ DEVI void box_box(const DModel& m, int g1, int g2, const GeomPose& P1, const Geo
   }
   float r[3];
   sub(r, p1, p2);
-  const float b = dot3(A[ea], B[eb]), c = dot3(A[ea], r), f = dot3(B[eb], r);
+  const float b = dot3(aea, beb), c = dot3(aea, r), f = dot3(beb, r);
   const float den = 1.f - b * b;
   float sp = den > 1e-12f ? (b * f - c) / den : 0.f;
   float tp = b * sp + f;
-  sp = fminf(fmaxf(sp, -h1[ea]), h1[ea]);
-  tp = fminf(fmaxf(tp, -h2[eb]), h2[eb]);
+  sp = fminf(fmaxf(sp, -h1a), h1a);
+  tp = fminf(fmaxf(tp, -h2b), h2b);
   float pos[3];
 #pragma unroll
-  for (int k = 0; k < 3; k++) pos[k] = 0.5f * (p1[k] + sp * A[ea][k] + p2[k] + tp * B[eb][k]);
+  for (int k = 0; k < 3; k++) pos[k] = 0.5f * (p1[k] + sp * aea[k] + p2[k] + tp * beb[k]);
   emit(o, -best / 1.05f, pos, bn);
 }
 

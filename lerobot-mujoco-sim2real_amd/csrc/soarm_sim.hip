@@ -324,7 +324,10 @@ __global__ __launch_bounds__(64) void k_geom(const DModel* __restrict__ dm, int 
 inline dim3 geom_grid(int n) { return dim3((n + 64 / GEOM_LPE - 1) / (64 / GEOM_LPE)); }
 
 // mj_collision, one lane per (env, candidate pair); blockIdx.y = pair
-__global__ __launch_bounds__(256, 3) void k_collide(const DModel* __restrict__ dm, int n,
+#ifndef SOARM_COLLIDE_WAVES
+#define SOARM_COLLIDE_WAVES 3  // min waves per SIMD (VGPR cap 512 / 3 = 168)
+#endif
+__global__ __launch_bounds__(256, SOARM_COLLIDE_WAVES) void k_collide(const DModel* __restrict__ dm, int n,
                                                  const float* __restrict__ gpose,
                                                  float* __restrict__ cbuf, int* __restrict__ ccount,
                                                  uint32_t* __restrict__ pmask,
