@@ -39,6 +39,8 @@ def parse():
     p.add_argument("--config", default="contact",
                    choices=["contact", "nocontact", "dr", "rollout", "mpc", "plumbing"])
     p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal on one GPU)")
+    p.add_argument("--solver", default="pgs", choices=["pgs", "newton"],
+                   help="constraint solver: PGS (BASELINE config 3) or MuJoCo's default Newton")
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -89,7 +91,7 @@ def launch_ranks(args):
     return bad[0] if bad else 0
 
 
-def cpu_baseline(cfg_name, seconds, seed):
+def cpu_baseline(cfg_name, seconds, seed, solver="pgs"):
     """The float64 oracle (C restatement of mj_step; for `mpc` plus the numpy MPC restatement)
     on the host cores, a bounded sample of the same workload: chunks of envs x T env-steps."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -98,7 +100,7 @@ def cpu_baseline(cfg_name, seconds, seed):
     from lerobot_mujoco_sim2real_amd import workloads as W
 
     cfg = W.CONFIGS[cfg_name]
-    cm = W.model(cfg_name)
+    cm = W.model(cfg_name, solver=solver)
     orc = Oracle(cm)
     try:
         cores = len(os.sched_getaffinity(0))
@@ -236,7 +238,7 @@ def main():
     cfg = W.CONFIGS[name]
     n = args.envs or cfg.get("envs", 4096)
     ids = np.arange(rank * n, (rank + 1) * n)
-    cm = W.model(name)
+    cm = W.model(name, solver=args.solver)
     sim = BatchSim(cm, n, gpu)
     q0 = W.initial_qpos(cm, ids, args.seed)
     sim.reset(init_qpos=q0[:, :5], extra_qpos=q0, seed=args.seed, env_offset=rank * n)
@@ -374,7 +376,8 @@ def main():
     # dominant kernel: HIP events (on the sim's stream) around every launch of a replay of
     # the timed region -- state, action stream and step index restored from the snapshot
     roof = None
-    cost = json.load(open(os.path.join(ROOT, "profiles", "algorithmic_cost.json")))[name]
+    costs = json.load(open(os.path.join(ROOT, "profiles", "algorithmic_cost.json")))
+    cost = costs.get(name if args.solver == "pgs" else f"{name}_newton", costs[name])
     if not args.no_profile:
         kp = args.steps
         restore_timed()
@@ -438,7 +441,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(name, args.cpu_seconds, args.seed)
+        cpu = cpu_baseline(name, args.cpu_seconds, args.seed, args.solver)
 
     if rank == 0:
         line = {
@@ -449,7 +452,8 @@ def main():
             "config": {"workload": cfg["desc"], "config": name, "envs_per_gpu": n, "global_envs": total_envs,
                        "frame_skip": 10, "substeps_per_s": value * 10,
                        "contacts_per_env_substep": contacts,
-                       "solver": "PGS (iterations 100, tol 1e-8, scale 1/(meaninertia nv))",
+                       "solver": ("PGS (iterations 100, tol 1e-8, scale 1/(meaninertia nv))" if args.solver == "pgs"
+                                  else "Newton (MuJoCo's default: iterations 100, tol 1e-8, exact line search)"),
                        "parallelism": f"env-sharded x{world} (no per-step collective)"},
             "steady_state": steady,
             "dist": {"world_size": world, "backend": (args.dist_backend if world > 1 else None),

@@ -15,7 +15,7 @@ from .abi import LIB_PATH, PKG_DIR
 
 SRC_DIR = os.path.join(PKG_DIR, "csrc")
 SOURCES = ["soarm_sim.hip", "koopman_mpc.hip"]
-HEADERS = ["dmodel.h", "soarm_kernels.h", "soarm_step.h", "soarm_collide.h", "soarm_pgs.h"]
+HEADERS = ["dmodel.h", "soarm_kernels.h", "soarm_step.h", "soarm_collide.h", "soarm_pgs.h", "soarm_newton.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # -fno-slp-vectorize: the per-lane algebra gains nothing from v_pk_* packing; the
 # packing's operand shuffles (v_mov) and the extra register pressure (AGPR

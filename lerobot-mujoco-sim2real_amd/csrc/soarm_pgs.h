@@ -339,10 +339,15 @@ DEVI void gram_step(float* v6, const float* jn, const float* j1, const float* j2
   for (int i = 0; i < 6; i++) v6[i] += Fd[i] * (jn[i] * Dn + j1[i] * D1 + j2[i] * D2);
 }
 
-// Builds every constraint row, solves the dual by PGS, sets S.qacc / S.fcon.
+}  // namespace soarm
+#include "soarm_newton.h"
+namespace soarm {
+
+// Builds every constraint row, solves the dual by PGS (or, SOL = Newton, the primal by
+// soarm_newton.h), sets S.qacc / S.fcon.
 // Contacts are read straight from the collide output (pair mask + cbuf, pair
 // order).  Returns the number of contacts used.
-template <int NA, int NF, bool CON>
+template <int NA, int NF, bool CON, int SOL = SIM_SOL_PGS>
 DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const int* __restrict__ ccount,
                            const uint32_t* __restrict__ pmask, int n, int e, const RowLds& L,
                            const ContactRows<NA, NF>& cr, const PairMask& pm) {
@@ -606,6 +611,11 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   RP_MARK(3);
   RP_STORE;
   const int nl = ncon < LDS_CON ? ncon : LDS_CON;
+  if constexpr (SOL == SIM_SOL_NEWTON) {  // MuJoCo's default solver on the same rows (soarm_newton.h)
+    const NewtonRows<NA, NF, CON> nr{m, L, cr, fR, fa, nlim, nl, ncon};
+    newton_solve(S, nr);
+    return ncon;
+  }
 #ifdef SOARM_PHASE_PROF
   if (e < 65536) g_pgs_prof[8 * e + 6] = clock64();  // rows built
   PSTAMP(8);

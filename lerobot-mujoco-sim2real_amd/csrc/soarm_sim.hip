@@ -252,7 +252,7 @@ __device__ unsigned long long g_phase[77];  // [53..56] contact-row build split 
 
 // one mj_forward (position + velocity + acceleration stages); the contacts
 // (cbuf/ccount, may be null) were produced by k_collide from this substep's positions
-template <int NA, int NF, bool CON>
+template <int NA, int NF, bool CON, int SOL>
 DEVI int forward(Sim<NA, NF>& S, const float* cbuf, const int* ccount, const uint32_t* pmask, int n, int e,
                  const RowLds& L, const ContactRows<NA, NF>& cr, const float* applied = nullptr,
                  PairMask pm = PairMask{}) {
@@ -262,7 +262,7 @@ DEVI int forward(Sim<NA, NF>& S, const float* cbuf, const int* ccount, const uin
   S.smooth_forces();
   pm.hold();
   if (applied) S.add_applied(applied, n, e);
-  return solve_constraints<NA, NF, CON>(S, cbuf, ccount, pmask, n, e, L, cr, pm);
+  return solve_constraints<NA, NF, CON, SOL>(S, cbuf, ccount, pmask, n, e, L, cr, pm);
 }
 
 // mj_resetData zeroes d.qfrc_applied: a reset / soft reset of env e clears its row
@@ -272,7 +272,7 @@ DEVI void zero_applied(float* applied, int nv, int n, int e) {
 
 // contact-free scenes (mjDSBL_CONTACT): all frame_skip substeps fused in one launch.
 // AP: st.qfrc_applied is set (a separate instantiation keeps the common case's code as is)
-template <int NA, int NF, bool AP>
+template <int NA, int NF, bool AP, int SOL>
 __global__ __launch_bounds__(64) void k_step(const DModel* __restrict__ dm, int n, int nsub,
                                              sim_state st, const float* __restrict__ action,
                                              float* __restrict__ obs, sim_params pp) {
@@ -296,11 +296,11 @@ __global__ __launch_bounds__(64) void k_step(const DModel* __restrict__ dm, int 
     const int sb = S.status;
     S.check_state();
     if (AP && S.status != sb) zero_applied(applied, Sim<NA, NF>::NV, n, e);
-    forward<NA, NF, false>(S, nullptr, nullptr, nullptr, n, e, L, cr, applied);
+    forward<NA, NF, false, SOL>(S, nullptr, nullptr, nullptr, n, e, L, cr, applied);
     if (S.acc_bad()) {
       S.soft_reset(SIM_ST_BADQACC);
       if (AP) zero_applied(applied, Sim<NA, NF>::NV, n, e);
-      forward<NA, NF, false>(S, nullptr, nullptr, nullptr, n, e, L, cr);
+      forward<NA, NF, false, SOL>(S, nullptr, nullptr, nullptr, n, e, L, cr);
     }
     S.integrate();
   }
@@ -388,7 +388,7 @@ DEVI int gather_contacts(const DModel& m, int n, int e, const float* __restrict_
 
 // one substep with contacts: gather -> forward -> Euler -> next substep's geom poses
 // (AP: st.qfrc_applied is set, as in k_step)
-template <int NA, int NF, bool AP>
+template <int NA, int NF, bool AP, int SOL>
 __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, int n, sim_state st,
                                                 const float* __restrict__ action,
                                                 float* __restrict__ obs, sim_params pp,
@@ -414,7 +414,8 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
   __shared__ float s_rows[(LDS_CON + 1) * CF][COLS];  // + one all-zero record
   __shared__ float s_lim[NA * LF][COLS];
   __shared__ float s_keep[keep_floats<NA, NF>()][COLS];
-  __shared__ float s_ext[NF == 1 ? XS_EXT : (lpe<NF>() == 4 ? XS_LIST : 1)][COLS];  // contact list (quad), y-sweep slots
+  // contact list (quad), y-sweep slots; Newton: its line-search rows (8 per LDS contact)
+  __shared__ float s_ext[NF == 1 ? XS_EXT : (lpe<NF>() == 4 ? XS_LIST + (SOL == SIM_SOL_NEWTON ? 8 * LDS_CON : 0) : 1)][COLS];
   const RowLds L{&s_rows[0][0], &s_lim[0][0], NF == 1 ? &s_keep[0][0] : nullptr, &s_ext[0][0], (int)threadIdx.x,
                  (int)threadIdx.x / lpe<NF>(), COLS};
   const ContactRows<NA, NF> cr{scratch + e, n};
@@ -446,16 +447,16 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
   PSTAMP(5);
   pm.hold();
   if (AP) S.add_applied(st.qfrc_applied, n, e);
-  int ncon = solve_constraints<NA, NF, true>(S, use ? cbuf : nullptr, use ? ccount : nullptr, pmask, n, e, L, cr, pm);
+  int ncon = solve_constraints<NA, NF, true, SOL>(S, use ? cbuf : nullptr, use ? ccount : nullptr, pmask, n, e, L, cr, pm);
 #else
-  int ncon = forward<NA, NF, true>(S, use ? cbuf : nullptr, use ? ccount : nullptr, pmask, n, e, L, cr,
-                                   AP ? st.qfrc_applied : nullptr, pm);
+  int ncon = forward<NA, NF, true, SOL>(S, use ? cbuf : nullptr, use ? ccount : nullptr, pmask, n, e, L, cr,
+                                        AP ? st.qfrc_applied : nullptr, pm);
 #endif
   if (S.acc_bad()) {
     S.soft_reset(SIM_ST_BADQACC);
     store_state(S, st, n, e);
     if (AP) zero_applied(st.qfrc_applied, Sim<NA, NF>::NV, n, e);
-    ncon = forward<NA, NF, true>(S, nullptr, nullptr, nullptr, n, e, L, cr);
+    ncon = forward<NA, NF, true, SOL>(S, nullptr, nullptr, nullptr, n, e, L, cr);
   }
   PSTAMP(10);
   if constexpr (NF == 1) {  // reload (laundered pointers: not CSE'd with the first load)
@@ -798,6 +799,15 @@ static void dispatch_nf(int nf, F&& f) {
     f(std::integral_constant<int, 1>{});
 }
 
+// solver of the compiled model: PGS (the north star's) or MuJoCo's default Newton
+template <class F>
+static void dispatch_sol(int sol, F&& f) {
+  if (sol == SIM_SOL_NEWTON)
+    f(std::integral_constant<int, SIM_SOL_NEWTON>{});
+  else
+    f(std::integral_constant<int, SIM_SOL_PGS>{});
+}
+
 static inline dim3 grid_for(int n) { return dim3((n + 63) / 64); }
 
 // profiling: kind >= 0 records a start event for that kernel kind, -1 the matching stop
@@ -882,8 +892,8 @@ static int validate_and_build(const sim_model_desc& d, sim_model* M) {
     nf++;
   }
   if (na != 6 || nf > 1) return fail(SIM_E_MODEL, "kernels are compiled for a 6-hinge arm + <=1 free body");
-  if (d.solver != SIM_SOL_PGS)
-    return fail(SIM_E_MODEL, "the kernels run the PGS solver (north star); Newton is CPU-oracle only");
+  if (d.solver != SIM_SOL_PGS && d.solver != SIM_SOL_NEWTON)
+    return fail(SIM_E_MODEL, "solver must be PGS or Newton");
   if (d.nv != na + 6 * nf || d.nq != na + 7 * nf) return fail(SIM_E_MODEL, "nq/nv mismatch");
   if (d.nu > na) return fail(SIM_E_MODEL, "more actuators than arm hinges");
   for (int a = 0; a < d.nu; a++)
@@ -1328,17 +1338,20 @@ int sim_step(sim_batch* b, const sim_state* s, const float* action, int frame_sk
   if (frame_skip < 1) return fail(SIM_E_ARG, "frame_skip must be >= 1");
   hipStream_t st = (hipStream_t)stream;
   const bool con = !b->model->desc.disable_contact;
+  const int sol = b->model->desc.solver;
   if (!con) {
     dispatch_nf(b->model->nf, [&](auto nfc) {
-      constexpr int NA = 6, NF = decltype(nfc)::value;
-      prof_mark(b, 0, st);
-      if (s->qfrc_applied)
-        hipLaunchKernelGGL((k_step<NA, NF, true>), grid_for(b->n), dim3(64), 0, st, b->d_model, b->n,
-                           frame_skip, *s, action, obs, b->params);
-      else
-        hipLaunchKernelGGL((k_step<NA, NF, false>), grid_for(b->n), dim3(64), 0, st, b->d_model, b->n,
-                           frame_skip, *s, action, obs, b->params);
-      prof_mark(b, -1, st);
+      dispatch_sol(sol, [&](auto solc) {
+        constexpr int NA = 6, NF = decltype(nfc)::value, SOL = decltype(solc)::value;
+        prof_mark(b, 0, st);
+        if (s->qfrc_applied)
+          hipLaunchKernelGGL((k_step<NA, NF, true, SOL>), grid_for(b->n), dim3(64), 0, st, b->d_model, b->n,
+                             frame_skip, *s, action, obs, b->params);
+        else
+          hipLaunchKernelGGL((k_step<NA, NF, false, SOL>), grid_for(b->n), dim3(64), 0, st, b->d_model, b->n,
+                             frame_skip, *s, action, obs, b->params);
+        prof_mark(b, -1, st);
+      });
     });
     HIPCHECK(hipGetLastError());
     return SIM_OK;
@@ -1347,7 +1360,8 @@ int sim_step(sim_batch* b, const sim_state* s, const float* action, int frame_sk
   const int np = b->model->desc.npair;
   auto enqueue = [&](hipStream_t q) {
     dispatch_nf(b->model->nf, [&](auto nfc) {
-      constexpr int NA = 6, NF = decltype(nfc)::value;
+     dispatch_sol(sol, [&](auto solc) {
+      constexpr int NA = 6, NF = decltype(nfc)::value, SOL = decltype(solc)::value;
       prof_mark(b, 3, q);
       {
         const TraceRange tr_("geom_poses");
@@ -1365,7 +1379,7 @@ int sim_step(sim_batch* b, const sim_state* s, const float* action, int frame_sk
         const bool last = sub == frame_skip - 1;
         const TraceRange tr_("substep");
         prof_mark(b, 2, q);
-        auto kern = s->qfrc_applied ? k_substep<NA, NF, true> : k_substep<NA, NF, false>;
+        auto kern = s->qfrc_applied ? k_substep<NA, NF, true, SOL> : k_substep<NA, NF, false, SOL>;
         hipLaunchKernelGGL(kern, dim3((b->n + 64 / lpe<NF>() - 1) / (64 / lpe<NF>())), dim3(64), 0, q,
                            b->d_model, b->n, *s,
                            sub == 0 ? action : nullptr, last ? obs : nullptr, b->params, b->d_scratch,
@@ -1373,6 +1387,7 @@ int sim_step(sim_batch* b, const sim_state* s, const float* action, int frame_sk
                            last ? nullptr : b->d_gpose);
         prof_mark(b, -1, q);
       }
+     });
     });
   };
   if (b->prof || !b->use_graphs || roctx().push) {  // profiling / tracing brackets every launch: no graph

@@ -43,13 +43,28 @@ def f32(st):
     return {k: (v.astype(np.float32).astype(np.float64) if v.dtype == np.float64 else v) for k, v in st.items()}
 
 
-def random_states(cm, orc, n, steps=3, lo=-1.0, hi=1.0):
+def random_states(cm, orc, n, steps=3, lo=-1.0, hi=1.0, rng=None):
     """Mid-trajectory states (qvel, warm start and ctrl populated) from the oracle."""
+    rng = RNG if rng is None else rng
     st = orc.new_state(n)
-    orc.reset(st, init_qpos=RNG.uniform(lo, hi, (n, 5)))
+    orc.reset(st, init_qpos=rng.uniform(lo, hi, (n, 5)))
     for _ in range(steps):
-        orc.step(st, RNG.uniform(-0.5, 0.5, (n, 5)))
+        orc.step(st, rng.uniform(-0.5, 0.5, (n, 5)))
     return f32(st)
+
+
+def assert_pct(err, p50, p99, mx, what=""):
+    """Percentile bars on an error sample (per env: the max over the compared fields)."""
+    e = np.asarray(err, np.float64).ravel()
+    got = (float(np.median(e)), float(np.percentile(e, 99)), float(e.max()))
+    assert got[0] <= p50 and got[1] <= p99 and got[2] <= mx, (what, "p50/p99/max", got, "bars", (p50, p99, mx))
+
+
+# Contact-path bars (one substep from oracle states, fp32 device PGS vs fp64 oracle PGS), set at
+# ~10x the spread measured on 4096 bench states at t = 20 and 120 (profiles/r03_newton_gap.json,
+# "substep_pgs_device_vs_pgs_fp64": qvel p50 2e-7, p99 3.3e-5 -- fp32 and fp64 PGS stopping one
+# sweep apart --, max 3.3e-5 on the cube, 2.4e-4 on the arm of an arm-contact env)
+QVEL_BARS = (2e-6, 3.5e-4, 2.5e-3)
 
 
 def test_reset_obs(gpu_lib, arm_model, cube_model):
@@ -166,12 +181,15 @@ def test_contacts_match_oracle(gpu_lib, arm_model, cube_model):
         pair_ids = out.astype(np.float32).view(np.int32)[..., 7]
         d = cm.desc
         checked = total = deep = deep_bad = shallow = nrm_bad = geo_bad = 0
+        skipped_grazing = skipped_count = 0
         for e in range(n):
             ref = orc.forward(full[e])
             rc = ref["contacts"]
             if len(rc) and np.min(np.abs(rc[:, 0])) < 2e-5:
+                skipped_grazing += 1
                 continue  # grazing contact: existence is decided below fp32 resolution
             if nc[e] != len(rc):
+                skipped_count += 1
                 # only a grazing contact may exist on one side: compare the pair multisets
                 gp = sorted((int(d.pair_geom1[x]), int(d.pair_geom2[x])) for x in pair_ids[e, :nc[e]])
                 op = sorted((int(a), int(b)) for a, b in rc[:, 7:9])
@@ -198,6 +216,9 @@ def test_contacts_match_oracle(gpu_lib, arm_model, cube_model):
                     deep_bad += abs(out[e, k, 0] - rc[k, 0]) > 3e-2 * abs(rc[k, 0])
             checked += 1
         assert checked > 0.9 * n and total > n // 4
+        # the envs left out of the pair-by-pair comparison: a grazing contact (|depth| < 20 um) on
+        # the oracle side, or a count mismatch whose extra contact is grazing on the GPU side
+        assert skipped_grazing + skipped_count <= 0.03 * n, (skipped_grazing, skipped_count)
         # deep (>5 mm) penetrations: MPR's depth there depends on the portal path, which
         # flips on near-tied support vertices; require agreement for the bulk only
         assert deep_bad <= max(2, 0.05 * deep), (deep_bad, deep)
@@ -208,7 +229,7 @@ def test_contacts_match_oracle(gpu_lib, arm_model, cube_model):
         # a different face in fp32 than in fp64 for a few edge contacts
         assert geo_bad <= max(2, 0.06 * shallow), ("depth/point", geo_bad, shallow)
         print(f"contacts: {total} checked, shallow {shallow} (geometry off {geo_bad}, normal off {nrm_bad}), "
-              f"deep {deep} (off {deep_bad})")
+              f"deep {deep} (off {deep_bad}); envs skipped: grazing {skipped_grazing}, count {skipped_count}")
 
 
 def test_one_substep_with_contacts(gpu_lib, cube_model):
@@ -226,8 +247,9 @@ def test_one_substep_with_contacts(gpu_lib, cube_model):
     S.substeps(1)
     orc.step(st, None, nsub=1)
     np.testing.assert_allclose(to_np(S.qpos).T, st["qpos"], atol=5e-6)
-    np.testing.assert_allclose(to_np(S.qvel).T[:, 6:], st["qvel"][:, 6:], atol=5e-3)
-    np.testing.assert_allclose(to_np(S.qvel).T[:, :6], st["qvel"][:, :6], atol=5e-3)
+    dv = np.abs(to_np(S.qvel).T - st["qvel"])
+    assert_pct(dv[:, 6:].max(1), *QVEL_BARS, what="cube qvel")
+    assert_pct(dv[:, :6].max(1), *QVEL_BARS, what="arm qvel")
     assert to_np(S.ncon).sum() == st["ncon"].sum()
 
 
@@ -262,7 +284,9 @@ def test_one_substep_bench_state_mixed_contacts(gpu_lib):
     orc.step(st, None, nsub=1)
     assert st["ncon"].sum() > 4 * 512, "no arm contacts in the sample"
     np.testing.assert_allclose(to_np(S.qpos).T, st["qpos"], atol=5e-6)
-    np.testing.assert_allclose(to_np(S.qvel).T, st["qvel"], atol=5e-3)
+    dv = np.abs(to_np(S.qvel).T - st["qvel"])
+    assert_pct(dv[:, 6:].max(1), *QVEL_BARS, what="cube qvel")
+    assert_pct(dv.max(1), *QVEL_BARS, what="qvel")
     assert to_np(S.ncon).sum() == st["ncon"].sum()
     # the arm's velocities (its rows retire from the sweeps early, soarm_pgs.h ysweeps): the
     # bulk stays at fp32 resolution, as with the full sweep schedule (measured p99 8e-8,
@@ -313,7 +337,10 @@ def test_one_substep_extra_contact_sweeps(gpu_lib):
     S.substeps(1)
     orc.step(sub, None, nsub=1)
     np.testing.assert_allclose(to_np(S.qpos).T, sub["qpos"], atol=5e-6)
-    np.testing.assert_allclose(to_np(S.qvel).T, sub["qvel"], atol=5e-3)
+    dv = np.abs(to_np(S.qvel).T - sub["qvel"]).max(1)
+    # the waves of these lanes run the extra-slot sweep variants: their envs carry arm contacts
+    # (arm-contact envs: fp32 / fp64 PGS may stop a sweep apart, measured max 2.4e-4)
+    assert_pct(dv, 2e-6, 2.5e-3, 2.5e-3, what="qvel")
     assert to_np(S.ncon).sum() == sub["ncon"].sum()
 
 
@@ -328,7 +355,7 @@ def test_one_substep_domain_randomised(gpu_lib):
     S.substeps(1)
     orc.step(st, None, nsub=1, params=prm)
     np.testing.assert_allclose(to_np(S.qpos).T, st["qpos"], atol=5e-6)
-    np.testing.assert_allclose(to_np(S.qvel).T, st["qvel"], atol=5e-3)
+    assert_pct(np.abs(to_np(S.qvel).T - st["qvel"]).max(1), *QVEL_BARS, what="qvel")
     assert to_np(S.ncon).sum() == st["ncon"].sum()
 
 
@@ -347,7 +374,7 @@ def test_odd_batch_sizes(gpu_lib, cube_model, n):
     S.substeps(1)
     orc.step(st, None, nsub=1)
     np.testing.assert_allclose(to_np(S.qpos).T, st["qpos"], atol=5e-6)
-    np.testing.assert_allclose(to_np(S.qvel).T, st["qvel"], atol=5e-3)
+    np.testing.assert_allclose(to_np(S.qvel).T, st["qvel"], atol=QVEL_BARS[2])
 
 
 def test_ik_rollout_tracks_fig8(gpu_lib):
@@ -646,3 +673,138 @@ def test_full_size_shard_invariance_and_determinism(gpu_lib):
     assert int((a["status"] != 0).sum()) == 0
     # the cube's 4 resting contacts on (nearly) every env and substep
     assert float(a["ncon"].sum()) / (n * T * 10) > 3.5
+
+
+def test_contact_env_step_late_states_full_size(gpu_lib):
+    """The graph-captured 10-substep contact sim_step (the headline's launch sequence) against one
+    oracle env-step, from late bench states (t = 100: the cube resting, arm-table and arm-cube
+    contacts in some envs) at the headline's 4096 envs.  Bars ~10x the measured fp32 / fp64 spread
+    (profiles/r03_newton_gap.json env_step pgs_device_vs_pgs_fp64: obs p50 6e-8, p99 1.3e-7, max
+    1.2e-5; cube qvel p50 5e-7, p99 4e-5, max 1.4e-4)."""
+    from lerobot_mujoco_sim2real_amd import workloads as W
+    n = 4096
+    cm, orc, st, _ = _bench_states("contact", n, 100, nthreads=16)
+    a = W.chirp_action(W.chirp_tables(np.arange(n)), 100).astype(np.float32)
+    S = make_sim(cm, n)
+    st["ncon"][:] = 0
+    load_state(S, st)
+    og = to_np(S.step(a))  # graph replay of geom + 10 x (collide, substep)
+    oc = orc.step(st, a.astype(np.float64), nthreads=16)
+    assert st["ncon"].sum() > 4 * 10 * n, "no arm contacts in the sample"
+    assert_pct(np.abs(og - oc).max(1), 1e-6, 2e-6, 2e-4, what="obs")
+    dv = np.abs(to_np(S.qvel).T - st["qvel"])
+    assert_pct(dv[:, 6:].max(1), 5e-6, 5e-4, 2e-3, what="cube qvel")
+    assert_pct(dv[:, :6].max(1), 5e-6, 5e-4, 5e-3, what="arm qvel")
+    np.testing.assert_allclose(to_np(S.qpos).T[:, 6:9], st["qpos"][:, 6:9], atol=5e-6)
+    assert int((to_np(S.status) != 0).sum()) == int((st["status"] != 0).sum())
+    assert abs(float(to_np(S.ncon).sum()) - float(st["ncon"].sum())) <= 1e-4 * float(st["ncon"].sum())
+
+
+def _contact_divergence(cm, n, T, t0, rng):
+    """Envelope of the pick scene: fp64 oracle vs the same oracle re-rounded to fp32 after every
+    env-step, from bench states at t0, chirp inputs."""
+    from lerobot_mujoco_sim2real_amd import workloads as W
+    _, _, st, _ = _bench_states("contact", n, t0)
+    tab = W.chirp_tables(np.arange(n))
+    acts = np.stack([W.chirp_action(tab, t0 + t) for t in range(T)]).astype(np.float32).astype(np.float64)
+    orc = Oracle(cm)
+    a = {k: v.copy() for k, v in st.items()}
+    b = {k: v.copy() for k, v in st.items()}
+    dev = []
+    for t in range(T):
+        oa, ob = orc.step(a, acts[t], nthreads=8), orc.step(b, acts[t], nthreads=8)
+        for k in ("qpos", "qvel", "warm"):
+            b[k][:] = b[k].astype(np.float32)
+        dev.append(np.abs(oa - ob))
+    return st, acts, np.stack(dev)
+
+
+def test_contact_trajectory_shadowing(gpu_lib, cube_model):
+    """Pick scene, 20 env-steps from t = 60 bench states: the GPU's fp32 trajectory stays within 10x
+    the envelope of fp32-sized perturbations of the fp64 oracle (as test_trajectory_shadowing for
+    the contact-free scene)."""
+    cm = cube_model
+    n, T = 512, 20
+    st, acts, envelope = _contact_divergence(cm, n, T, 60, np.random.default_rng(11))
+    S, orc = make_sim(cm, n), Oracle(cm)
+    ref = {k: v.copy() for k, v in st.items()}
+    load_state(S, st)
+    for t in range(T):
+        e = np.abs(to_np(S.step(acts[t].astype(np.float32))) - orc.step(ref, acts[t], nthreads=8))
+        env = envelope[t]
+        assert np.median(e) <= 10 * np.median(env) + 1e-5, (t, np.median(e), np.median(env))
+        assert np.quantile(e, 0.9) <= 10 * np.quantile(env, 0.9) + 2e-4, (t, np.quantile(e, 0.9))
+    # the cube stays with its shadow too (not in obs): position after T steps
+    assert_pct(np.abs(to_np(S.qpos).T[:, 6:9] - ref["qpos"][:, 6:9]).max(1), 1e-4, 2e-3, 5e-2, what="cube pos")
+
+
+def _exact_newton_substep(cm, st):
+    o = Oracle(cm, solver="newton", tolerance=0.0)
+    s = {k: v.copy() for k, v in st.items()}
+    o.step(s, None, nsub=1, nthreads=16)
+    return s
+
+
+def test_pgs_vs_reference_newton(gpu_lib):
+    """Fidelity to what the reference computes: its scene has no <option>, so mj_step runs MuJoCo's
+    default Newton solver (SOARM101/SO101/scene_with_table_v.xml:1-32, SOARM101_Env.py:131-132).
+    The device's PGS (north star) against the exact optimum of the same constraint problem (oracle
+    Newton, tolerance 0), one substep from bench states at t = 20 and 120, 1024 envs.  Bars from
+    the 4096-env measurement (profiles/r03_newton_gap.json): block envs (cube resting) cube qvel
+    p50 1.9e-5 / 3.6e-5, p99 3.6e-5, max 3.7e-5; arm-contact envs cube qvel max 7.1e-3, arm qvel
+    max 2.4e-4; arm qvel elsewhere <= 1.6e-7."""
+    for t0 in (20, 120):
+        cm, orc, st, _ = _bench_states("contact", 1024, t0, nthreads=16)
+        ref = _exact_newton_substep(cm, st)
+        S = make_sim(cm, 1024)
+        load_state(S, st)
+        S.substeps(1)
+        dv = np.abs(to_np(S.qvel).T - ref["qvel"])
+        names = cm.geom_names
+        table, cube = names.index("table"), names.index("cube")
+        arm = np.array([any({int(c[7]), int(c[8])} != {table, cube} for c in
+                            orc.forward(st["qpos"][i], st["qvel"][i], st["ctrl"][i], st["warm"][i])["contacts"])
+                        for i in range(1024)])
+        assert_pct(dv[~arm, 6:].max(1), 4e-5, 5e-5, 1e-4, what=f"t{t0} block envs cube qvel")
+        assert_pct(dv[~arm, :6].max(1), 1e-6, 1e-6, 2e-6, what=f"t{t0} block envs arm qvel")
+        if arm.any():
+            assert dv[arm, 6:].max() < 2e-2 and dv[arm, :6].max() < 1e-3, (dv[arm].max(0))
+
+
+@pytest.mark.parametrize("t0", [20, 120])
+def test_newton_solver_matches_oracle(gpu_lib, t0):
+    """solver="Newton" (MuJoCo's default, what the reference's scene runs; soarm_newton.h) on the
+    device against the oracle's Newton (oracle.c orc_solve_newton, exact optimum): one substep
+    from bench states of the pick scene, 1024 envs, and one graph-captured env-step."""
+    from lerobot_mujoco_sim2real_amd import workloads as W
+    cmp, orc, st, _ = _bench_states("contact", 1024, t0, nthreads=16)
+    cm = W.model("contact", solver="Newton")
+    ref = _exact_newton_substep(cm, st)
+    S = make_sim(cm, 1024)
+    load_state(S, st)
+    S.substeps(1)
+    dv = np.abs(to_np(S.qvel).T - ref["qvel"])
+    assert_pct(dv.max(1), 2e-6, 2e-5, 5e-4, what="qvel")
+    dw = np.abs(to_np(S.qacc_warmstart).T - ref["warm"])  # = qacc
+    assert_pct(dw.max(1), 1e-3, 1e-2, 0.25, what="qacc")
+    a = W.chirp_action(W.chirp_tables(np.arange(1024)), t0).astype(np.float32)
+    load_state(S, st)
+    og = to_np(S.step(a))
+    s2 = {k: v.copy() for k, v in st.items()}
+    oc = Oracle(cm, solver="newton", tolerance=0.0).step(s2, a.astype(np.float64), nthreads=16)
+    assert_pct(np.abs(og - oc).max(1), 1e-6, 2e-6, 2e-4, what="obs")
+
+
+def test_newton_solver_contact_free(gpu_lib):
+    """Newton on the contact-free scene (frictionloss + limits): fused k_step vs the oracle."""
+    from lerobot_mujoco_sim2real_amd import mjcf
+    cm = mjcf.compile_mjcf(mjcf.SCENE_XML, disable_contact=True, solver="Newton")
+    n = 1024
+    orc = Oracle(cm, tolerance=0.0)
+    st = random_states(cm, orc, n, lo=-1.8, hi=1.8, rng=np.random.default_rng(5))  # limits active too
+    S = make_sim(cm, n)
+    load_state(S, st)
+    S.substeps(1)
+    orc.step(st, None, nsub=1)
+    np.testing.assert_allclose(to_np(S.qpos).T, st["qpos"], atol=2e-6)
+    assert_pct(np.abs(to_np(S.qvel).T - st["qvel"]).max(1), 2e-6, 2e-5, 5e-4, what="qvel")

@@ -38,13 +38,19 @@ def mpc_net(seed=0):
 
 
 def main():
-    only = sys.argv[1:]
+    args = sys.argv[1:]
+    solver = "pgs"
+    if "--solver" in args:
+        i = args.index("--solver")
+        solver = args[i + 1]
+        del args[i:i + 2]
+    only = args
     path = os.path.join(ROOT, "profiles", "algorithmic_cost.json")
     out = json.load(open(path)) if only else {}
     for name, c in W.CONFIGS.items():
         if only and name not in only:
             continue
-        cm = W.model(name)
+        cm = W.model(name, solver=solver)
         orc = Oracle(cm)
         ids = np.arange(N)
         st = orc.new_state(N)
@@ -89,7 +95,8 @@ def main():
             tot += orc.last_flops
             col += orc.last_collision_flops
         fs = 10
-        out[name] = dict(
+        key = name if solver == "pgs" else f"{name}_{solver}"
+        out[key] = dict(
             flops_per_env_step=tot / (N * T),
             collision_flops_per_env_step=col / (N * T),
             dynamics_flops_per_env_step=(tot - col) / (N * T),
@@ -99,14 +106,15 @@ def main():
             hbm_bytes_per_env_step=state_bytes(cm, c["dr"]),
             sample=f"{N} envs x {T} env-steps, oracle float64, seed 0",
         )
+        out[key]["solver"] = solver
         if c["action"] == "koopman_mpc":
             # per env and frame: encoder 2 sum(in*out) + control 2 u (nz + u), counted from the widths
             ws = [l[0].shape for l in layers]
             enc = 2.0 * sum(o * i for o, i in ws)
-            out[name]["mpc_flops_per_env_step"] = enc + 2.0 * 5 * (32 + 5)
-            out[name]["mpc_note"] = ("encoder + [Gz|Gu] per env-step (f64 MFMA, k_mpc_step); the physics "
+            out[key]["mpc_flops_per_env_step"] = enc + 2.0 * 5 * (32 + 5)
+            out[key]["mpc_note"] = ("encoder + [Gz|Gu] per env-step (f64 MFMA, k_mpc_step); the physics "
                                      "share above is the arm scene with gravity compensation")
-        print(name, json.dumps(out[name]))
+        print(key, json.dumps(out[key]))
     json.dump(out, open(path, "w"), indent=1)
     print("wrote", path)
 
