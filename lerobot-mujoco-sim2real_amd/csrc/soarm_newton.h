@@ -36,10 +36,13 @@ struct NewtonRows {
   const float *fR, *fa;  // frictionloss rows: R, aref (= -B qvel)
   int nlim, nl, ncon;
 
-  // one pass over every row at a: cost, J' f, and (want_h) the rows' Hessian terms added to H
+  // one pass over every row at a: cost, J' f, (want_h) the rows' Hessian terms added to H, and
+  // sig, a signature of the rows' zones (quadratic / linear / inactive): Newton has converged
+  // once a full step leaves it unchanged (the cost is one quadratic there)
   template <bool WANT_H>
-  DEVI float pass(const float a[NV], float jtf[NV], float H[NH]) const {
+  DEVI float pass(const float a[NV], float jtf[NV], float H[NH], uint32_t& sig) const {
     float cost = 0.f;
+    sig = 0u;
 #pragma unroll
     for (int i = 0; i < NV; i++) jtf[i] = 0.f;
     // frictionloss rows (J = e_i)
@@ -58,6 +61,7 @@ struct NewtonRows {
       }
       cost += c;
       jtf[i] += f;
+      sig = sig * 3u + (q ? 1u : (x < 0.f ? 2u : 0u));
       if constexpr (WANT_H)
         if (q) H[i * (i + 1) / 2 + i] += 1.f / R;
     }
@@ -69,6 +73,7 @@ struct NewtonRows {
 #pragma unroll
       for (int i = 0; i < NA; i++) ad = i == d ? a[i] : ad;
       const float x = sg * ad - L.lm(l, L_AREF);
+      sig = sig * 2u + (x < 0.f ? 1u : 0u);
       if (x < 0.f) {
         cost += 0.5f * x * x / R;
         const float f = -x / R;
@@ -81,24 +86,29 @@ struct NewtonRows {
     }
     if constexpr (CON) {
       // contacts in LDS records: the frame Jacobian once, the 4 pyramid edges in its 3-D space
-      for (int c = 0; c < nl; c++) {
+      // one contact over the dof range [LO, HI) it can touch (J_c is zero elsewhere): the free
+      // body's 6 dofs for the cube's contacts, the arm's for arm-only ones, all of them for an
+      // arm-cube contact -- a wave-uniform choice, as the PGS sweeps make it
+      auto contact = [&](int c, auto lo_c, auto hi_c) {
+        constexpr int LO = decltype(lo_c)::value, HI = decltype(hi_c)::value;
         float jc[3][NV];
 #pragma unroll
         for (int q = 0; q < 3; q++)
 #pragma unroll
-          for (int i = 0; i < NV; i++) jc[q][i] = L.at(c, 12 * q + i);
+          for (int i = LO; i < HI; i++) jc[q][i] = L.at(c, 12 * q + i);
         const float mu = L.at(c, F_MU), R = L.at(c, F_R), D = 1.f / R;
         float y[3] = {0.f, 0.f, 0.f};
 #pragma unroll
         for (int q = 0; q < 3; q++)
 #pragma unroll
-          for (int i = 0; i < NV; i++) y[q] = fmaf(jc[q][i], a[i], y[q]);
+          for (int i = LO; i < HI; i++) y[q] = fmaf(jc[q][i], a[i], y[q]);
         float F[3] = {0.f, 0.f, 0.f}, K[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // K: nn n1 n2 11 12 22
 #pragma unroll
         for (int ed = 0; ed < 4; ed++) {
           const float s = (ed & 1) ? -mu : mu;
           const int t = 1 + (ed >> 1);
           const float x = y[0] + s * y[t] - L.at(c, F_AREF + ed);
+          sig = sig * 2u + (x < 0.f ? 1u : 0u);
           if (x < 0.f) {
             cost += 0.5f * x * x * D;
             const float f = -x * D;
@@ -107,28 +117,37 @@ struct NewtonRows {
           }
         }
 #pragma unroll
-        for (int i = 0; i < NV; i++) jtf[i] += jc[0][i] * F[0] + jc[1][i] * F[1] + jc[2][i] * F[2];
-        if constexpr (WANT_H) {
-          // H += J_c' K J_c
+        for (int i = LO; i < HI; i++) jtf[i] += jc[0][i] * F[0] + jc[1][i] * F[1] + jc[2][i] * F[2];
+        if constexpr (WANT_H) {  // H += J_c' K J_c
           float kj[3][NV];
 #pragma unroll
-          for (int i = 0; i < NV; i++) {
+          for (int i = LO; i < HI; i++) {
             kj[0][i] = K[0] * jc[0][i] + K[1] * jc[1][i] + K[2] * jc[2][i];
             kj[1][i] = K[1] * jc[0][i] + K[3] * jc[1][i] + K[4] * jc[2][i];
             kj[2][i] = K[2] * jc[0][i] + K[4] * jc[1][i] + K[5] * jc[2][i];
           }
 #pragma unroll
-          for (int i = 0; i < NV; i++)
+          for (int i = LO; i < HI; i++)
 #pragma unroll
-            for (int j = 0; j <= i; j++)
+            for (int j = LO; j <= i; j++)
               H[i * (i + 1) / 2 + j] += jc[0][i] * kj[0][j] + jc[1][i] * kj[1][j] + jc[2][i] * kj[2][j];
         }
+      };
+      for (int c = 0; c < nl; c++) {
+        const int fl = (int)L.at(c, F_FLAGS);
+        if (NF > 0 && __all(fl == TOUCH_FREE))
+          contact(c, std::integral_constant<int, NA>{}, std::integral_constant<int, NV>{});
+        else if (__all(!(fl & TOUCH_FREE)))
+          contact(c, std::integral_constant<int, 0>{}, std::integral_constant<int, NA>{});
+        else
+          contact(c, std::integral_constant<int, 0>{}, std::integral_constant<int, NV>{});
       }
       // contacts past the LDS records: per-edge rows in the global slab (rare)
       for (int r = 4 * nl; r < 4 * ncon; r++) {
         float J[NV], x = -cr.S(r, 0);
 #pragma unroll
         for (int i = 0; i < NV; i++) J[i] = cr.J(r, i), x = fmaf(J[i], a[i], x);
+        sig = sig * 2u + (x < 0.f ? 1u : 0u);
         if (x < 0.f) {
           const float D = 1.f / cr.S(r, 1), f = -x * D;
           cost += 0.5f * x * x * D;
@@ -249,17 +268,23 @@ DEVI int newton_solve(Sim<NA, NF>& S, const NewtonRows<NA, NF, CON>& R) {
     return c;
   };
   float a[NV], jtf[NV], H[NH], Ma[NV];
+  uint32_t sig = 0u;
   // warm start: qacc_warmstart unless qacc_smooth costs less
   {
     float js[NV];
-    const float cs = R.template pass<false>(a0, js, H);
-    const float cw = gauss(S.warm, Ma) + R.template pass<false>(S.warm, jtf, H);
+    const float cs = R.template pass<false>(a0, js, H, sig);
+    const float cw = gauss(S.warm, Ma) + R.template pass<false>(S.warm, jtf, H, sig);
 #pragma unroll
     for (int i = 0; i < NV; i++) a[i] = cw < cs ? S.warm[i] : a0[i];
   }
+  // an arm-cube contact (or a generic overflow row) couples the arm and free-body blocks of H;
+  // otherwise H is block diagonal and factors as two 6x6 blocks
+  bool coupled = NF > 0 && CON && __any(R.ncon > R.nl);
+  if constexpr (NF > 0 && CON)
+    for (int c = 0; c < R.nl; c++) coupled |= __any((int)R.L.at(c, F_FLAGS) == (TOUCH_ARM | TOUCH_FREE));
 #pragma unroll
   for (int i = 0; i < NH; i++) H[i] = 0.f;
-  float cost = gauss(a, Ma) + R.template pass<true>(a, jtf, H);
+  float cost = gauss(a, Ma) + R.template pass<true>(a, jtf, H, sig);
   int it = 0;
   for (; it < m.iterations; it++) {
     float g[NV], gn = 0.f;
@@ -278,19 +303,34 @@ DEVI int newton_solve(Sim<NA, NF>& S, const NewtonRows<NA, NF, CON>& R) {
         const int d = NA + 6 * f + i;
         H[d * (d + 1) / 2 + d] += S.MF[f][i * (i + 1) / 2 + i];
       }
-    float Hd[NV], p[NV], mg[NV];
-    ldl_factor<NV>(H, Hd);
+    float p[NV], mg[NV];
 #pragma unroll
     for (int i = 0; i < NV; i++) mg[i] = -g[i];
-    ldl_solve<NV>(H, Hd, p, mg);
+    if (NF == 0 || coupled) {
+      float Hd[NV];
+      ldl_factor<NV>(H, Hd);
+      ldl_solve<NV>(H, Hd, p, mg);
+    } else {
+      // block diagonal: the arm block is H's first 21 packed entries; the free block is gathered
+      float Ha[NA * (NA + 1) / 2], Hf[21], Had[NA], Hfd[6];
+#pragma unroll
+      for (int k = 0; k < NA * (NA + 1) / 2; k++) Ha[k] = H[k];
+#pragma unroll
+      for (int i = 0; i < 6; i++)
+#pragma unroll
+        for (int j = 0; j <= i; j++) Hf[i * (i + 1) / 2 + j] = H[(NA + i) * (NA + i + 1) / 2 + NA + j];
+      ldl_factor<NA>(Ha, Had);
+      ldl_solve<NA>(Ha, Had, p, mg);
+      ldl_factor<6>(Hf, Hfd);
+      ldl_solve<6>(Hf, Hfd, p + NA, mg + NA);
+    }
     // exact line search: phi'(al) = (a - a0)' M p + al p' M p + rows; 1-D Newton, bracketed
-    float Mp[NV], g0 = 0.f, pMp = 0.f, pn = 0.f;
+    float Mp[NV], g0 = 0.f, pMp = 0.f;
     mul_m(S, p, Mp);
 #pragma unroll
     for (int i = 0; i < NV; i++) {
       g0 = fmaf(a[i] - a0[i], Mp[i], g0);
       pMp = fmaf(p[i], Mp[i], pMp);
-      pn = fmaf(p[i], p[i], pn);
     }
     R.ls_setup(a, p);
     auto deriv = [&](float al, float& d2) {
@@ -313,7 +353,7 @@ DEVI int newton_solve(Sim<NA, NF>& S, const NewtonRows<NA, NF, CON>& R) {
       if (d1 == 0.f) break;
       float an = al - d1 / d2;  // exact within the current piece
       if (!(an > lo && an < hi)) an = hi < 3.0e38f ? 0.5f * (lo + hi) : 2.f * al;
-      if (fabsf(an - al) <= 1e-7f * al) {
+      if (fabsf(an - al) <= 1e-6f * al) {
         al = an;
         break;
       }
@@ -325,13 +365,17 @@ DEVI int newton_solve(Sim<NA, NF>& S, const NewtonRows<NA, NF, CON>& R) {
     float jn[NV], Man[NV];
 #pragma unroll
     for (int i = 0; i < NH; i++) H[i] = 0.f;
-    const float cn = gauss(an_, Man) + R.template pass<true>(an_, jn, H);
+    const uint32_t sig0 = sig;
+    const float cn = gauss(an_, Man) + R.template pass<true>(an_, jn, H, sig);
     if (!(cn <= cost)) break;  // rounding-level: no further progress (keep a)
 #pragma unroll
     for (int i = 0; i < NV; i++) a[i] = an_[i], jtf[i] = jn[i], Ma[i] = Man[i];
-    const float improvement = scale * (cost - cn);
+    const float improvement = cost - cn;
     cost = cn;
-    if (improvement < tol) {
+    // MuJoCo's test; its fp32 floor (a relative improvement at rounding level); and exactness:
+    // a full Newton step that leaves every row in its zone minimised the one quadratic there
+    if (scale * improvement < tol || improvement <= 1e-6f * fabsf(cn) ||
+        (sig == sig0 && fabsf(al - 1.f) < 1e-3f)) {
       it++;
       break;
     }
