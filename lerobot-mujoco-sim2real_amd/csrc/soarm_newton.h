@@ -10,18 +10,23 @@
 //     s_r(x) = x^2 / 2R                    pyramid edges, limits: x < 0 (else 0)
 //            = Huber(x; R, frictionloss)   dof frictionloss rows
 //   gradient g = M (a - a0) - J' f(a);  Hessian H = M + J_q' D J_q over the rows in their
-//   quadratic zone (D = 1/R);  p = -H^-1 g (dense LDL' of the nv x nv H);  exact line search
-//   along p (1-D Newton on the piecewise-linear derivative, bracketed);  stop when
-//   scale * improvement < tolerance or scale * |g| < tolerance (scale = 1 / (meaninertia nv)).
+//   quadratic zone (D = 1/R);  p = -H^-1 g (dense LDL');  exact line search along p (1-D Newton
+//   on the piecewise-linear derivative, bracketed);  stop when scale * improvement < tolerance
+//   or scale * |g| < tolerance (scale = 1 / (meaninertia nv)).
 //   Warm start: qacc_warmstart unless qacc_smooth costs less (mj_fwdConstraint).
 //
-// The problem is strictly convex (R > 0): its optimum is unique and this converges to it in a
-// few iterations from the warm start, so the result equals the reference's to fp32 precision
-// (the oracle restatement: oracle/oracle.c orc_solve_newton).  Per row the arithmetic is short
-// and independent across rows (no Gauss-Seidel chain): a contact contributes its frame
-// Jacobian J_c = [J_n; J_t1; J_t2] once, edges e = J_n + s_e J_t(e) are formed in that 3-D
-// space, and its Hessian term is J_c' K J_c with the 3x3 K = sum over quadratic edges of
-// D u_e u_e' (u_e = (1, s_e on t(e))).
+// The problem is strictly convex (R > 0): its optimum is unique and Newton reaches it in a few
+// iterations from the warm start, so the result equals the reference's to fp32 precision (the
+// oracle restatement: oracle/oracle.c orc_solve_newton).
+//
+// Decomposition.  M is block diagonal (arm chain | free body) and a row couples the two blocks
+// only if it is a contact between an arm link and the cube.  Without such a contact in the wave
+// the cost separates, c(a) = c_arm(a_arm) + c_free(a_free), and the two 6-dof problems are solved
+// one after the other (same optimum; half the Hessian, so half the registers); with one, the
+// whole 12-dof problem is solved.  A contact contributes its frame Jacobian J_c = [J_n; J_t1;
+// J_t2] once: its 4 pyramid edges e = J_n + s_e J_t(e) live in that 3-D space, and its Hessian
+// term is J_c' K J_c with the 3x3 K = sum over quadratic edges of D u_e u_e' (u_e = (1, s_e on
+// t(e))).
 #pragma once
 
 namespace soarm {
@@ -29,79 +34,87 @@ namespace soarm {
 template <int NA, int NF, bool CON>
 struct NewtonRows {
   static constexpr int NV = NA + 6 * NF;
-  static constexpr int NH = NV * (NV + 1) / 2;
   const DModel& m;
   const RowLds& L;
   const ContactRows<NA, NF>& cr;
   const float *fR, *fa;  // frictionloss rows: R, aref (= -B qvel)
   int nlim, nl, ncon;
 
-  // one pass over every row at a: cost, J' f, (want_h) the rows' Hessian terms added to H, and
-  // sig, a signature of the rows' zones (quadratic / linear / inactive): Newton has converged
-  // once a full step leaves it unchanged (the cost is one quadratic there)
-  template <bool WANT_H>
-  DEVI float pass(const float a[NV], float jtf[NV], float H[NH], uint32_t& sig) const {
+  // does the subsystem over dofs [LO, HI) own a contact of class fl?  (full range: all of them)
+  template <int LO, int HI>
+  static DEVI bool owns(int fl) {
+    if constexpr (LO == 0 && HI == NV) return true;
+    else if constexpr (HI == NA) return !(fl & TOUCH_FREE);
+    else return fl == TOUCH_FREE;
+  }
+  static constexpr int hidx(int i, int j) { return i * (i + 1) / 2 + j; }  // packed lower, i >= j
+
+  // one pass over the subsystem's rows at a: its cost, J' f (dofs LO..HI-1), (WANT_H) the rows'
+  // Hessian terms added to H (packed lower over the subsystem's dofs), and sig, a signature of
+  // the rows' zones (quadratic / linear / inactive): Newton has converged once a full step
+  // leaves it unchanged (the cost is one quadratic there)
+  template <int LO, int HI, bool WANT_H>
+  DEVI float pass(const float a[NV], float jtf[NV], float H[], uint32_t& sig) const {
     float cost = 0.f;
     sig = 0u;
 #pragma unroll
-    for (int i = 0; i < NV; i++) jtf[i] = 0.f;
-    // frictionloss rows (J = e_i)
+    for (int i = LO; i < HI; i++) jtf[i] = 0.f;
+    if constexpr (LO == 0) {
+      // frictionloss rows (J = e_i)
 #pragma unroll
-    for (int i = 0; i < NA; i++) {
-      const float fl = m.dof_frictionloss[i], R = fR[i];
-      const float x = a[i] - fa[i];
-      float f, c;
-      bool q = false;
-      if (x <= -R * fl) {
-        f = fl, c = -fl * x - 0.5f * R * fl * fl;
-      } else if (x >= R * fl) {
-        f = -fl, c = fl * x - 0.5f * R * fl * fl;
-      } else {
-        f = -x / R, c = 0.5f * x * x / R, q = fl > 0.f;
+      for (int i = 0; i < NA; i++) {
+        const float fl = m.dof_frictionloss[i], R = fR[i];
+        const float x = a[i] - fa[i];
+        float f, c;
+        bool q = false;
+        if (x <= -R * fl) {
+          f = fl, c = -fl * x - 0.5f * R * fl * fl;
+        } else if (x >= R * fl) {
+          f = -fl, c = fl * x - 0.5f * R * fl * fl;
+        } else {
+          f = -x / R, c = 0.5f * x * x / R, q = fl > 0.f;
+        }
+        cost += c;
+        jtf[i] += f;
+        sig = sig * 3u + (q ? 1u : (x < 0.f ? 2u : 0u));
+        if constexpr (WANT_H)
+          if (q) H[hidx(i, i)] += 1.f / R;
       }
-      cost += c;
-      jtf[i] += f;
-      sig = sig * 3u + (q ? 1u : (x < 0.f ? 2u : 0u));
-      if constexpr (WANT_H)
-        if (q) H[i * (i + 1) / 2 + i] += 1.f / R;
-    }
-    // joint limits (J = sign e_dof)
-    for (int l = 0; l < nlim; l++) {
-      const int d = (int)L.lm(l, L_DOF);
-      const float sg = L.lm(l, L_SGN), R = L.lm(l, L_R);
-      float ad = 0.f;
+      // joint limits (J = sign e_dof)
+      for (int l = 0; l < nlim; l++) {
+        const int d = (int)L.lm(l, L_DOF);
+        const float sg = L.lm(l, L_SGN), R = L.lm(l, L_R);
+        float ad = 0.f;
 #pragma unroll
-      for (int i = 0; i < NA; i++) ad = i == d ? a[i] : ad;
-      const float x = sg * ad - L.lm(l, L_AREF);
-      sig = sig * 2u + (x < 0.f ? 1u : 0u);
-      if (x < 0.f) {
-        cost += 0.5f * x * x / R;
-        const float f = -x / R;
+        for (int i = 0; i < NA; i++) ad = i == d ? a[i] : ad;
+        const float x = sg * ad - L.lm(l, L_AREF);
+        sig = sig * 2u + (x < 0.f ? 1u : 0u);
+        if (x < 0.f) {
+          cost += 0.5f * x * x / R;
+          const float f = -x / R;
 #pragma unroll
-        for (int i = 0; i < NA; i++) {
-          jtf[i] += i == d ? sg * f : 0.f;
-          if constexpr (WANT_H) H[i * (i + 1) / 2 + i] += i == d ? 1.f / R : 0.f;
+          for (int i = 0; i < NA; i++) {
+            jtf[i] += i == d ? sg * f : 0.f;
+            if constexpr (WANT_H) H[hidx(i, i)] += i == d ? 1.f / R : 0.f;
+          }
         }
       }
     }
     if constexpr (CON) {
-      // contacts in LDS records: the frame Jacobian once, the 4 pyramid edges in its 3-D space
-      // one contact over the dof range [LO, HI) it can touch (J_c is zero elsewhere): the free
-      // body's 6 dofs for the cube's contacts, the arm's for arm-only ones, all of them for an
-      // arm-cube contact -- a wave-uniform choice, as the PGS sweeps make it
-      auto contact = [&](int c, auto lo_c, auto hi_c) {
-        constexpr int LO = decltype(lo_c)::value, HI = decltype(hi_c)::value;
+      // one contact over the dof range [CL, CH) its Jacobian can be nonzero on
+      auto contact = [&](int c, auto cl, auto ch) {
+        constexpr int CL = decltype(cl)::value, CH = decltype(ch)::value;
         float jc[3][NV];
 #pragma unroll
         for (int q = 0; q < 3; q++)
 #pragma unroll
-          for (int i = LO; i < HI; i++) jc[q][i] = L.at(c, 12 * q + i);
-        const float mu = L.at(c, F_MU), R = L.at(c, F_R), D = 1.f / R;
+          for (int i = CL; i < CH; i++) jc[q][i] = L.at(c, 12 * q + i);
+        const float mu = L.at(c, F_MU), D = 1.f / L.at(c, F_R);
         float y[3] = {0.f, 0.f, 0.f};
 #pragma unroll
         for (int q = 0; q < 3; q++)
 #pragma unroll
-          for (int i = LO; i < HI; i++) y[q] = fmaf(jc[q][i], a[i], y[q]);
+          for (int i = CL; i < CH; i++) y[q] = fmaf(jc[q][i], a[i], y[q]);
         float F[3] = {0.f, 0.f, 0.f}, K[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // K: nn n1 n2 11 12 22
 #pragma unroll
         for (int ed = 0; ed < 4; ed++) {
@@ -117,63 +130,72 @@ struct NewtonRows {
           }
         }
 #pragma unroll
-        for (int i = LO; i < HI; i++) jtf[i] += jc[0][i] * F[0] + jc[1][i] * F[1] + jc[2][i] * F[2];
+        for (int i = CL; i < CH; i++) jtf[i] += jc[0][i] * F[0] + jc[1][i] * F[1] + jc[2][i] * F[2];
         if constexpr (WANT_H) {  // H += J_c' K J_c
           float kj[3][NV];
 #pragma unroll
-          for (int i = LO; i < HI; i++) {
+          for (int i = CL; i < CH; i++) {
             kj[0][i] = K[0] * jc[0][i] + K[1] * jc[1][i] + K[2] * jc[2][i];
             kj[1][i] = K[1] * jc[0][i] + K[3] * jc[1][i] + K[4] * jc[2][i];
             kj[2][i] = K[2] * jc[0][i] + K[4] * jc[1][i] + K[5] * jc[2][i];
           }
 #pragma unroll
-          for (int i = LO; i < HI; i++)
+          for (int i = CL; i < CH; i++)
 #pragma unroll
-            for (int j = LO; j <= i; j++)
-              H[i * (i + 1) / 2 + j] += jc[0][i] * kj[0][j] + jc[1][i] * kj[1][j] + jc[2][i] * kj[2][j];
+            for (int j = CL; j <= i; j++)
+              H[hidx(i - LO, j - LO)] += jc[0][i] * kj[0][j] + jc[1][i] * kj[1][j] + jc[2][i] * kj[2][j];
         }
       };
       for (int c = 0; c < nl; c++) {
         const int fl = (int)L.at(c, F_FLAGS);
-        if (NF > 0 && __all(fl == TOUCH_FREE))
-          contact(c, std::integral_constant<int, NA>{}, std::integral_constant<int, NV>{});
-        else if (__all(!(fl & TOUCH_FREE)))
-          contact(c, std::integral_constant<int, 0>{}, std::integral_constant<int, NA>{});
-        else
-          contact(c, std::integral_constant<int, 0>{}, std::integral_constant<int, NV>{});
+        if constexpr (LO == 0 && HI == NV) {
+          // whole problem: still skip the halves a contact cannot touch (wave-uniform choice)
+          if (NF > 0 && __all(fl == TOUCH_FREE))
+            contact(c, std::integral_constant<int, NA>{}, std::integral_constant<int, NV>{});
+          else if (__all(!(fl & TOUCH_FREE)))
+            contact(c, std::integral_constant<int, 0>{}, std::integral_constant<int, NA>{});
+          else
+            contact(c, std::integral_constant<int, 0>{}, std::integral_constant<int, NV>{});
+        } else if (owns<LO, HI>(fl)) {
+          contact(c, std::integral_constant<int, LO>{}, std::integral_constant<int, HI>{});
+        }
       }
-      // contacts past the LDS records: per-edge rows in the global slab (rare)
-      for (int r = 4 * nl; r < 4 * ncon; r++) {
-        float J[NV], x = -cr.S(r, 0);
+      if constexpr (LO == 0 && HI == NV) {
+        // contacts past the LDS records: per-edge rows in the global slab (rare; whole problem)
+        for (int r = 4 * nl; r < 4 * ncon; r++) {
+          float J[NV], x = -cr.S(r, 0);
 #pragma unroll
-        for (int i = 0; i < NV; i++) J[i] = cr.J(r, i), x = fmaf(J[i], a[i], x);
-        sig = sig * 2u + (x < 0.f ? 1u : 0u);
-        if (x < 0.f) {
-          const float D = 1.f / cr.S(r, 1), f = -x * D;
-          cost += 0.5f * x * x * D;
+          for (int i = 0; i < NV; i++) J[i] = cr.J(r, i), x = fmaf(J[i], a[i], x);
+          sig = sig * 2u + (x < 0.f ? 1u : 0u);
+          if (x < 0.f) {
+            const float D = 1.f / cr.S(r, 1), f = -x * D;
+            cost += 0.5f * x * x * D;
 #pragma unroll
-          for (int i = 0; i < NV; i++) jtf[i] += J[i] * f;
-          if constexpr (WANT_H)
+            for (int i = 0; i < NV; i++) jtf[i] += J[i] * f;
+            if constexpr (WANT_H)
 #pragma unroll
-            for (int i = 0; i < NV; i++)
+              for (int i = 0; i < NV; i++)
 #pragma unroll
-              for (int j = 0; j <= i; j++) H[i * (i + 1) / 2 + j] += D * J[i] * J[j];
+                for (int j = 0; j <= i; j++) H[hidx(i, j)] += D * J[i] * J[j];
+          }
         }
       }
     }
     return cost;
   }
 
-  // line-search data along p: per row the residual at a and its rate along p, in LDS scratch
-  // (ext area; contacts: 4 edges each) -- evaluated at every line-search point
+  // line-search data along p: per contact edge the residual at a and its rate along p, in LDS
+  // scratch (ext area, 8 floats per contact), read at every line-search point
+  template <int LO, int HI>
   DEVI void ls_setup(const float a[NV], const float p[NV]) const {
     if constexpr (CON) {
       for (int c = 0; c < nl; c++) {
+        if (!owns<LO, HI>((int)L.at(c, F_FLAGS))) continue;
         float ya[3] = {0.f, 0.f, 0.f}, yp[3] = {0.f, 0.f, 0.f};
 #pragma unroll
         for (int q = 0; q < 3; q++)
 #pragma unroll
-          for (int i = 0; i < NV; i++) {
+          for (int i = LO; i < HI; i++) {
             const float j = L.at(c, 12 * q + i);
             ya[q] = fmaf(j, a[i], ya[q]), yp[q] = fmaf(j, p[i], yp[q]);
           }
@@ -186,36 +208,41 @@ struct NewtonRows {
           L.ex(XS_LIST + 8 * c + 4 + ed) = yp[0] + s * yp[t];
         }
       }
-      for (int r = 4 * nl; r < 4 * ncon; r++) {
-        float x = -cr.S(r, 0), v = 0.f;
+      if constexpr (LO == 0 && HI == NV)
+        for (int r = 4 * nl; r < 4 * ncon; r++) {
+          float x = -cr.S(r, 0), v = 0.f;
 #pragma unroll
-        for (int i = 0; i < NV; i++) x = fmaf(cr.J(r, i), a[i], x), v = fmaf(cr.J(r, i), p[i], v);
-        cr.W(r, 0) = x, cr.W(r, 1) = v;  // (the PGS M^-1 J' slot: unused by Newton)
-      }
+          for (int i = 0; i < NV; i++) x = fmaf(cr.J(r, i), a[i], x), v = fmaf(cr.J(r, i), p[i], v);
+          cr.W(r, 0) = x, cr.W(r, 1) = v;  // (the PGS M^-1 J' slot: unused by Newton)
+        }
     }
   }
 
-  // d/dalpha and d2/dalpha2 of the rows' cost at a + alpha p (Gauss part added by the caller)
+  // d/dalpha and d2/dalpha2 of the subsystem rows' cost at a + alpha p (Gauss part: caller)
+  template <int LO, int HI>
   DEVI void ls_eval(const float a[NV], const float p[NV], float al, float& d1, float& d2) const {
+    if constexpr (LO == 0) {
 #pragma unroll
-    for (int i = 0; i < NA; i++) {
-      const float fl = m.dof_frictionloss[i], R = fR[i];
-      const float x = a[i] - fa[i] + al * p[i];
-      const float f = x <= -R * fl ? fl : (x >= R * fl ? -fl : -x / R);
-      d1 -= f * p[i];
-      d2 += (x > -R * fl && x < R * fl && fl > 0.f) ? p[i] * p[i] / R : 0.f;
-    }
-    for (int l = 0; l < nlim; l++) {
-      const int d = (int)L.lm(l, L_DOF);
-      const float sg = L.lm(l, L_SGN), R = L.lm(l, L_R);
-      float ad = 0.f, pd = 0.f;
+      for (int i = 0; i < NA; i++) {
+        const float fl = m.dof_frictionloss[i], R = fR[i];
+        const float x = a[i] - fa[i] + al * p[i];
+        const float f = x <= -R * fl ? fl : (x >= R * fl ? -fl : -x / R);
+        d1 -= f * p[i];
+        d2 += (x > -R * fl && x < R * fl && fl > 0.f) ? p[i] * p[i] / R : 0.f;
+      }
+      for (int l = 0; l < nlim; l++) {
+        const int d = (int)L.lm(l, L_DOF);
+        const float sg = L.lm(l, L_SGN), R = L.lm(l, L_R);
+        float ad = 0.f, pd = 0.f;
 #pragma unroll
-      for (int i = 0; i < NA; i++) ad = i == d ? a[i] : ad, pd = i == d ? p[i] : pd;
-      const float x = sg * (ad + al * pd) - L.lm(l, L_AREF), v = sg * pd;
-      if (x < 0.f) d1 += x * v / R, d2 += v * v / R;
+        for (int i = 0; i < NA; i++) ad = i == d ? a[i] : ad, pd = i == d ? p[i] : pd;
+        const float x = sg * (ad + al * pd) - L.lm(l, L_AREF), v = sg * pd;
+        if (x < 0.f) d1 += x * v / R, d2 += v * v / R;
+      }
     }
     if constexpr (CON) {
       for (int c = 0; c < nl; c++) {
+        if (!owns<LO, HI>((int)L.at(c, F_FLAGS))) continue;
         const float D = 1.f / L.at(c, F_R);
 #pragma unroll
         for (int ed = 0; ed < 4; ed++) {
@@ -224,124 +251,110 @@ struct NewtonRows {
           if (x < 0.f) d1 += x * v * D, d2 += v * v * D;
         }
       }
-      for (int r = 4 * nl; r < 4 * ncon; r++) {
-        const float D = 1.f / cr.S(r, 1), v = cr.W(r, 1);
-        const float x = fmaf(al, v, cr.W(r, 0));
-        if (x < 0.f) d1 += x * v * D, d2 += v * v * D;
-      }
+      if constexpr (LO == 0 && HI == NV)
+        for (int r = 4 * nl; r < 4 * ncon; r++) {
+          const float D = 1.f / cr.S(r, 1), v = cr.W(r, 1);
+          const float x = fmaf(al, v, cr.W(r, 0));
+          if (x < 0.f) d1 += x * v * D, d2 += v * v * D;
+        }
     }
   }
 };
 
-// M x for the block-diagonal M (arm block packed lower, free bodies' diagonal blocks)
-template <int NA, int NF>
+// y = M x over dofs [LO, HI) of the block-diagonal M (arm block packed lower, the free body's
+// diagonal block); [LO, HI) is a union of whole blocks
+template <int LO, int HI, int NA, int NF>
 DEVI void mul_m(const Sim<NA, NF>& S, const float x[], float y[]) {
+  if constexpr (LO < NA) {
 #pragma unroll
-  for (int i = 0; i < NA; i++) {
-    float s = 0.f;
+    for (int i = 0; i < NA; i++) {
+      float s = 0.f;
 #pragma unroll
-    for (int k = 0; k < NA; k++) s = fmaf(S.MA[i >= k ? i * (i + 1) / 2 + k : k * (k + 1) / 2 + i], x[k], s);
-    y[i] = s;
+      for (int k = 0; k < NA; k++) s = fmaf(S.MA[i >= k ? i * (i + 1) / 2 + k : k * (k + 1) / 2 + i], x[k], s);
+      y[i] = s;
+    }
   }
+  if constexpr (HI > NA) {
 #pragma unroll
-  for (int f = 0; f < NF; f++)
-#pragma unroll
-    for (int i = 0; i < 6; i++) y[NA + 6 * f + i] = S.MF[f][i * (i + 1) / 2 + i] * x[NA + 6 * f + i];
+    for (int i = 0; i < 6 * NF; i++) y[NA + i] = S.MF[i / 6][(i % 6) * (i % 6 + 1) / 2 + i % 6] * x[NA + i];
+  }
 }
 
-// Primal Newton solve of the rows built by solve_constraints; sets S.qacc and S.fcon = J' f.
-// Returns the iteration count.
-template <int NA, int NF, bool CON>
-DEVI int newton_solve(Sim<NA, NF>& S, const NewtonRows<NA, NF, CON>& R) {
-  constexpr int NV = NA + 6 * NF, NH = NV * (NV + 1) / 2;
+// Newton on the subsystem over dofs [LO, HI): a[] (all dofs; only this range moves) in/out,
+// jtf[LO..HI) = J' f at the result.  Returns the iteration count.
+template <int LO, int HI, int NA, int NF, bool CON>
+DEVI int newton_range(const Sim<NA, NF>& S, const NewtonRows<NA, NF, CON>& R, float a[], float jtf[]) {
+  constexpr int NV = NA + 6 * NF, NR = HI - LO, NH = NR * (NR + 1) / 2;
   const DModel& m = *S.mp;
   const float scale = m.pgs_scale, tol = m.tolerance;
   const float* a0 = S.qacc_s;
-  auto gauss = [&](const float a[NV], float Ma[NV]) {  // 1/2 (a - a0)' M (a - a0); Ma = M (a - a0)
-    float da[NV];
+  auto gauss = [&](const float x[], float Mx[]) {  // 1/2 (x - a0)' M (x - a0) on the range; Mx = M (x - a0)
+    float dx[NV];
 #pragma unroll
-    for (int i = 0; i < NV; i++) da[i] = a[i] - a0[i];
-    mul_m(S, da, Ma);
+    for (int i = LO; i < HI; i++) dx[i] = x[i] - a0[i];
+    mul_m<LO, HI>(S, dx, Mx);
     float c = 0.f;
 #pragma unroll
-    for (int i = 0; i < NV; i++) c = fmaf(0.5f * da[i], Ma[i], c);
+    for (int i = LO; i < HI; i++) c = fmaf(0.5f * dx[i], Mx[i], c);
     return c;
   };
-  float a[NV], jtf[NV], H[NH], Ma[NV];
+  float H[NH], Ma[NV];
   uint32_t sig = 0u;
-  // warm start: qacc_warmstart unless qacc_smooth costs less
+  // warm start: qacc_warmstart unless qacc_smooth costs less (on this subsystem's cost)
   {
-    float js[NV];
-    const float cs = R.template pass<false>(a0, js, H, sig);
-    const float cw = gauss(S.warm, Ma) + R.template pass<false>(S.warm, jtf, H, sig);
+    float js[NV], wa[NV];
 #pragma unroll
-    for (int i = 0; i < NV; i++) a[i] = cw < cs ? S.warm[i] : a0[i];
+    for (int i = 0; i < NV; i++) wa[i] = S.warm[i];
+    const float cs = R.template pass<LO, HI, false>(a0, js, H, sig);
+    const float cw = gauss(wa, Ma) + R.template pass<LO, HI, false>(wa, jtf, H, sig);
+#pragma unroll
+    for (int i = LO; i < HI; i++) a[i] = cw < cs ? wa[i] : a0[i];
   }
-  // an arm-cube contact (or a generic overflow row) couples the arm and free-body blocks of H;
-  // otherwise H is block diagonal and factors as two 6x6 blocks
-  bool coupled = NF > 0 && CON && __any(R.ncon > R.nl);
-  if constexpr (NF > 0 && CON)
-    for (int c = 0; c < R.nl; c++) coupled |= __any((int)R.L.at(c, F_FLAGS) == (TOUCH_ARM | TOUCH_FREE));
 #pragma unroll
   for (int i = 0; i < NH; i++) H[i] = 0.f;
-  float cost = gauss(a, Ma) + R.template pass<true>(a, jtf, H, sig);
+  float cost = gauss(a, Ma) + R.template pass<LO, HI, true>(a, jtf, H, sig);
   int it = 0;
   for (; it < m.iterations; it++) {
     float g[NV], gn = 0.f;
 #pragma unroll
-    for (int i = 0; i < NV; i++) g[i] = Ma[i] - jtf[i], gn = fmaf(g[i], g[i], gn);
+    for (int i = LO; i < HI; i++) g[i] = Ma[i] - jtf[i], gn = fmaf(g[i], g[i], gn);
     if (scale * sqrtf(gn) < tol) break;
-    // H = M + rows' terms; p = -H^-1 g
+    // H = M + rows' terms (relative dof indices); p = -H^-1 g
+    if constexpr (LO < NA) {
 #pragma unroll
-    for (int i = 0; i < NA; i++)
+      for (int i = 0; i < NA; i++)
 #pragma unroll
-      for (int j = 0; j <= i; j++) H[i * (i + 1) / 2 + j] += S.MA[i * (i + 1) / 2 + j];
-#pragma unroll
-    for (int f = 0; f < NF; f++)
-#pragma unroll
-      for (int i = 0; i < 6; i++) {
-        const int d = NA + 6 * f + i;
-        H[d * (d + 1) / 2 + d] += S.MF[f][i * (i + 1) / 2 + i];
-      }
-    float p[NV], mg[NV];
-#pragma unroll
-    for (int i = 0; i < NV; i++) mg[i] = -g[i];
-    if (NF == 0 || coupled) {
-      float Hd[NV];
-      ldl_factor<NV>(H, Hd);
-      ldl_solve<NV>(H, Hd, p, mg);
-    } else {
-      // block diagonal: the arm block is H's first 21 packed entries; the free block is gathered
-      float Ha[NA * (NA + 1) / 2], Hf[21], Had[NA], Hfd[6];
-#pragma unroll
-      for (int k = 0; k < NA * (NA + 1) / 2; k++) Ha[k] = H[k];
-#pragma unroll
-      for (int i = 0; i < 6; i++)
-#pragma unroll
-        for (int j = 0; j <= i; j++) Hf[i * (i + 1) / 2 + j] = H[(NA + i) * (NA + i + 1) / 2 + NA + j];
-      ldl_factor<NA>(Ha, Had);
-      ldl_solve<NA>(Ha, Had, p, mg);
-      ldl_factor<6>(Hf, Hfd);
-      ldl_solve<6>(Hf, Hfd, p + NA, mg + NA);
+        for (int j = 0; j <= i; j++) H[(i - LO) * (i - LO + 1) / 2 + j - LO] += S.MA[i * (i + 1) / 2 + j];
     }
+    if constexpr (HI > NA) {
+#pragma unroll
+      for (int i = NA; i < NV; i++)
+        H[(i - LO) * (i - LO + 1) / 2 + i - LO] += S.MF[(i - NA) / 6][((i - NA) % 6) * ((i - NA) % 6 + 1) / 2 + (i - NA) % 6];
+    }
+    float Hd[NR], pr[NR], mg[NR], p[NV];
+#pragma unroll
+    for (int i = 0; i < NR; i++) mg[i] = -g[LO + i];
+    ldl_factor<NR>(H, Hd);
+    ldl_solve<NR>(H, Hd, pr, mg);
+#pragma unroll
+    for (int i = 0; i < NV; i++) p[i] = (i >= LO && i < HI) ? pr[i - LO] : 0.f;
     // exact line search: phi'(al) = (a - a0)' M p + al p' M p + rows; 1-D Newton, bracketed
     float Mp[NV], g0 = 0.f, pMp = 0.f;
-    mul_m(S, p, Mp);
+    mul_m<LO, HI>(S, p, Mp);
 #pragma unroll
-    for (int i = 0; i < NV; i++) {
+    for (int i = LO; i < HI; i++) {
       g0 = fmaf(a[i] - a0[i], Mp[i], g0);
       pMp = fmaf(p[i], Mp[i], pMp);
     }
-    R.ls_setup(a, p);
+    R.template ls_setup<LO, HI>(a, p);
     auto deriv = [&](float al, float& d2) {
       float d1 = fmaf(al, pMp, g0);
       d2 = pMp;
-      R.ls_eval(a, p, al, d1, d2);
+      R.template ls_eval<LO, HI>(a, p, al, d1, d2);
       return d1;
     };
     float h0;
-    const float dz = deriv(0.f, h0);
-    if (!(dz < 0.f)) break;  // not a descent direction at fp32 resolution: converged
+    if (!(deriv(0.f, h0) < 0.f)) break;  // not a descent direction at fp32 resolution: converged
     float lo = 0.f, hi = 3.0e38f, al = 1.f;
     for (int ls = 0; ls < 30; ls++) {
       float d2;
@@ -359,17 +372,16 @@ DEVI int newton_solve(Sim<NA, NF>& S, const NewtonRows<NA, NF, CON>& R) {
       }
       al = an;
     }
-    float an_[NV];
+    float an_[NV], jn[NV], Man[NV];
 #pragma unroll
     for (int i = 0; i < NV; i++) an_[i] = fmaf(al, p[i], a[i]);
-    float jn[NV], Man[NV];
 #pragma unroll
     for (int i = 0; i < NH; i++) H[i] = 0.f;
     const uint32_t sig0 = sig;
-    const float cn = gauss(an_, Man) + R.template pass<true>(an_, jn, H, sig);
+    const float cn = gauss(an_, Man) + R.template pass<LO, HI, true>(an_, jn, H, sig);
     if (!(cn <= cost)) break;  // rounding-level: no further progress (keep a)
 #pragma unroll
-    for (int i = 0; i < NV; i++) a[i] = an_[i], jtf[i] = jn[i], Ma[i] = Man[i];
+    for (int i = LO; i < HI; i++) a[i] = an_[i], jtf[i] = jn[i], Ma[i] = Man[i];
     const float improvement = cost - cn;
     cost = cn;
     // MuJoCo's test; its fp32 floor (a relative improvement at rounding level); and exactness:
@@ -378,6 +390,37 @@ DEVI int newton_solve(Sim<NA, NF>& S, const NewtonRows<NA, NF, CON>& R) {
         (sig == sig0 && fabsf(al - 1.f) < 1e-3f)) {
       it++;
       break;
+    }
+  }
+  return it;
+}
+
+// Primal Newton solve of the rows built by solve_constraints; sets S.qacc and S.fcon = J' f.
+// Returns the iteration count (both subsystems').
+template <int NA, int NF, bool CON>
+DEVI int newton_solve(Sim<NA, NF>& S, const NewtonRows<NA, NF, CON>& R) {
+  constexpr int NV = NA + 6 * NF;
+  float a[NV], jtf[NV];
+#pragma unroll
+  for (int i = 0; i < NV; i++) a[i] = S.qacc_s[i], jtf[i] = 0.f;
+  // an arm-cube contact (or a generic overflow row) in any lane of the wave couples the blocks
+  // (wave-uniform: every lane takes part in every vote)
+  bool coupled = false;
+  if constexpr (NF > 0 && CON) {
+    coupled = __any(R.ncon > R.nl);
+#pragma unroll
+    for (int c = 0; c < LDS_CON; c++)
+      coupled |= __any(c < R.nl && (int)R.L.at(c < R.nl ? c : 0, F_FLAGS) == (TOUCH_ARM | TOUCH_FREE));
+  }
+  int it;
+  if constexpr (NF == 0) {
+    it = newton_range<0, NV>(S, R, a, jtf);
+  } else {
+    if (coupled) {
+      it = newton_range<0, NV>(S, R, a, jtf);
+    } else {
+      it = newton_range<0, NA>(S, R, a, jtf);
+      it += newton_range<NA, NV>(S, R, a, jtf);
     }
   }
 #pragma unroll
