@@ -354,7 +354,8 @@ DEVI int newton_range(const Sim<NA, NF>& S, const NewtonRows<NA, NF, CON>& R, fl
       return d1;
     };
     float h0;
-    if (!(deriv(0.f, h0) < 0.f)) break;  // not a descent direction at fp32 resolution: converged
+    const float dz = deriv(0.f, h0);
+    if (!(dz < 0.f)) break;  // not a descent direction at fp32 resolution: converged
     float lo = 0.f, hi = 3.0e38f, al = 1.f;
     for (int ls = 0; ls < 30; ls++) {
       float d2;
@@ -379,15 +380,16 @@ DEVI int newton_range(const Sim<NA, NF>& S, const NewtonRows<NA, NF, CON>& R, fl
     for (int i = 0; i < NH; i++) H[i] = 0.f;
     const uint32_t sig0 = sig;
     const float cn = gauss(an_, Man) + R.template pass<LO, HI, true>(an_, jn, H, sig);
-    if (!(cn <= cost)) break;  // rounding-level: no further progress (keep a)
+    if (!(cn <= cost + 1e-5f * fabsf(cost))) break;  // a real increase (numerical trouble): keep a
 #pragma unroll
     for (int i = LO; i < HI; i++) a[i] = an_[i], jtf[i] = jn[i], Ma[i] = Man[i];
-    const float improvement = cost - cn;
     cost = cn;
-    // MuJoCo's test; its fp32 floor (a relative improvement at rounding level); and exactness:
-    // a full Newton step that leaves every row in its zone minimised the one quadratic there
-    if (scale * improvement < tol || improvement <= 1e-6f * fabsf(cn) ||
-        (sig == sig0 && fabsf(al - 1.f) < 1e-3f)) {
+    // MuJoCo's stopping test on the cost improvement, with the improvement taken from the
+    // quadratic model along p, -al phi'(0) / 2, instead of the difference of two costs: in fp32
+    // that difference is rounding noise (~1e-7 of a cost of order 1) long before the light
+    // rotational dofs of the cube (inertia 4.5e-6) have converged.  And exactness: a full
+    // Newton step that leaves every row in its zone has minimised the one quadratic there.
+    if (scale * (-0.5f * al * dz) < tol || (sig == sig0 && fabsf(al - 1.f) < 1e-3f)) {
       it++;
       break;
     }
