@@ -31,6 +31,13 @@
 
 namespace soarm {
 
+#ifdef SOARM_PHASE_PROF
+// diagnostic build: [0] solves (one lane per env), [1] sum of iterations, [2] sum of line-search
+// evaluations, [3] solves on the coupled (whole-problem) path, [4] sum of solve cycles, [5] max
+// solve cycles, [6] max iterations, [7] max line-search evaluations of one solve
+__device__ unsigned long long g_newton[8];
+#endif
+
 template <int NA, int NF, bool CON>
 struct NewtonRows {
   static constexpr int NV = NA + 6 * NF;
@@ -283,7 +290,7 @@ DEVI void mul_m(const Sim<NA, NF>& S, const float x[], float y[]) {
 // Newton on the subsystem over dofs [LO, HI): a[] (all dofs; only this range moves) in/out,
 // jtf[LO..HI) = J' f at the result.  Returns the iteration count.
 template <int LO, int HI, int NA, int NF, bool CON>
-DEVI int newton_range(const Sim<NA, NF>& S, const NewtonRows<NA, NF, CON>& R, float a[], float jtf[]) {
+DEVI int newton_range(const Sim<NA, NF>& S, const NewtonRows<NA, NF, CON>& R, float a[], float jtf[], int& nls) {
   constexpr int NV = NA + 6 * NF, NR = HI - LO, NH = NR * (NR + 1) / 2;
   const DModel& m = *S.mp;
   const float scale = m.pgs_scale, tol = m.tolerance;
@@ -348,6 +355,7 @@ DEVI int newton_range(const Sim<NA, NF>& S, const NewtonRows<NA, NF, CON>& R, fl
     }
     R.template ls_setup<LO, HI>(a, p);
     auto deriv = [&](float al, float& d2) {
+      nls++;
       float d1 = fmaf(al, pMp, g0);
       d2 = pMp;
       R.template ls_eval<LO, HI>(a, p, al, d1, d2);
@@ -414,17 +422,33 @@ DEVI int newton_solve(Sim<NA, NF>& S, const NewtonRows<NA, NF, CON>& R) {
     for (int c = 0; c < LDS_CON; c++)
       coupled |= __any(c < R.nl && (int)R.L.at(c < R.nl ? c : 0, F_FLAGS) == (TOUCH_ARM | TOUCH_FREE));
   }
-  int it;
+  int it, nls = 0;
+#ifdef SOARM_PHASE_PROF
+  const long long t0 = clock64();
+#endif
   if constexpr (NF == 0) {
-    it = newton_range<0, NV>(S, R, a, jtf);
+    it = newton_range<0, NV>(S, R, a, jtf, nls);
   } else {
     if (coupled) {
-      it = newton_range<0, NV>(S, R, a, jtf);
+      it = newton_range<0, NV>(S, R, a, jtf, nls);
     } else {
-      it = newton_range<0, NA>(S, R, a, jtf);
-      it += newton_range<NA, NV>(S, R, a, jtf);
+      it = newton_range<0, NA>(S, R, a, jtf, nls);
+      it += newton_range<NA, NV>(S, R, a, jtf, nls);
     }
   }
+#ifdef SOARM_PHASE_PROF
+  if ((threadIdx.x & (lpe<NF>() - 1)) == 0) {
+    const unsigned long long dt = (unsigned long long)(clock64() - t0);
+    atomicAdd(&g_newton[0], 1ull);
+    atomicAdd(&g_newton[1], (unsigned long long)it);
+    atomicAdd(&g_newton[2], (unsigned long long)nls);
+    atomicAdd(&g_newton[3], (unsigned long long)coupled);
+    atomicAdd(&g_newton[4], dt);
+    atomicMax(&g_newton[5], dt);
+    atomicMax(&g_newton[6], (unsigned long long)it);
+    atomicMax(&g_newton[7], (unsigned long long)nls);
+  }
+#endif
 #pragma unroll
   for (int i = 0; i < NV; i++) S.qacc[i] = a[i], S.fcon[i] = jtf[i];
   return it;

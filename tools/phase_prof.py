@@ -37,14 +37,14 @@ from lerobot_mujoco_sim2real_amd.sim import BatchSim  # noqa: E402
 
 n = int(os.environ.get("ENVS", 4096))
 T = int(sys.argv[1]) if len(sys.argv) > 1 else 120
-cm = W.model(os.environ.get("CONFIG", "contact"))
+cm = W.model(os.environ.get("CONFIG", "contact"), solver=os.environ.get("SOLVER", "PGS"))
 ids = np.arange(n)
 sim = BatchSim(cm, n, 0)
 q0 = W.initial_qpos(cm, ids, 0)
 sim.reset(init_qpos=q0[:, :5], extra_qpos=q0, seed=0)
 tab = {k: (torch.as_tensor(v, dtype=torch.float32, device="cuda") if isinstance(v, np.ndarray) else v)
        for k, v in W.chirp_tables(ids, 0).items()}
-out = (ctypes.c_double * 77)()
+out = (ctypes.c_double * 85)()
 res = {}
 every = int(os.environ.get("EVERY", 0))
 starts = set(range(0, T, every)) if every else {0, T // 2, T - 10}
@@ -88,6 +88,11 @@ for t in range(T):
                                      "mean_pgs_cycles": v[69 + i] / max(v[61 + i], 1),
                                      "mean_retire_sweep": v[73 + i] / max(v[61 + i], 1)}
                                  for i, k in enumerate(["E", "E_coupled", "EF", "EF_coupled"])}
+        if v[77] > 0:
+            r["newton"] = {"solves": v[77], "mean_iters": v[78] / v[77], "mean_ls_evals": v[79] / v[77],
+                           "coupled_frac": v[80] / v[77], "mean_cycles": v[81] / v[77], "max_cycles": v[82],
+                           "max_iters": v[83], "max_ls_evals": v[84],
+                           "solve_frac_of_total": v[81] / max(tot, 1)}
         res[t] = r
         print(t, json.dumps(r), flush=True)
-json.dump(res, open(os.path.join(ROOT, "gpurun_out", f"phase_prof_{os.environ.get('CONFIG', 'contact')}.json"), "w"), indent=1)
+json.dump(res, open(os.path.join(ROOT, "gpurun_out", f"phase_prof_{os.environ.get('CONFIG', 'contact')}_{os.environ.get('SOLVER', 'PGS').lower()}.json"), "w"), indent=1)
