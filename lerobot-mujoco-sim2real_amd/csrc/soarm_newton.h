@@ -34,8 +34,16 @@ namespace soarm {
 #ifdef SOARM_PHASE_PROF
 // diagnostic build: [0] solves (one lane per env), [1] sum of iterations, [2] sum of line-search
 // evaluations, [3] solves on the coupled (whole-problem) path, [4] sum of solve cycles, [5] max
-// solve cycles, [6] max iterations, [7] max line-search evaluations of one solve
-__device__ unsigned long long g_newton[8];
+// solve cycles, [6] max iterations, [7] max line-search evaluations of one solve; split solves
+// (per env): [8] arm iterations, [9] arm evaluations, [10] free-body iterations, [11] free-body
+// evaluations; per wave: [12] waves, [13] sum over waves of the wave's max evaluations, [14] of
+// its max iterations, [15] sum of wave solve cycles (lane 0)
+__device__ unsigned long long g_newton[16];
+DEVI int wave_max_i(int v) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) v = max(v, __shfl_xor(v, o));
+  return v;
+}
 #endif
 
 template <int NA, int NF, bool CON>
@@ -56,58 +64,40 @@ struct NewtonRows {
   }
   static constexpr int hidx(int i, int j) { return i * (i + 1) / 2 + j; }  // packed lower, i >= j
 
+  // Quad mode (lpe() = 4 lanes per env): the env's contacts (and overflow rows) are split over
+  // its lanes, lane k taking contacts k, k+4, ...; the partial sums are combined by quad
+  // butterflies (bit-identical on the 4 lanes), so every later step runs on identical values.
+  // The dof rows (frictionloss, limits) are cheap and run on every lane.
+  static constexpr int QL = lpe<NF>();
+  static_assert(QL == 1 || QL == 4, "Newton lane split: 1 or 4 lanes per env");
+  DEVI int ql() const { return QL == 1 ? 0 : (L.lane & 3); }
+  static DEVI float qred(float x) {
+    if constexpr (QL == 4) return qsum(x);
+    else return x;
+  }
+  static DEVI float qmaxf(float x) {
+    if constexpr (QL == 4) {
+      const float t = fmaxf(x, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xF, 0xF, false)));
+      return fmaxf(t, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(t), 0x4E, 0xF, 0xF, false)));
+    } else {
+      return x;
+    }
+  }
+  static DEVI float qminf(float x) { return -qmaxf(-x); }
+
   // one pass over the subsystem's rows at a: its cost, J' f (dofs LO..HI-1), (WANT_H) the rows'
-  // Hessian terms added to H (packed lower over the subsystem's dofs), and sig, a signature of
-  // the rows' zones (quadratic / linear / inactive): Newton has converged once a full step
-  // leaves it unchanged (the cost is one quadratic there)
+  // Hessian terms added to H (packed lower over the subsystem's dofs; zero on entry), and sig, a
+  // signature of this lane's rows' zones (quadratic / linear / inactive): Newton has converged
+  // once a full step leaves every lane's unchanged (the cost is one quadratic there)
   template <int LO, int HI, bool WANT_H>
   DEVI float pass(const float a[NV], float jtf[NV], float H[], uint32_t& sig) const {
+    constexpr int NR = HI - LO, NH = NR * (NR + 1) / 2;
     float cost = 0.f;
     sig = 0u;
 #pragma unroll
     for (int i = LO; i < HI; i++) jtf[i] = 0.f;
-    if constexpr (LO == 0) {
-      // frictionloss rows (J = e_i)
-#pragma unroll
-      for (int i = 0; i < NA; i++) {
-        const float fl = m.dof_frictionloss[i], R = fR[i];
-        const float x = a[i] - fa[i];
-        float f, c;
-        bool q = false;
-        if (x <= -R * fl) {
-          f = fl, c = -fl * x - 0.5f * R * fl * fl;
-        } else if (x >= R * fl) {
-          f = -fl, c = fl * x - 0.5f * R * fl * fl;
-        } else {
-          f = -x / R, c = 0.5f * x * x / R, q = fl > 0.f;
-        }
-        cost += c;
-        jtf[i] += f;
-        sig = sig * 3u + (q ? 1u : (x < 0.f ? 2u : 0u));
-        if constexpr (WANT_H)
-          if (q) H[hidx(i, i)] += 1.f / R;
-      }
-      // joint limits (J = sign e_dof)
-      for (int l = 0; l < nlim; l++) {
-        const int d = (int)L.lm(l, L_DOF);
-        const float sg = L.lm(l, L_SGN), R = L.lm(l, L_R);
-        float ad = 0.f;
-#pragma unroll
-        for (int i = 0; i < NA; i++) ad = i == d ? a[i] : ad;
-        const float x = sg * ad - L.lm(l, L_AREF);
-        sig = sig * 2u + (x < 0.f ? 1u : 0u);
-        if (x < 0.f) {
-          cost += 0.5f * x * x / R;
-          const float f = -x / R;
-#pragma unroll
-          for (int i = 0; i < NA; i++) {
-            jtf[i] += i == d ? sg * f : 0.f;
-            if constexpr (WANT_H) H[hidx(i, i)] += i == d ? 1.f / R : 0.f;
-          }
-        }
-      }
-    }
     if constexpr (CON) {
+      bool mine = false;
       // one contact over the dof range [CL, CH) its Jacobian can be nonzero on
       auto contact = [&](int c, auto cl, auto ch) {
         constexpr int CL = decltype(cl)::value, CH = decltype(ch)::value;
@@ -153,10 +143,12 @@ struct NewtonRows {
               H[hidx(i - LO, j - LO)] += jc[0][i] * kj[0][j] + jc[1][i] * kj[1][j] + jc[2][i] * kj[2][j];
         }
       };
-      for (int c = 0; c < nl; c++) {
+      for (int c = ql(); c < nl; c += QL) {
         const int fl = (int)L.at(c, F_FLAGS);
         if constexpr (LO == 0 && HI == NV) {
-          // whole problem: still skip the halves a contact cannot touch (wave-uniform choice)
+          mine = true;
+          // whole problem: still skip the halves a contact cannot touch (choice uniform over
+          // the lanes still in the loop)
           if (NF > 0 && __all(fl == TOUCH_FREE))
             contact(c, std::integral_constant<int, NA>{}, std::integral_constant<int, NV>{});
           else if (__all(!(fl & TOUCH_FREE)))
@@ -164,12 +156,14 @@ struct NewtonRows {
           else
             contact(c, std::integral_constant<int, 0>{}, std::integral_constant<int, NV>{});
         } else if (owns<LO, HI>(fl)) {
+          mine = true;
           contact(c, std::integral_constant<int, LO>{}, std::integral_constant<int, HI>{});
         }
       }
       if constexpr (LO == 0 && HI == NV) {
         // contacts past the LDS records: per-edge rows in the global slab (rare; whole problem)
-        for (int r = 4 * nl; r < 4 * ncon; r++) {
+        for (int r = 4 * nl + ql(); r < 4 * ncon; r += QL) {
+          mine = true;
           float J[NV], x = -cr.S(r, 0);
 #pragma unroll
           for (int i = 0; i < NV; i++) J[i] = cr.J(r, i), x = fmaf(J[i], a[i], x);
@@ -187,16 +181,72 @@ struct NewtonRows {
           }
         }
       }
+      // combine the quad's partial sums (skipped, wave-uniformly, when no lane has a row here:
+      // every partial is then zero)
+      if constexpr (QL > 1) {
+        if (__any(mine)) {
+          cost = qred(cost);
+#pragma unroll
+          for (int i = LO; i < HI; i++) jtf[i] = qred(jtf[i]);
+          if constexpr (WANT_H)
+#pragma unroll
+            for (int k = 0; k < NH; k++) H[k] = qred(H[k]);
+        }
+      }
+    }
+    if constexpr (LO == 0) {
+      // frictionloss rows (J = e_i)
+#pragma unroll
+      for (int i = 0; i < NA; i++) {
+        const float fl = m.dof_frictionloss[i], R = fR[i];
+        const float x = a[i] - fa[i];
+        float f, c;
+        bool q = false;
+        if (x <= -R * fl) {
+          f = fl, c = -fl * x - 0.5f * R * fl * fl;
+        } else if (x >= R * fl) {
+          f = -fl, c = fl * x - 0.5f * R * fl * fl;
+        } else {
+          f = -x / R, c = 0.5f * x * x / R, q = fl > 0.f;
+        }
+        cost += c;
+        jtf[i] += f;
+        sig = sig * 3u + (q ? 1u : (x < 0.f ? 2u : 0u));
+        if constexpr (WANT_H)
+          if (q) H[hidx(i, i)] += 1.f / R;
+      }
+      // joint limits (J = sign e_dof)
+      for (int l = 0; l < nlim; l++) {
+        const int d = (int)L.lm(l, L_DOF);
+        const float sg = L.lm(l, L_SGN), R = L.lm(l, L_R);
+        float ad = 0.f;
+#pragma unroll
+        for (int i = 0; i < NA; i++) ad = i == d ? a[i] : ad;
+        const float x = sg * ad - L.lm(l, L_AREF);
+        sig = sig * 2u + (x < 0.f ? 1u : 0u);
+        if (x < 0.f) {
+          cost += 0.5f * x * x / R;
+          const float f = -x / R;
+#pragma unroll
+          for (int i = 0; i < NA; i++) {
+            jtf[i] += i == d ? sg * f : 0.f;
+            if constexpr (WANT_H) H[hidx(i, i)] += i == d ? 1.f / R : 0.f;
+          }
+        }
+      }
     }
     return cost;
   }
 
-  // line-search data along p: per contact edge the residual at a and its rate along p, in LDS
-  // scratch (ext area, 8 floats per contact), read at every line-search point
+  // line-search data along p: per contact edge its residual at a, its rate along p and the step
+  // length where it changes zone (a kink of the line cost), in LDS scratch (ext area, 12 floats
+  // per contact; written and read by the lane that owns the contact)
+  static constexpr int LS_STRIDE = 12;
+  static_assert(XS_LIST + LS_STRIDE * LDS_CON <= XS_EXT, "line-search scratch fits the ext area");
   template <int LO, int HI>
   DEVI void ls_setup(const float a[NV], const float p[NV]) const {
     if constexpr (CON) {
-      for (int c = 0; c < nl; c++) {
+      for (int c = ql(); c < nl; c += QL) {
         if (!owns<LO, HI>((int)L.at(c, F_FLAGS))) continue;
         float ya[3] = {0.f, 0.f, 0.f}, yp[3] = {0.f, 0.f, 0.f};
 #pragma unroll
@@ -211,12 +261,14 @@ struct NewtonRows {
         for (int ed = 0; ed < 4; ed++) {
           const float s = (ed & 1) ? -mu : mu;
           const int t = 1 + (ed >> 1);
-          L.ex(XS_LIST + 8 * c + ed) = ya[0] + s * ya[t] - L.at(c, F_AREF + ed);
-          L.ex(XS_LIST + 8 * c + 4 + ed) = yp[0] + s * yp[t];
+          const float x0 = ya[0] + s * ya[t] - L.at(c, F_AREF + ed), v = yp[0] + s * yp[t];
+          L.ex(XS_LIST + LS_STRIDE * c + ed) = x0;
+          L.ex(XS_LIST + LS_STRIDE * c + 4 + ed) = v;
+          L.ex(XS_LIST + LS_STRIDE * c + 8 + ed) = v != 0.f ? -x0 / v : 3.0e38f;
         }
       }
       if constexpr (LO == 0 && HI == NV)
-        for (int r = 4 * nl; r < 4 * ncon; r++) {
+        for (int r = 4 * nl + ql(); r < 4 * ncon; r += QL) {
           float x = -cr.S(r, 0), v = 0.f;
 #pragma unroll
           for (int i = 0; i < NV; i++) x = fmaf(cr.J(r, i), a[i], x), v = fmaf(cr.J(r, i), p[i], v);
@@ -225,17 +277,57 @@ struct NewtonRows {
     }
   }
 
-  // d/dalpha and d2/dalpha2 of the subsystem rows' cost at a + alpha p (Gauss part: caller)
+  // d/dalpha and d2/dalpha2 of the subsystem rows' cost at a + alpha p added to d1, d2 (Gauss
+  // part: caller), and the piece [bl, br] of the piecewise-quadratic line cost that alpha lies in
+  // (the nearest kinks at or below / above alpha): d/dalpha is linear there
   template <int LO, int HI>
-  DEVI void ls_eval(const float a[NV], const float p[NV], float al, float& d1, float& d2) const {
+  DEVI void ls_eval(const float a[NV], const float p[NV], float al, float& d1, float& d2, float& bl,
+                    float& br) const {
+    auto kink = [&](float t, float& l, float& r) {
+      r = t > al ? fminf(r, t) : r;
+      l = t <= al ? fmaxf(l, t) : l;
+    };
+    if constexpr (CON) {
+      float c1 = 0.f, c2 = 0.f, cl = -3.0e38f, cr_ = 3.0e38f;
+      bool mine = false;
+      for (int c = ql(); c < nl; c += QL) {
+        if (!owns<LO, HI>((int)L.at(c, F_FLAGS))) continue;
+        mine = true;
+        const float D = 1.f / L.at(c, F_R);
+#pragma unroll
+        for (int ed = 0; ed < 4; ed++) {
+          const float v = L.ex(XS_LIST + LS_STRIDE * c + 4 + ed);
+          const float x = fmaf(al, v, L.ex(XS_LIST + LS_STRIDE * c + ed));
+          if (x < 0.f) c1 += x * v * D, c2 += v * v * D;
+          kink(L.ex(XS_LIST + LS_STRIDE * c + 8 + ed), cl, cr_);
+        }
+      }
+      if constexpr (LO == 0 && HI == NV)
+        for (int r = 4 * nl + ql(); r < 4 * ncon; r += QL) {
+          mine = true;
+          const float D = 1.f / cr.S(r, 1), v = cr.W(r, 1), x0 = cr.W(r, 0);
+          const float x = fmaf(al, v, x0);
+          if (x < 0.f) c1 += x * v * D, c2 += v * v * D;
+          if (v != 0.f) kink(-x0 * __builtin_amdgcn_rcpf(v), cl, cr_);
+        }
+      if constexpr (QL > 1) {
+        if (__any(mine)) c1 = qred(c1), c2 = qred(c2), cl = qmaxf(cl), cr_ = qminf(cr_);
+      }
+      d1 += c1, d2 += c2, bl = fmaxf(bl, cl), br = fminf(br, cr_);
+    }
     if constexpr (LO == 0) {
 #pragma unroll
       for (int i = 0; i < NA; i++) {
         const float fl = m.dof_frictionloss[i], R = fR[i];
-        const float x = a[i] - fa[i] + al * p[i];
+        const float x0 = a[i] - fa[i], x = fmaf(al, p[i], x0);
         const float f = x <= -R * fl ? fl : (x >= R * fl ? -fl : -x / R);
         d1 -= f * p[i];
         d2 += (x > -R * fl && x < R * fl && fl > 0.f) ? p[i] * p[i] / R : 0.f;
+        if (fl > 0.f && p[i] != 0.f) {
+          const float rp = __builtin_amdgcn_rcpf(p[i]);
+          kink((R * fl - x0) * rp, bl, br);
+          kink((-R * fl - x0) * rp, bl, br);
+        }
       }
       for (int l = 0; l < nlim; l++) {
         const int d = (int)L.lm(l, L_DOF);
@@ -243,27 +335,10 @@ struct NewtonRows {
         float ad = 0.f, pd = 0.f;
 #pragma unroll
         for (int i = 0; i < NA; i++) ad = i == d ? a[i] : ad, pd = i == d ? p[i] : pd;
-        const float x = sg * (ad + al * pd) - L.lm(l, L_AREF), v = sg * pd;
+        const float x0 = sg * ad - L.lm(l, L_AREF), v = sg * pd, x = fmaf(al, v, x0);
         if (x < 0.f) d1 += x * v / R, d2 += v * v / R;
+        if (v != 0.f) kink(-x0 * __builtin_amdgcn_rcpf(v), bl, br);
       }
-    }
-    if constexpr (CON) {
-      for (int c = 0; c < nl; c++) {
-        if (!owns<LO, HI>((int)L.at(c, F_FLAGS))) continue;
-        const float D = 1.f / L.at(c, F_R);
-#pragma unroll
-        for (int ed = 0; ed < 4; ed++) {
-          const float v = L.ex(XS_LIST + 8 * c + 4 + ed);
-          const float x = fmaf(al, v, L.ex(XS_LIST + 8 * c + ed));
-          if (x < 0.f) d1 += x * v * D, d2 += v * v * D;
-        }
-      }
-      if constexpr (LO == 0 && HI == NV)
-        for (int r = 4 * nl; r < 4 * ncon; r++) {
-          const float D = 1.f / cr.S(r, 1), v = cr.W(r, 1);
-          const float x = fmaf(al, v, cr.W(r, 0));
-          if (x < 0.f) d1 += x * v * D, d2 += v * v * D;
-        }
     }
   }
 };
@@ -307,19 +382,25 @@ DEVI int newton_range(const Sim<NA, NF>& S, const NewtonRows<NA, NF, CON>& R, fl
   };
   float H[NH], Ma[NV];
   uint32_t sig = 0u;
-  // warm start: qacc_warmstart unless qacc_smooth costs less (on this subsystem's cost)
+  // warm start: qacc_warmstart unless qacc_smooth costs less (on this subsystem's cost); the
+  // Hessian pass runs at the warm point, and again at qacc_smooth only in lanes where it wins
+  float cost;
   {
-    float js[NV], wa[NV];
-#pragma unroll
-    for (int i = 0; i < NV; i++) wa[i] = S.warm[i];
+    float js[NV];
     const float cs = R.template pass<LO, HI, false>(a0, js, H, sig);
-    const float cw = gauss(wa, Ma) + R.template pass<LO, HI, false>(wa, jtf, H, sig);
 #pragma unroll
-    for (int i = LO; i < HI; i++) a[i] = cw < cs ? wa[i] : a0[i];
+    for (int i = 0; i < NV; i++) a[i] = (i >= LO && i < HI) ? S.warm[i] : a[i];
+#pragma unroll
+    for (int i = 0; i < NH; i++) H[i] = 0.f;
+    cost = gauss(a, Ma) + R.template pass<LO, HI, true>(a, jtf, H, sig);
+    if (cs < cost) {
+#pragma unroll
+      for (int i = LO; i < HI; i++) a[i] = a0[i], Ma[i] = 0.f;
+#pragma unroll
+      for (int i = 0; i < NH; i++) H[i] = 0.f;
+      cost = R.template pass<LO, HI, true>(a, jtf, H, sig);
+    }
   }
-#pragma unroll
-  for (int i = 0; i < NH; i++) H[i] = 0.f;
-  float cost = gauss(a, Ma) + R.template pass<LO, HI, true>(a, jtf, H, sig);
   int it = 0;
   for (; it < m.iterations; it++) {
     float g[NV], gn = 0.f;
@@ -345,40 +426,37 @@ DEVI int newton_range(const Sim<NA, NF>& S, const NewtonRows<NA, NF, CON>& R, fl
     ldl_solve<NR>(H, Hd, pr, mg);
 #pragma unroll
     for (int i = 0; i < NV; i++) p[i] = (i >= LO && i < HI) ? pr[i - LO] : 0.f;
-    // exact line search: phi'(al) = (a - a0)' M p + al p' M p + rows; 1-D Newton, bracketed
-    float Mp[NV], g0 = 0.f, pMp = 0.f;
+    // exact line search: phi'(al) = (a - a0)' M p + al p' M p + rows, continuous and piecewise
+    // linear in al.  From al = 1 (the Newton step): evaluate phi', phi'' and the piece around al;
+    // the 1-D Newton target is the exact minimiser when it lies in that piece (usually the first
+    // evaluation), else it moves the bracket and the next point is that target, or the secant
+    // of the bracket when the target leaves it.  phi'(0) = g'p needs no evaluation.
+    float Mp[NV], g0 = 0.f, pMp = 0.f, dz = 0.f;
     mul_m<LO, HI>(S, p, Mp);
 #pragma unroll
     for (int i = LO; i < HI; i++) {
       g0 = fmaf(a[i] - a0[i], Mp[i], g0);
       pMp = fmaf(p[i], Mp[i], pMp);
+      dz = fmaf(g[i], p[i], dz);
     }
-    R.template ls_setup<LO, HI>(a, p);
-    auto deriv = [&](float al, float& d2) {
-      nls++;
-      float d1 = fmaf(al, pMp, g0);
-      d2 = pMp;
-      R.template ls_eval<LO, HI>(a, p, al, d1, d2);
-      return d1;
-    };
-    float h0;
-    const float dz = deriv(0.f, h0);
     if (!(dz < 0.f)) break;  // not a descent direction at fp32 resolution: converged
-    float lo = 0.f, hi = 3.0e38f, al = 1.f;
-    for (int ls = 0; ls < 30; ls++) {
-      float d2;
-      const float d1 = deriv(al, d2);
-      if (d1 < 0.f)
-        lo = al;
-      else
-        hi = al;
-      if (d1 == 0.f) break;
-      float an = al - d1 / d2;  // exact within the current piece
-      if (!(an > lo && an < hi)) an = hi < 3.0e38f ? 0.5f * (lo + hi) : 2.f * al;
-      if (fabsf(an - al) <= 1e-6f * al) {
+    R.template ls_setup<LO, HI>(a, p);
+    float lo = 0.f, dlo = dz, hi = 3.0e38f, dhi = 0.f, al = 1.f;
+    for (int ls = 0; ls < 24; ls++) {
+      nls++;
+      float d1 = fmaf(al, pMp, g0), d2 = pMp, bl = -3.0e38f, br = 3.0e38f;
+      R.template ls_eval<LO, HI>(a, p, al, d1, d2, bl, br);
+      float an = al - d1 / d2;
+      if (an >= bl && an <= br) {
         al = an;
         break;
       }
+      if (d1 < 0.f)
+        lo = al, dlo = d1;
+      else
+        hi = al, dhi = d1;
+      if (!(an > lo && an < hi)) an = lo + (hi - lo) * (dlo / (dlo - dhi));
+      if (!(an > lo && an < hi)) break;  // bracket exhausted at fp32 resolution
       al = an;
     }
     float an_[NV], jn[NV], Man[NV];
@@ -397,7 +475,9 @@ DEVI int newton_range(const Sim<NA, NF>& S, const NewtonRows<NA, NF, CON>& R, fl
     // that difference is rounding noise (~1e-7 of a cost of order 1) long before the light
     // rotational dofs of the cube (inertia 4.5e-6) have converged.  And exactness: a full
     // Newton step that leaves every row in its zone has minimised the one quadratic there.
-    if (scale * (-0.5f * al * dz) < tol || (sig == sig0 && fabsf(al - 1.f) < 1e-3f)) {
+    bool same = sig == sig0;  // every lane of the env: its rows kept their zones
+    if constexpr (NewtonRows<NA, NF, CON>::QL > 1) same = qsum(same ? 0.f : 1.f) == 0.f;
+    if (scale * (-0.5f * al * dz) < tol || (same && fabsf(al - 1.f) < 1e-3f)) {
       it++;
       break;
     }
@@ -433,7 +513,18 @@ DEVI int newton_solve(Sim<NA, NF>& S, const NewtonRows<NA, NF, CON>& R) {
       it = newton_range<0, NV>(S, R, a, jtf, nls);
     } else {
       it = newton_range<0, NA>(S, R, a, jtf, nls);
+#ifdef SOARM_PHASE_PROF
+      const int it_arm = it, nls_arm = nls;
+#endif
       it += newton_range<NA, NV>(S, R, a, jtf, nls);
+#ifdef SOARM_PHASE_PROF
+      if ((threadIdx.x & (lpe<NF>() - 1)) == 0) {
+        atomicAdd(&g_newton[8], (unsigned long long)it_arm);
+        atomicAdd(&g_newton[9], (unsigned long long)nls_arm);
+        atomicAdd(&g_newton[10], (unsigned long long)(it - it_arm));
+        atomicAdd(&g_newton[11], (unsigned long long)(nls - nls_arm));
+      }
+#endif
     }
   }
 #ifdef SOARM_PHASE_PROF
@@ -447,6 +538,13 @@ DEVI int newton_solve(Sim<NA, NF>& S, const NewtonRows<NA, NF, CON>& R) {
     atomicMax(&g_newton[5], dt);
     atomicMax(&g_newton[6], (unsigned long long)it);
     atomicMax(&g_newton[7], (unsigned long long)nls);
+  }
+  const int wl = wave_max_i(nls), wi = wave_max_i(it);
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(&g_newton[12], 1ull);
+    atomicAdd(&g_newton[13], (unsigned long long)wl);
+    atomicAdd(&g_newton[14], (unsigned long long)wi);
+    atomicAdd(&g_newton[15], (unsigned long long)(clock64() - t0));
   }
 #endif
 #pragma unroll

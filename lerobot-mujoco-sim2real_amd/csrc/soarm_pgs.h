@@ -353,9 +353,11 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
                            const ContactRows<NA, NF>& cr, const PairMask& pm) {
   constexpr int NV = Sim<NA, NF>::NV;
   const DModel& m = *S.mp;
+  // Newton needs neither M^-1 nor the rows' ARdiag (PGS's step sizes): its rows are J, aref, R
+  constexpr bool NEWT = SOL == SIM_SOL_NEWTON;
   S.solve_m(S.qacc_s, S.fsmooth);
   MInv<NA, NF> Mi;
-  Mi.build(S);
+  if constexpr (!NEWT) Mi.build(S);
   PSTAMP(6);
 
   // ---- dof frictionloss rows (MuJoCo row order: all of them first)
@@ -364,9 +366,11 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   for (int i = 0; i < NA; i++) {
     fR[i] = m.dof_fricR[i];
     fa[i] = -m.dof_fricB[i] * S.qvel[i];
-    const float ard = Mi.a(i, i) + fR[i];
-    fhD[i] = 0.5f * ard;
-    fiD[i] = 1.f / ard;
+    if constexpr (!NEWT) {
+      const float ard = Mi.a(i, i) + fR[i];
+      fhD[i] = 0.5f * ard;
+      fiD[i] = 1.f / ard;
+    }
   }
   // ---- joint-limit rows: joint by joint, lower then upper; compact list in LDS
   int nlim = 0;
@@ -379,13 +383,15 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
         const float imp = impedance(m.jnt_solimp[i], dist, m.jnt_margin[i]);
         const float R = fmaxf(MINVALF, (1.f - imp) * m.dof_invweight0[i] / imp);
         const float vel = side == 0 ? S.qvel[i] : -S.qvel[i];
-        const float ard = Mi.a(i, i) + R;
         L.lm(nlim, L_DOF) = (float)i;
         L.lm(nlim, L_SGN) = side == 0 ? 1.f : -1.f;
         L.lm(nlim, L_AREF) = -m.jnt_KB[i][1] * vel - m.jnt_KB[i][0] * imp * (dist - m.jnt_margin[i]);
         L.lm(nlim, L_R) = R;
-        L.lm(nlim, L_ARD) = ard;
-        L.lm(nlim, L_IARD) = 1.f / ard;
+        if constexpr (!NEWT) {
+          const float ard = Mi.a(i, i) + R;
+          L.lm(nlim, L_ARD) = ard;
+          L.lm(nlim, L_IARD) = 1.f / ard;
+        }
         nlim++;
       }
     }
@@ -479,21 +485,24 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       // avoids running both sides of a divergent flag test) unless no lane's contact
       // touches the arm: then the free-body half alone (diagonal M^-1).
       float W0[NV], W1[NV], W2[NV], G[6];
-      const bool arm_any = NF == 0 || !__all(!ta);
-      Mi.mul(jd[0], W0, arm_any, true);
-      Mi.mul(jd[1], W1, arm_any, true);
-      Mi.mul(jd[2], W2, arm_any, true);
-      G[0] = dotv<NA, NF>(jd[0], W0, arm_any, true), G[1] = dotv<NA, NF>(jd[0], W1, arm_any, true);
-      G[2] = dotv<NA, NF>(jd[0], W2, arm_any, true), G[3] = dotv<NA, NF>(jd[1], W1, arm_any, true);
-      G[4] = dotv<NA, NF>(jd[1], W2, arm_any, true), G[5] = dotv<NA, NF>(jd[2], W2, arm_any, true);
+      if constexpr (!NEWT) {
+        const bool arm_any = NF == 0 || !__all(!ta);
+        Mi.mul(jd[0], W0, arm_any, true);
+        Mi.mul(jd[1], W1, arm_any, true);
+        Mi.mul(jd[2], W2, arm_any, true);
+        G[0] = dotv<NA, NF>(jd[0], W0, arm_any, true), G[1] = dotv<NA, NF>(jd[0], W1, arm_any, true);
+        G[2] = dotv<NA, NF>(jd[0], W2, arm_any, true), G[3] = dotv<NA, NF>(jd[1], W1, arm_any, true);
+        G[4] = dotv<NA, NF>(jd[1], W2, arm_any, true), G[5] = dotv<NA, NF>(jd[2], W2, arm_any, true);
+      }
       float vq[3] = {0.f, 0.f, 0.f};
 #pragma unroll
       for (int i = 0; i < NV; i++)
         vq[0] += jd[0][i] * S.qvel[i], vq[1] += jd[1][i] * S.qvel[i], vq[2] += jd[2][i] * S.qvel[i];
-      if (lds) {
+      if constexpr (!NEWT)
+        if (lds) {
 #pragma unroll
-        for (int k2 = 0; k2 < 6; k2++) wrec(c, F_GRAM + k2, G[k2], split);
-      }
+          for (int k2 = 0; k2 < 6; k2++) wrec(c, F_GRAM + k2, G[k2], split);
+        }
       RP_MARK(2);
 #pragma unroll
       for (int ed = 0; ed < 4; ed++) {
@@ -501,22 +510,24 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
         const bool k2 = ed >> 1;
         const float vel = vq[0] + s * (k2 ? vq[2] : vq[1]);
         // J_e M^-1 J_e' = G_nn + 2 s G_nk + s^2 G_kk
-        const float ard = G[0] + s * (2.f * (k2 ? G[2] : G[1]) + s * (k2 ? G[5] : G[3])) + Rpy;
+        const float ard = NEWT ? 0.f : G[0] + s * (2.f * (k2 ? G[2] : G[1]) + s * (k2 ? G[5] : G[3])) + Rpy;
         const float ar = -KB1 * vel - KB0 * imp * (cdist - margin);
         if (lds) {
           wrec(c, F_AREF + ed, ar, split);
-          wrec(c, F_HARD + ed, 0.5f * ard, split);
-          wrec(c, F_IARD + ed, 1.f / ard, split);
+          if constexpr (!NEWT) {
+            wrec(c, F_HARD + ed, 0.5f * ard, split);
+            wrec(c, F_IARD + ed, 1.f / ard, split);
+          }
         } else {
           const int r = 4 * c + ed;
 #pragma unroll
           for (int i = 0; i < NV; i++) {
             cr.J(r, i) = jd[0][i] + s * (k2 ? jd[2][i] : jd[1][i]);
-            cr.W(r, i) = W0[i] + s * (k2 ? W2[i] : W1[i]);
+            if constexpr (!NEWT) cr.W(r, i) = W0[i] + s * (k2 ? W2[i] : W1[i]);
           }
           cr.S(r, 0) = ar;
           cr.S(r, 1) = Rpy;
-          cr.S(r, 2) = ard;
+          if constexpr (!NEWT) cr.S(r, 2) = ard;
         }
       }
   };
@@ -613,7 +624,19 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   const int nl = ncon < LDS_CON ? ncon : LDS_CON;
   if constexpr (SOL == SIM_SOL_NEWTON) {  // MuJoCo's default solver on the same rows (soarm_newton.h)
     const NewtonRows<NA, NF, CON> nr{m, L, cr, fR, fa, nlim, nl, ncon};
-    newton_solve(S, nr);
+#ifdef SOARM_PHASE_PROF
+    if (e < 65536) g_pgs_prof[8 * e + 6] = g_pgs_prof[8 * e + 7] = g_pgs_prof[8 * e] = clock64();
+    PSTAMP(8);
+    PSTAMP(9);  // (no separate warm-start phase: the solve below is stamp 9's phase and "pgs")
+#endif
+    const int nit = newton_solve(S, nr);
+#ifdef SOARM_PHASE_PROF
+    if (e < 65536)
+      g_pgs_prof[8 * e + 1] = clock64(), g_pgs_prof[8 * e + 2] = nit, g_pgs_prof[8 * e + 3] = 0,
+                        g_pgs_prof[8 * e + 4] = nlim, g_pgs_prof[8 * e + 5] = ncon;
+#else
+    (void)nit;
+#endif
     return ncon;
   }
 #ifdef SOARM_PHASE_PROF

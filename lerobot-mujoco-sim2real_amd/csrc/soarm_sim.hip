@@ -415,7 +415,7 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
   __shared__ float s_lim[NA * LF][COLS];
   __shared__ float s_keep[keep_floats<NA, NF>()][COLS];
   // contact list (quad), y-sweep slots; Newton: its line-search rows (8 per LDS contact)
-  __shared__ float s_ext[NF == 1 ? XS_EXT : (lpe<NF>() == 4 ? XS_LIST + (SOL == SIM_SOL_NEWTON ? 8 * LDS_CON : 0) : 1)][COLS];
+  __shared__ float s_ext[NF == 1 ? XS_EXT : (lpe<NF>() == 4 ? XS_LIST + (SOL == SIM_SOL_NEWTON ? 12 * LDS_CON : 0) : 1)][COLS];
   const RowLds L{&s_rows[0][0], &s_lim[0][0], NF == 1 ? &s_keep[0][0] : nullptr, &s_ext[0][0], (int)threadIdx.x,
                  (int)threadIdx.x / lpe<NF>(), COLS};
   const ContactRows<NA, NF> cr{scratch + e, n};
@@ -1489,12 +1489,12 @@ int sim_collide_profile(sim_batch* b, const sim_state* s, double* cycles, void* 
 int sim_phase_profile(double* out, int reset) {
   if (!out) return fail(SIM_E_ARG, "null output");
 #ifdef SOARM_PHASE_PROF
-  unsigned long long h[77], nw[8];
+  unsigned long long h[77], nw[16];
   HIPCHECK(hipDeviceSynchronize());
   HIPCHECK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_phase), sizeof(h)));
   HIPCHECK(hipMemcpyFromSymbol(nw, HIP_SYMBOL(g_newton), sizeof(nw)));
   for (int k = 0; k < 77; k++) out[k] = (double)h[k];
-  for (int k = 0; k < 8; k++) out[77 + k] = (double)nw[k];
+  for (int k = 0; k < 16; k++) out[77 + k] = (double)nw[k];
   if (reset) {
     const unsigned long long z[77] = {};
     HIPCHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof(z)));

@@ -44,7 +44,7 @@ q0 = W.initial_qpos(cm, ids, 0)
 sim.reset(init_qpos=q0[:, :5], extra_qpos=q0, seed=0)
 tab = {k: (torch.as_tensor(v, dtype=torch.float32, device="cuda") if isinstance(v, np.ndarray) else v)
        for k, v in W.chirp_tables(ids, 0).items()}
-out = (ctypes.c_double * 85)()
+out = (ctypes.c_double * 93)()
 res = {}
 every = int(os.environ.get("EVERY", 0))
 starts = set(range(0, T, every)) if every else {0, T // 2, T - 10}
@@ -92,7 +92,10 @@ for t in range(T):
             r["newton"] = {"solves": v[77], "mean_iters": v[78] / v[77], "mean_ls_evals": v[79] / v[77],
                            "coupled_frac": v[80] / v[77], "mean_cycles": v[81] / v[77], "max_cycles": v[82],
                            "max_iters": v[83], "max_ls_evals": v[84],
-                           "solve_frac_of_total": v[81] / max(tot, 1)}
+                           "split": {"arm_iters": v[85] / v[77], "arm_ls": v[86] / v[77],
+                                     "free_iters": v[87] / v[77], "free_ls": v[88] / v[77]},
+                           "wave_mean_max_ls": v[90] / max(v[89], 1), "wave_mean_max_iters": v[91] / max(v[89], 1),
+                           "wave_mean_cycles": v[92] / max(v[89], 1)}
         res[t] = r
         print(t, json.dumps(r), flush=True)
 json.dump(res, open(os.path.join(ROOT, "gpurun_out", f"phase_prof_{os.environ.get('CONFIG', 'contact')}_{os.environ.get('SOLVER', 'PGS').lower()}.json"), "w"), indent=1)
