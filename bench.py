@@ -46,6 +46,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-profile", action="store_true")
     p.add_argument("--no-steady", action="store_true", help="skip the steps 20-120 steady-state window")
+    p.add_argument("--no-other-solver", action="store_true",
+                   help="skip timing the same workload with the other constraint solver (contact configs)")
     p.add_argument("--launcher-check", action="store_true",
                    help="exercise the rank launcher / process group / max-over-ranks timing with an empty "
                         "timed region (no GPU; CPU tests)")
@@ -439,6 +441,54 @@ def main():
         steady = {"window": "env-steps 20-120", "value": value, "ms_per_step": dt / args.steps * 1e3,
                   "note": "= the timed window"}
 
+    # the other constraint solver on the same workload (contact configs): PGS is the configured
+    # solver (BASELINE.json configs[2]); Newton is what the reference's MuJoCo runs by default
+    # (its scene has no <option>), so both numbers are reported -- value is always --solver's
+    other_solver = None
+    if not args.no_other_solver and name in ("contact", "dr"):
+        other = "newton" if args.solver == "pgs" else "pgs"
+        cm2 = W.model(name, solver=other)
+        sim2 = BatchSim(cm2, n, gpu)
+        sim2.reset(init_qpos=q0[:, :5], extra_qpos=q0, seed=args.seed, env_offset=rank * n)
+        if cfg["dr"]:
+            sim2.set_params(**W.dr_params(ids, args.seed))
+        act2 = sim2.action_buffer()
+        gen2 = torch.Generator(device=dev)
+        gen2.manual_seed(args.seed * 1000003 + rank)
+
+        def step2(t):
+            if cfg["action"] == "chirp":
+                act2.copy_(W.chirp_action(tab, float(t), lib=torch))
+            else:
+                torch.rand((n, 5), generator=gen2, device=dev, out=act2)
+                act2.sub_(0.5)
+            sim2.step(act2)
+
+        windows = [(args.warmup, args.steps)] + ([(20, 100)] if steady is not None and (args.warmup, args.steps) != (20, 100) else [])
+        res = {}
+        t = 0
+        for w0, ns in windows:
+            while t < w0:
+                step2(t)
+                t += 1
+            if t > w0:  # the second window starts before the first ended: replay from the reset
+                sim2.reset(init_qpos=q0[:, :5], extra_qpos=q0, seed=args.seed, env_offset=rank * n)
+                gen2.manual_seed(args.seed * 1000003 + rank)
+                t = 0
+                while t < w0:
+                    step2(t)
+                    t += 1
+            sync()
+            ts = time.perf_counter()
+            for _ in range(ns):
+                step2(t)
+                t += 1
+            sync()
+            (dto,) = max_over_ranks(time.perf_counter() - ts)
+            res[f"env-steps {w0}-{w0 + ns}"] = {"value": total_envs * ns / dto, "ms_per_step": dto / ns * 1e3}
+        other_solver = {"solver": other, "windows": res}
+        del sim2, cm2
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(name, args.cpu_seconds, args.seed, args.solver)
@@ -456,6 +506,7 @@ def main():
                                   else "Newton (MuJoCo's default: iterations 100, tol 1e-8, exact line search)"),
                        "parallelism": f"env-sharded x{world} (no per-step collective)"},
             "steady_state": steady,
+            "other_solver": other_solver,
             "dist": {"world_size": world, "backend": (args.dist_backend if world > 1 else None),
                      "launcher": launcher, "rollout_gather_s": gather_s},
             "roofline": roof, "cpu_baseline": cpu,
