@@ -400,7 +400,8 @@ def main():
         traffic = None
         tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(tpath):
-            traffic = json.load(open(tpath)).get(name, {}).get(kind)
+            tr = json.load(open(tpath))
+            traffic = tr.get(name if args.solver == "pgs" else f"{name}_newton", {}).get(kind)
         # 64-lane waves, one lane per env (four per env in k_substep: quad mode, soarm_pgs.h
         # lpe()): the kernel can occupy at most that many of the chip's 1024 SIMDs; the VALU
         # peak those SIMDs can issue bounds it first

@@ -64,6 +64,11 @@ class KoopmanMPCTracking:
     def runFunc(self):
         """One frame: gravity compensation, MPC, env.step (Koopman_MPC.py:110-136, 197-222)."""
         k = self.traj_index
+        if k >= self.total_frames:
+            # the reference switches to its hold / return-home playback here (Koopman_MPC.py:148-183),
+            # which is out of scope (DESIGN.md section 9)
+            raise IndexError(f"runFunc: frame {k} is past the trajectory's {self.total_frames} frames "
+                             "(return-home playback is not built)")
         self.sim.bias(out=self.sim.qfrc_applied)
         self.ctl.step(self.state, self.ff[k], self.u_prev, self.action)
         self.state = self.sim.step(self.action)

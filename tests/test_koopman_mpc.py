@@ -277,6 +277,9 @@ def test_tracking_loop_matches_oracle(gpu_lib, arm_model):
         q = run.sim.qpos[:6, 3].double().cpu().numpy()
         assert json.loads(sent.msgs[-1]) == real_targets(q) and len(sent.msgs) == k + 1
     assert int(run.sim.status.abs().sum()) == 0
+    # past the last frame the reference plays back its return-home path (out of scope): a clear error
+    with pytest.raises(IndexError, match="past the trajectory"):
+        run.runFunc()
 
 
 class _Sink:

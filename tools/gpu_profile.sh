@@ -25,17 +25,22 @@ if [ "$2" != "--no-tests" ]; then
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
 fi
 step bench_contact 600 python bench.py > $O/bench_contact.json 2> $O/bench_contact.err
+step bench_contact_newton 600 python bench.py --solver newton --no-cpu-baseline > $O/bench_contact_newton.json 2> $O/bench_contact_newton.err
+step bench_driver 300 python bench.py --steps 20 --warmup 5 > $O/bench_contact_steps20_warmup5.json 2> $O/bench_contact_drv.err
 step bench_nocontact 300 python bench.py --config nocontact --steps 200 --warmup 20 --cpu-seconds 8 > $O/bench_nocontact.json 2> $O/bench_nocontact.err
 step bench_dr 600 python bench.py --config dr --steps 50 --warmup 5 --cpu-seconds 8 > $O/bench_dr.json 2> $O/bench_dr.err
 step bench_rollout 600 python bench.py --config rollout --steps 100 --warmup 5 --cpu-seconds 8 > $O/bench_rollout.json 2> $O/bench_rollout.err
 step bench_mpc 600 python bench.py --config mpc --cpu-seconds 8 > $O/bench_mpc.json 2> $O/bench_mpc.err
 KRE="k_substep|k_collide|k_step|k_geom|k_mpc_step|k_bias"
 cd /tmp
-for C in contact mpc; do
-  P=$O/prof_${TAG}_$C
-  step trace_$C 600 rocprofv3 --kernel-trace --stats -f csv -d $P -o trace -- python3 $R/bench.py --config $C --no-cpu-baseline > $O/bench_${C}_traced.json
-  step pmc_fetch_$C 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$KRE" -f csv -d $P -o pmc_fetch -- python3 $R/bench.py --config $C --steps 10 --warmup 2 --no-cpu-baseline --no-profile
-  step pmc_write_$C 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$KRE" -f csv -d $P -o pmc_write -- python3 $R/bench.py --config $C --steps 10 --warmup 2 --no-cpu-baseline --no-profile
-  step pmc_sq_$C 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY --kernel-include-regex "$KRE" -f csv -d $P -o pmc_sq -- python3 $R/bench.py --config $C --steps 10 --warmup 2 --no-cpu-baseline --no-profile
+for SPEC in contact:contact: contact_newton:contact:--solver_newton mpc:mpc:; do
+  IFS=: read TAGC C EXTRA <<< "$SPEC"
+  EXTRA=${EXTRA//_/ }
+  P=$O/prof_${TAG}_$TAGC
+  step trace_$TAGC 600 rocprofv3 --kernel-trace --stats -f csv -d $P -o trace -- python3 $R/bench.py --config $C $EXTRA --no-cpu-baseline > $O/bench_${TAGC}_traced.json
+  NP="--steps 10 --warmup 2 --no-cpu-baseline --no-profile --no-steady --no-other-solver"
+  step pmc_fetch_$TAGC 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$KRE" -f csv -d $P -o pmc_fetch -- python3 $R/bench.py --config $C $EXTRA $NP
+  step pmc_write_$TAGC 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$KRE" -f csv -d $P -o pmc_write -- python3 $R/bench.py --config $C $EXTRA $NP
+  step pmc_sq_$TAGC 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY --kernel-include-regex "$KRE" -f csv -d $P -o pmc_sq -- python3 $R/bench.py --config $C $EXTRA $NP
 done
 ls -R $O/prof_${TAG}_contact | head -20
