@@ -396,12 +396,32 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
                                                 const float* __restrict__ cbuf,
                                                 const int* __restrict__ ccount,
                                                 uint32_t* __restrict__ pmask,
-                                                float* __restrict__ gpose) {
+                                                float* __restrict__ gpose, const float* gpose_in) {
   // lpe<NF>() lanes per env (soarm_pgs.h): they run the same per-env code
   const int e = blockIdx.x * (64 / lpe<NF>()) + (int)threadIdx.x / lpe<NF>();
   if (e >= n) return;
   PHASE_T(t0);
   const DModel& m = *dm;
+#ifdef SOARM_FUSE_COLLIDE
+  // experiment: mj_collision of this env on its own lanes (pairs split over the
+  // quad) instead of the (env, pair)-parallel k_collide launch before this one
+  if (ccount != nullptr) {
+    for (int p = (int)threadIdx.x % lpe<NF>(); p < m.npair; p += lpe<NF>()) {
+      GeomPose P1, P2;
+      load_pose(gpose_in, n, e, m.pair_geom1[p], P1);
+      load_pose(gpose_in, n, e, m.pair_geom2[p], P2);
+      PairOut o{const_cast<float*>(cbuf), n, e, m.pair_slot[p], m.pair_cap[p], 0};
+      collide_pair(m, p, P1, P2, o);
+      soa(const_cast<int*>(ccount), p, n, e) = o.n;
+      if (o.n > 0) {
+        atomicOr(&pmask[(size_t)(p >> 5) * n + e], 1u << (p & 31));
+        const int cq = m.pair_cq[p];
+        if (cq >= 0) atomicOr(&pmask[(size_t)((m.npair + 31) >> 5) * n + e], (uint32_t)(o.n - 1) << (2 * cq));
+      }
+    }
+    __threadfence_block();
+  }
+#endif
   Sim<NA, NF> S(dm, pp.mass_scale ? pp.mass_scale[e] : 1.f, pp.friction ? pp.friction[e] : -1.f,
                 pp.damping_scale ? pp.damping_scale[e] : 1.f);
   load_state(S, st, n, e);
@@ -1370,12 +1390,14 @@ int sim_step(sim_batch* b, const sim_state* s, const float* action, int frame_sk
       }
       prof_mark(b, -1, q);
       for (int sub = 0; sub < frame_skip; sub++) {
+#ifndef SOARM_FUSE_COLLIDE
         if (np > 0) {
           prof_mark(b, 1, q);
           const TraceRange tr_("collide");
           launch_collide(b, q, nullptr);
           prof_mark(b, -1, q);
         }
+#endif
         const bool last = sub == frame_skip - 1;
         const TraceRange tr_("substep");
         prof_mark(b, 2, q);
@@ -1384,7 +1406,7 @@ int sim_step(sim_batch* b, const sim_state* s, const float* action, int frame_sk
                            b->d_model, b->n, *s,
                            sub == 0 ? action : nullptr, last ? obs : nullptr, b->params, b->d_scratch,
                            b->d_cbuf, np > 0 ? b->d_ccount : nullptr, np > 0 ? b->d_pmask : nullptr,
-                           last ? nullptr : b->d_gpose);
+                           last ? nullptr : b->d_gpose, b->d_gpose);
         prof_mark(b, -1, q);
       }
      });
