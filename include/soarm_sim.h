@@ -278,12 +278,12 @@ int sim_contacts(sim_batch* b, const sim_state* s, float* out, int32_t* ncon, vo
 int sim_collide_profile(sim_batch* b, const sim_state* s, double* cycles, void* stream);
 
 /* diagnostic: summed wave cycles per phase of the contact substep kernel in a
-   build compiled with -DSOARM_PHASE_PROF (out[93]; the first 19: load, smooth dynamics, rows,
+   build compiled with -DSOARM_PHASE_PROF (out[101]; the first 19: load, smooth dynamics, rows,
    PGS, integrate+output, waves, sum of PGS sweeps over envs, envs, max wave
    cycles, waves on the register fast path, max wave PGS cycles, sum of per-wave
    max sweeps, waves with an active limit / a non-block contact / contact
    overflow past LDS, max contacts per env; then the rows phase split: contact rows,
-   warm start + cost, register-block setup; the rest to 77: see g_phase in soarm_sim.hip; 77..92:
+   warm start + cost, register-block setup; the rest to 77: see g_phase in soarm_sim.hip; 77..100:
    the Newton solver's counters, g_newton in soarm_newton.h);
    returns SIM_E_ARG in a regular build. */
 int sim_phase_profile(double* out, int reset);

@@ -37,13 +37,24 @@ namespace soarm {
 // solve cycles, [6] max iterations, [7] max line-search evaluations of one solve; split solves
 // (per env): [8] arm iterations, [9] arm evaluations, [10] free-body iterations, [11] free-body
 // evaluations; per wave: [12] waves, [13] sum over waves of the wave's max evaluations, [14] of
-// its max iterations, [15] sum of wave solve cycles (lane 0)
-__device__ unsigned long long g_newton[16];
+// its max iterations, [15] sum of the wave's max solve cycles; per env (sum over both ranges):
+// [16] warm-start cycles, [17] Hessian + factor + solve cycles, [18] line-search cycles,
+// [19] cycles of the pass at the new point, [20] wave-max sum of [16], [21] of [17], [22] of [18],
+// [23] of [19]
+__device__ unsigned long long g_newton[24];
+#define NT_STAMP(k)                          \
+  {                                          \
+    const long long t_ = clock64();          \
+    ncyc[k] += t_ - nt_;                     \
+    nt_ = t_;                                \
+  }
 DEVI int wave_max_i(int v) {
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) v = max(v, __shfl_xor(v, o));
   return v;
 }
+#else
+#define NT_STAMP(k)
 #endif
 
 template <int NA, int NF, bool CON>
@@ -243,8 +254,27 @@ struct NewtonRows {
   // per contact; written and read by the lane that owns the contact)
   static constexpr int LS_STRIDE = 12;
   static_assert(XS_LIST + LS_STRIDE * LDS_CON <= XS_EXT, "line-search scratch fits the ext area");
+  // per frictionloss row along p (registers): residual at a, the step lengths of its two kinks
+  // (x = -R fl, x = R fl; +inf when p_i = 0 or fl = 0) and p_i / R_i
+  struct FricLS {
+    float x0[NA], k1[NA], k2[NA], piR[NA];
+  };
   template <int LO, int HI>
-  DEVI void ls_setup(const float a[NV], const float p[NV]) const {
+  DEVI void ls_setup(const float a[NV], const float p[NV], FricLS& fr) const {
+    if constexpr (LO == 0) {
+#pragma unroll
+      for (int i = 0; i < NA; i++) {
+        const float fl = m.dof_frictionloss[i], R = fR[i], x0 = a[i] - fa[i];
+        const bool live = fl > 0.f && p[i] != 0.f;
+        const float rp = 1.f / p[i];
+        fr.x0[i] = x0;
+        fr.k1[i] = live ? (-R * fl - x0) * rp : 3.0e38f;
+        fr.k2[i] = live ? (R * fl - x0) * rp : 3.0e38f;
+        fr.piR[i] = p[i] / R;
+      }
+    } else {
+      (void)fr;
+    }
     if constexpr (CON) {
       for (int c = ql(); c < nl; c += QL) {
         if (!owns<LO, HI>((int)L.at(c, F_FLAGS))) continue;
@@ -281,8 +311,8 @@ struct NewtonRows {
   // part: caller), and the piece [bl, br] of the piecewise-quadratic line cost that alpha lies in
   // (the nearest kinks at or below / above alpha): d/dalpha is linear there
   template <int LO, int HI>
-  DEVI void ls_eval(const float a[NV], const float p[NV], float al, float& d1, float& d2, float& bl,
-                    float& br) const {
+  DEVI void ls_eval(const float a[NV], const float p[NV], const FricLS& fr, float al, float& d1, float& d2,
+                    float& bl, float& br) const {
     auto kink = [&](float t, float& l, float& r) {
       r = t > al ? fminf(r, t) : r;
       l = t <= al ? fmaxf(l, t) : l;
@@ -316,18 +346,16 @@ struct NewtonRows {
       d1 += c1, d2 += c2, bl = fmaxf(bl, cl), br = fminf(br, cr_);
     }
     if constexpr (LO == 0) {
+      // frictionloss rows: d/dalpha of the Huber cost is x p / R inside |x| < R fl, +-fl p outside
 #pragma unroll
       for (int i = 0; i < NA; i++) {
-        const float fl = m.dof_frictionloss[i], R = fR[i];
-        const float x0 = a[i] - fa[i], x = fmaf(al, p[i], x0);
-        const float f = x <= -R * fl ? fl : (x >= R * fl ? -fl : -x / R);
-        d1 -= f * p[i];
-        d2 += (x > -R * fl && x < R * fl && fl > 0.f) ? p[i] * p[i] / R : 0.f;
-        if (fl > 0.f && p[i] != 0.f) {
-          const float rp = __builtin_amdgcn_rcpf(p[i]);
-          kink((R * fl - x0) * rp, bl, br);
-          kink((-R * fl - x0) * rp, bl, br);
-        }
+        const float fl = m.dof_frictionloss[i], x = fmaf(al, p[i], fr.x0[i]);
+        const bool in = fabsf(x) < fR[i] * fl;
+        const float flp = fl * p[i];
+        d1 += in ? x * fr.piR[i] : (x < 0.f ? -flp : flp);
+        d2 += in ? p[i] * fr.piR[i] : 0.f;
+        kink(fr.k1[i], bl, br);
+        kink(fr.k2[i], bl, br);
       }
       for (int l = 0; l < nlim; l++) {
         const int d = (int)L.lm(l, L_DOF);
@@ -365,7 +393,13 @@ DEVI void mul_m(const Sim<NA, NF>& S, const float x[], float y[]) {
 // Newton on the subsystem over dofs [LO, HI): a[] (all dofs; only this range moves) in/out,
 // jtf[LO..HI) = J' f at the result.  Returns the iteration count.
 template <int LO, int HI, int NA, int NF, bool CON>
-DEVI int newton_range(const Sim<NA, NF>& S, const NewtonRows<NA, NF, CON>& R, float a[], float jtf[], int& nls) {
+DEVI int newton_range(const Sim<NA, NF>& S, const NewtonRows<NA, NF, CON>& R, float a[], float jtf[], int& nls,
+                      long long* ncyc) {
+#ifdef SOARM_PHASE_PROF
+  long long nt_ = clock64();
+#else
+  (void)ncyc;
+#endif
   constexpr int NV = NA + 6 * NF, NR = HI - LO, NH = NR * (NR + 1) / 2;
   const DModel& m = *S.mp;
   const float scale = m.pgs_scale, tol = m.tolerance;
@@ -401,6 +435,7 @@ DEVI int newton_range(const Sim<NA, NF>& S, const NewtonRows<NA, NF, CON>& R, fl
       cost = R.template pass<LO, HI, true>(a, jtf, H, sig);
     }
   }
+  NT_STAMP(0);
   int it = 0;
   for (; it < m.iterations; it++) {
     float g[NV], gn = 0.f;
@@ -431,6 +466,7 @@ DEVI int newton_range(const Sim<NA, NF>& S, const NewtonRows<NA, NF, CON>& R, fl
     // the 1-D Newton target is the exact minimiser when it lies in that piece (usually the first
     // evaluation), else it moves the bracket and the next point is that target, or the secant
     // of the bracket when the target leaves it.  phi'(0) = g'p needs no evaluation.
+    NT_STAMP(1);
     float Mp[NV], g0 = 0.f, pMp = 0.f, dz = 0.f;
     mul_m<LO, HI>(S, p, Mp);
 #pragma unroll
@@ -440,13 +476,15 @@ DEVI int newton_range(const Sim<NA, NF>& S, const NewtonRows<NA, NF, CON>& R, fl
       dz = fmaf(g[i], p[i], dz);
     }
     if (!(dz < 0.f)) break;  // not a descent direction at fp32 resolution: converged
-    R.template ls_setup<LO, HI>(a, p);
+    typename NewtonRows<NA, NF, CON>::FricLS fr;
+    R.template ls_setup<LO, HI>(a, p, fr);
     float lo = 0.f, dlo = dz, hi = 3.0e38f, dhi = 0.f, al = 1.f;
     for (int ls = 0; ls < 24; ls++) {
       nls++;
       float d1 = fmaf(al, pMp, g0), d2 = pMp, bl = -3.0e38f, br = 3.0e38f;
-      R.template ls_eval<LO, HI>(a, p, al, d1, d2, bl, br);
-      float an = al - d1 / d2;
+      R.template ls_eval<LO, HI>(a, p, fr, al, d1, d2, bl, br);
+      // (the target within its piece is exact up to rounding: the approximate reciprocal suffices)
+      float an = al - d1 * __builtin_amdgcn_rcpf(d2);
       if (an >= bl && an <= br) {
         al = an;
         break;
@@ -459,6 +497,7 @@ DEVI int newton_range(const Sim<NA, NF>& S, const NewtonRows<NA, NF, CON>& R, fl
       if (!(an > lo && an < hi)) break;  // bracket exhausted at fp32 resolution
       al = an;
     }
+    NT_STAMP(2);
     float an_[NV], jn[NV], Man[NV];
 #pragma unroll
     for (int i = 0; i < NV; i++) an_[i] = fmaf(al, p[i], a[i]);
@@ -466,6 +505,7 @@ DEVI int newton_range(const Sim<NA, NF>& S, const NewtonRows<NA, NF, CON>& R, fl
     for (int i = 0; i < NH; i++) H[i] = 0.f;
     const uint32_t sig0 = sig;
     const float cn = gauss(an_, Man) + R.template pass<LO, HI, true>(an_, jn, H, sig);
+    NT_STAMP(3);
     if (!(cn <= cost + 1e-5f * fabsf(cost))) break;  // a real increase (numerical trouble): keep a
 #pragma unroll
     for (int i = LO; i < HI; i++) a[i] = an_[i], jtf[i] = jn[i], Ma[i] = Man[i];
@@ -503,48 +543,56 @@ DEVI int newton_solve(Sim<NA, NF>& S, const NewtonRows<NA, NF, CON>& R) {
       coupled |= __any(c < R.nl && (int)R.L.at(c < R.nl ? c : 0, F_FLAGS) == (TOUCH_ARM | TOUCH_FREE));
   }
   int it, nls = 0;
+  long long ncyc[4] = {0, 0, 0, 0};
 #ifdef SOARM_PHASE_PROF
   const long long t0 = clock64();
+  int it_arm = 0, nls_arm = 0;
 #endif
   if constexpr (NF == 0) {
-    it = newton_range<0, NV>(S, R, a, jtf, nls);
+    it = newton_range<0, NV>(S, R, a, jtf, nls, ncyc);
   } else {
     if (coupled) {
-      it = newton_range<0, NV>(S, R, a, jtf, nls);
+      it = newton_range<0, NV>(S, R, a, jtf, nls, ncyc);
     } else {
-      it = newton_range<0, NA>(S, R, a, jtf, nls);
+      it = newton_range<0, NA>(S, R, a, jtf, nls, ncyc);
 #ifdef SOARM_PHASE_PROF
-      const int it_arm = it, nls_arm = nls;
+      it_arm = it, nls_arm = nls;
 #endif
-      it += newton_range<NA, NV>(S, R, a, jtf, nls);
-#ifdef SOARM_PHASE_PROF
-      if ((threadIdx.x & (lpe<NF>() - 1)) == 0) {
-        atomicAdd(&g_newton[8], (unsigned long long)it_arm);
-        atomicAdd(&g_newton[9], (unsigned long long)nls_arm);
-        atomicAdd(&g_newton[10], (unsigned long long)(it - it_arm));
-        atomicAdd(&g_newton[11], (unsigned long long)(nls - nls_arm));
-      }
-#endif
+      it += newton_range<NA, NV>(S, R, a, jtf, nls, ncyc);
     }
   }
 #ifdef SOARM_PHASE_PROF
-  if ((threadIdx.x & (lpe<NF>() - 1)) == 0) {
-    const unsigned long long dt = (unsigned long long)(clock64() - t0);
-    atomicAdd(&g_newton[0], 1ull);
-    atomicAdd(&g_newton[1], (unsigned long long)it);
-    atomicAdd(&g_newton[2], (unsigned long long)nls);
-    atomicAdd(&g_newton[3], (unsigned long long)coupled);
-    atomicAdd(&g_newton[4], dt);
-    atomicMax(&g_newton[5], dt);
-    atomicMax(&g_newton[6], (unsigned long long)it);
-    atomicMax(&g_newton[7], (unsigned long long)nls);
-  }
-  const int wl = wave_max_i(nls), wi = wave_max_i(it);
-  if ((threadIdx.x & 63) == 0) {
-    atomicAdd(&g_newton[12], 1ull);
-    atomicAdd(&g_newton[13], (unsigned long long)wl);
-    atomicAdd(&g_newton[14], (unsigned long long)wi);
-    atomicAdd(&g_newton[15], (unsigned long long)(clock64() - t0));
+  {
+    // reduced over the wave first (one lane per env counts), then one atomic per counter and
+    // wave: per-env atomics on shared counters serialise in L2 and stall the waves being measured
+    const long long dt = clock64() - t0;
+    const bool one = (threadIdx.x & (lpe<NF>() - 1)) == 0;
+    auto wsum = [](double v) {
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) v += __shfl_xor(v, o);
+      return v;
+    };
+    const double sv[16] = {1.0, (double)it, (double)nls, (double)coupled, (double)dt, (double)it_arm,
+                           (double)nls_arm, (double)(it - it_arm), (double)(nls - nls_arm),
+                           (double)ncyc[0], (double)ncyc[1], (double)ncyc[2], (double)ncyc[3], 0.0, 0.0, 0.0};
+    const int sk[13] = {0, 1, 2, 3, 4, 8, 9, 10, 11, 16, 17, 18, 19};
+    for (int k = 0; k < 13; k++) {
+      const double w = wsum(one ? sv[k] : 0.0);
+      if ((threadIdx.x & 63) == 0) atomicAdd(&g_newton[sk[k]], (unsigned long long)w);
+    }
+    const int mx[4] = {wave_max_i((int)dt), wave_max_i(it), wave_max_i(nls), 0};
+    const int wc[4] = {wave_max_i((int)ncyc[0]), wave_max_i((int)ncyc[1]), wave_max_i((int)ncyc[2]),
+                       wave_max_i((int)ncyc[3])};
+    if ((threadIdx.x & 63) == 0) {
+      atomicMax(&g_newton[5], (unsigned long long)mx[0]);
+      atomicMax(&g_newton[6], (unsigned long long)mx[1]);
+      atomicMax(&g_newton[7], (unsigned long long)mx[2]);
+      atomicAdd(&g_newton[12], 1ull);
+      atomicAdd(&g_newton[13], (unsigned long long)mx[2]);
+      atomicAdd(&g_newton[14], (unsigned long long)mx[1]);
+      atomicAdd(&g_newton[15], (unsigned long long)mx[0]);
+      for (int k = 0; k < 4; k++) atomicAdd(&g_newton[20 + k], (unsigned long long)wc[k]);
+    }
   }
 #endif
 #pragma unroll

@@ -1511,12 +1511,12 @@ int sim_collide_profile(sim_batch* b, const sim_state* s, double* cycles, void* 
 int sim_phase_profile(double* out, int reset) {
   if (!out) return fail(SIM_E_ARG, "null output");
 #ifdef SOARM_PHASE_PROF
-  unsigned long long h[77], nw[16];
+  unsigned long long h[77], nw[24];
   HIPCHECK(hipDeviceSynchronize());
   HIPCHECK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_phase), sizeof(h)));
   HIPCHECK(hipMemcpyFromSymbol(nw, HIP_SYMBOL(g_newton), sizeof(nw)));
   for (int k = 0; k < 77; k++) out[k] = (double)h[k];
-  for (int k = 0; k < 16; k++) out[77 + k] = (double)nw[k];
+  for (int k = 0; k < 24; k++) out[77 + k] = (double)nw[k];
   if (reset) {
     const unsigned long long z[77] = {};
     HIPCHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof(z)));

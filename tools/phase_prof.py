@@ -44,7 +44,7 @@ q0 = W.initial_qpos(cm, ids, 0)
 sim.reset(init_qpos=q0[:, :5], extra_qpos=q0, seed=0)
 tab = {k: (torch.as_tensor(v, dtype=torch.float32, device="cuda") if isinstance(v, np.ndarray) else v)
        for k, v in W.chirp_tables(ids, 0).items()}
-out = (ctypes.c_double * 93)()
+out = (ctypes.c_double * 101)()
 res = {}
 every = int(os.environ.get("EVERY", 0))
 starts = set(range(0, T, every)) if every else {0, T // 2, T - 10}
@@ -95,7 +95,9 @@ for t in range(T):
                            "split": {"arm_iters": v[85] / v[77], "arm_ls": v[86] / v[77],
                                      "free_iters": v[87] / v[77], "free_ls": v[88] / v[77]},
                            "wave_mean_max_ls": v[90] / max(v[89], 1), "wave_mean_max_iters": v[91] / max(v[89], 1),
-                           "wave_mean_cycles": v[92] / max(v[89], 1)}
+                           "wave_mean_cycles": v[92] / max(v[89], 1),
+                           "split_cycles_per_env": {k: v[93 + i] / v[77] for i, k in enumerate(["warm", "hessian+factor", "line_search", "new_point_pass"])},
+                           "split_cycles_wave_max": {k: v[97 + i] / max(v[89], 1) for i, k in enumerate(["warm", "hessian+factor", "line_search", "new_point_pass"])}}
         res[t] = r
         print(t, json.dumps(r), flush=True)
 json.dump(res, open(os.path.join(ROOT, "gpurun_out", f"phase_prof_{os.environ.get('CONFIG', 'contact')}_{os.environ.get('SOLVER', 'PGS').lower()}.json"), "w"), indent=1)
