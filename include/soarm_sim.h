@@ -228,6 +228,16 @@ int sim_model_create(const sim_model_desc* desc, const float* hull_vert, const i
 /* frees the model and its device copies; every batch of the model must be freed first */
 void sim_model_free(sim_model* m);
 
+/* Compiled-model files, the MjModel.from_xml_path (SOARM101_Env.py:34) of a C / C++ caller with no
+   Python at run time: mjcf.py compiles the MJCF once (CompiledModel.save) and writes the desc and
+   hull arrays; sim_model_load reads them back and calls sim_model_create.  Format (little endian):
+   "SOARMMDL" | u32 version (1) | u32 sizeof(sim_model_desc) | desc | f32 hull_vert[nhullvert][3] |
+   i32 hull_adr[nhullvert+1] (absent when nhullvert = 0) | i32 hull_adj[nhulladj].  A file of
+   another version or desc size, or a short file, is rejected (SIM_E_ARG). */
+int sim_model_save(const sim_model_desc* desc, const float* hull_vert, const int32_t* hull_adr,
+                   const int32_t* hull_adj, const char* path);
+int sim_model_load(const char* path, sim_model** out);
+
 /* replaces MjData(model) for n_envs envs on `device` (HIP ordinal).  The model's
    read-only device data (constants, hull records, support LUT) is uploaded by the
    first batch on a device and shared by the model's later batches there. */

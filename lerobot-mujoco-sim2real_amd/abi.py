@@ -120,6 +120,7 @@ EXPORTS = [
     "sim_batch_create", "sim_batch_free", "sim_batch_set_params", "sim_reset",
     "sim_step", "sim_substeps", "sim_bias", "sim_observe", "sim_contacts", "sim_collide_profile", "sim_phase_profile", "sim_ik_dls",
     "sim_profile_begin", "sim_profile_end", "sim_rand_uniform", "sim_ik_dls_pose",
+    "sim_model_save", "sim_model_load",
     # include/koopman_mpc.h
     "sim_koopman_create", "sim_koopman_free", "sim_koopman_encode", "sim_koopman_feedforward",
     "sim_koopman_mpc_step",
@@ -145,6 +146,8 @@ def load_lib(path=None):
     lib.sim_model_create.argtypes = [C.POINTER(ModelDesc), vp, vp, vp, C.POINTER(vp)]
     lib.sim_model_free.argtypes = [vp]
     lib.sim_model_free.restype = None
+    lib.sim_model_save.argtypes = [C.POINTER(ModelDesc), vp, vp, vp, C.c_char_p]
+    lib.sim_model_load.argtypes = [C.c_char_p, C.POINTER(vp)]
     lib.sim_batch_create.argtypes = [vp, ip, ip, C.POINTER(vp)]
     lib.sim_batch_free.argtypes = [vp]
     lib.sim_batch_free.restype = None

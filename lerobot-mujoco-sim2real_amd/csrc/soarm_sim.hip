@@ -15,6 +15,7 @@
 #include <type_traits>
 #include <mutex>
 #include <thread>
+#include <vector>
 #include <dlfcn.h>
 #include <sched.h>
 #include <vector>
@@ -504,6 +505,8 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
     S.kinematics();
     PSTAMP(14);
     write_geom_poses(S, gpose, n, e, (int)threadIdx.x % lpe<NF>(), lpe<NF>());
+  } else {
+    PSTAMP(14);  // (the last substep writes no poses: both phases empty)
   }
 #ifdef SOARM_PHASE_PROF
   PHASE_T(t5);
@@ -1272,6 +1275,64 @@ int sim_model_create(const sim_model_desc* desc, const float* hull_vert, const i
   }
   *out = M;
   return SIM_OK;
+}
+
+// compiled-model files (soarm_sim.h): the desc and hull arrays as sim_model_create takes them
+static const char kModelMagic[8] = {'S', 'O', 'A', 'R', 'M', 'M', 'D', 'L'};
+static const uint32_t kModelVersion = 1;
+
+int sim_model_save(const sim_model_desc* desc, const float* hull_vert, const int32_t* hull_adr,
+                   const int32_t* hull_adj, const char* path) {
+  if (!desc || !path) return fail(SIM_E_ARG, "null argument");
+  if (desc->nhullvert < 0 || desc->nhulladj < 0) return fail(SIM_E_ARG, "bad hull sizes");
+  if (desc->nhullvert > 0 && (!hull_vert || !hull_adr || !hull_adj)) return fail(SIM_E_ARG, "hull arrays missing");
+  FILE* f = fopen(path, "wb");
+  if (!f) return fail(SIM_E_ARG, "cannot open model file for writing");
+  const uint32_t hdr[2] = {kModelVersion, (uint32_t)sizeof(sim_model_desc)};
+  bool ok = fwrite(kModelMagic, 1, 8, f) == 8 && fwrite(hdr, sizeof(uint32_t), 2, f) == 2 &&
+            fwrite(desc, sizeof(sim_model_desc), 1, f) == 1;
+  if (ok && desc->nhullvert > 0)
+    ok = fwrite(hull_vert, sizeof(float), 3 * (size_t)desc->nhullvert, f) == 3 * (size_t)desc->nhullvert &&
+         fwrite(hull_adr, sizeof(int32_t), (size_t)desc->nhullvert + 1, f) == (size_t)desc->nhullvert + 1 &&
+         fwrite(hull_adj, sizeof(int32_t), (size_t)desc->nhulladj, f) == (size_t)desc->nhulladj;
+  ok = (fclose(f) == 0) && ok;
+  return ok ? SIM_OK : fail(SIM_E_ARG, "model file write failed");
+}
+
+int sim_model_load(const char* path, sim_model** out) {
+  if (!path || !out) return fail(SIM_E_ARG, "null argument");
+  *out = nullptr;
+  FILE* f = fopen(path, "rb");
+  if (!f) return fail(SIM_E_ARG, "cannot open model file");
+  char magic[8];
+  uint32_t hdr[2];
+  sim_model_desc d;
+  if (fread(magic, 1, 8, f) != 8 || memcmp(magic, kModelMagic, 8) != 0 || fread(hdr, sizeof(uint32_t), 2, f) != 2) {
+    fclose(f);
+    return fail(SIM_E_ARG, "not a compiled SO-ARM101 model file");
+  }
+  if (hdr[0] != kModelVersion || hdr[1] != sizeof(sim_model_desc)) {
+    fclose(f);
+    return fail(SIM_E_ARG, "model file version / layout does not match this library");
+  }
+  if (fread(&d, sizeof(d), 1, f) != 1 || d.nhullvert < 0 || d.nhulladj < 0 || d.nhullvert > (1 << 24) ||
+      d.nhulladj > (1 << 26)) {
+    fclose(f);
+    return fail(SIM_E_ARG, "model file truncated or corrupt");
+  }
+  std::vector<float> hv(3 * (size_t)d.nhullvert);
+  std::vector<int32_t> ha(d.nhullvert > 0 ? (size_t)d.nhullvert + 1 : 0), hj((size_t)d.nhulladj);
+  bool ok = true;
+  if (d.nhullvert > 0)
+    ok = fread(hv.data(), sizeof(float), hv.size(), f) == hv.size() &&
+         fread(ha.data(), sizeof(int32_t), ha.size(), f) == ha.size() &&
+         fread(hj.data(), sizeof(int32_t), hj.size(), f) == hj.size();
+  char extra;
+  ok = ok && fread(&extra, 1, 1, f) == 0;  // nothing after the arrays
+  fclose(f);
+  if (!ok) return fail(SIM_E_ARG, "model file truncated or corrupt");
+  return sim_model_create(&d, d.nhullvert ? hv.data() : nullptr, d.nhullvert ? ha.data() : nullptr,
+                          d.nhullvert ? hj.data() : nullptr, out);
 }
 
 void sim_model_free(sim_model* m) { delete m; }

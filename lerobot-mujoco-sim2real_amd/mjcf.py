@@ -210,6 +210,20 @@ class CompiledModel:
         self.hull_adj = np.zeros(0, np.int32)
         self.source = None
 
+    def save(self, path):
+        """Write the compiled model file `sim_model_load` reads (include/soarm_sim.h): a C / C++
+        caller then loads the model with no Python at run time (SOARM101_Env.py:34's
+        MjModel.from_xml_path).  Names and keyframes are not part of the file."""
+        import ctypes as C
+
+        lib = abi.load_lib()
+        hv = np.ascontiguousarray(self.hull_vert, np.float32)
+        ha = np.ascontiguousarray(self.hull_adr, np.int32)
+        hj = np.ascontiguousarray(self.hull_adj, np.int32)
+        abi.check(lib, lib.sim_model_save(C.byref(self.desc), hv.ctypes.data_as(C.c_void_p),
+                                          ha.ctypes.data_as(C.c_void_p), hj.ctypes.data_as(C.c_void_p),
+                                          os.fsencode(path)))
+
     # name lookup (mj_name2id equivalents)
     def body(self, name):
         return self.body_names.index(name)

@@ -9,6 +9,7 @@ is asynchronous on torch's current stream; nothing here falls back to a CPU
 path — if the HIP library or the GPU is missing, construction raises.
 """
 import ctypes as C
+import os
 
 import numpy as np
 
@@ -72,6 +73,15 @@ class SimModel:
             self._hadj.ctypes.data_as(C.c_void_p), C.byref(self.ptr)))
 
     @classmethod
+    def from_file(cls, path, lib):
+        """A handle loaded from a compiled model file (`sim_model_load`; CompiledModel.save)."""
+        h = cls.__new__(cls)
+        h.lib, h.key = lib, None
+        h.ptr = C.c_void_p()
+        abi.check(lib, lib.sim_model_load(os.fsencode(path), C.byref(h.ptr)))
+        return h
+
+    @classmethod
     def of(cls, cm, lib):
         """The cached handle of `cm` (rebuilt if its desc was edited since)."""
         h = getattr(cm, "_sim_model", None)
@@ -92,7 +102,9 @@ class SimModel:
 class BatchSim:
     """`n_envs` SO-ARM101 environments stepped in lockstep on one GPU."""
 
-    def __init__(self, model=None, n_envs=1, device=0, **compile_kw):
+    def __init__(self, model=None, n_envs=1, device=0, model_handle=None, **compile_kw):
+        """model: a CompiledModel (sizes, names); model_handle: a SimModel to run instead of the
+        model's own (e.g. SimModel.from_file of the same model's saved file)."""
         import torch
 
         if not torch.cuda.is_available():
@@ -106,7 +118,7 @@ class BatchSim:
         self.nq, self.nv, self.nu = d.nq, d.nv, d.nu
         self.nact, self.obs_dim = d.nact, 3 + d.obs_nq
         self.frame_skip = max(1, int(round(0.02 / d.timestep)))
-        self._handle = SimModel.of(self.cm, self.lib)  # shared; kept alive by this batch
+        self._handle = model_handle if model_handle is not None else SimModel.of(self.cm, self.lib)  # kept alive by this batch
         self._model = self._handle.ptr
         self._batch = C.c_void_p()
         abi.check(self.lib, self.lib.sim_batch_create(self._model, self.n, device, C.byref(self._batch)))

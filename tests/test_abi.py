@@ -52,6 +52,43 @@ def test_no_device_fails_loudly():
     lib.sim_model_free(model)
 
 
+def test_model_file_round_trip_and_rejects(tmp_path):
+    """sim_model_save / sim_model_load (the C caller's MjModel.from_xml_path): a saved model
+    loads (sim_model_create runs on the host: no GPU needed); wrong magic, version, layout or a
+    truncated / padded file are rejected with SIM_E_ARG."""
+    import numpy as np
+    import soarm_pkg  # noqa: F401
+    from lerobot_mujoco_sim2real_amd import mjcf
+    cm = mjcf.compile_mjcf(mjcf.SCENE_XML)
+    lib = abi.load_lib()
+    path = tmp_path / "scene.soarm"
+    cm.save(str(path))
+    raw = path.read_bytes()
+    d = cm.desc
+    assert len(raw) == 16 + C.sizeof(d) + 12 * d.nhullvert + 4 * (d.nhullvert + 1) + 4 * d.nhulladj
+    assert raw[:8] == b"SOARMMDL" and raw[16:16 + C.sizeof(d)] == bytes(d)
+    off = 16 + C.sizeof(d)
+    np.testing.assert_array_equal(np.frombuffer(raw, np.float32, 3 * d.nhullvert, off).reshape(-1, 3),
+                                  cm.hull_vert)
+    model = C.c_void_p()
+    assert lib.sim_model_load(str(path).encode(), C.byref(model)) == 0 and model
+    lib.sim_model_free(model)
+
+    def rejected(data, what):
+        bad = tmp_path / "bad.soarm"
+        bad.write_bytes(data)
+        m = C.c_void_p()
+        assert lib.sim_model_load(str(bad).encode(), C.byref(m)) == -1 and not m, what
+        return lib.sim_last_error()
+
+    assert b"not a compiled" in rejected(b"XOARMMDL" + raw[8:], "magic")
+    assert b"version" in rejected(raw[:8] + (2).to_bytes(4, "little") + raw[12:], "version")
+    assert b"version" in rejected(raw[:12] + (C.sizeof(d) + 4).to_bytes(4, "little") + raw[16:], "layout")
+    assert b"truncated" in rejected(raw[:-4], "truncated")
+    assert b"truncated" in rejected(raw + b"\0", "trailing bytes")
+    assert lib.sim_model_load(str(tmp_path / "missing.soarm").encode(), C.byref(model)) == -1
+
+
 def test_model_validation_rejects_unsupported():
     import soarm_pkg  # noqa: F401
     from lerobot_mujoco_sim2real_amd import mjcf

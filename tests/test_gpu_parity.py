@@ -813,3 +813,27 @@ def test_newton_solver_contact_free(gpu_lib):
     orc.step(st, None, nsub=1)
     np.testing.assert_allclose(to_np(S.qpos).T, st["qpos"], atol=2e-6)
     assert_pct(np.abs(to_np(S.qvel).T - st["qvel"]).max(1), 2e-6, 2e-5, 5e-4, what="qvel")
+
+
+def test_model_file_runs_identically(gpu_lib, cube_model, tmp_path):
+    """A model loaded from its compiled file (sim_model_load, the C caller's from_xml_path) runs
+    the pick scene bit-identically to the model compiled in Python: reset + 5 chirp env-steps."""
+    import torch
+    from lerobot_mujoco_sim2real_amd import abi, workloads as W
+    from lerobot_mujoco_sim2real_amd.sim import BatchSim, SimModel
+    path = tmp_path / "cube.soarm"
+    cube_model.save(str(path))
+    n = 256
+    ids = np.arange(n)
+    q0 = W.initial_qpos(cube_model, ids, 0)
+    tab = W.chirp_tables(ids, 0)
+    out = []
+    for h in (None, SimModel.from_file(str(path), abi.load_lib())):
+        S = BatchSim(cube_model, n, 0, model_handle=h)
+        S.reset(init_qpos=q0[:, :5], extra_qpos=q0, seed=0)
+        for t in range(5):
+            S.step(W.chirp_action(tab, t).astype(np.float32))
+        torch.cuda.synchronize()
+        out.append((to_np(S.obs), to_np(S.qpos), to_np(S.qvel)))
+    for a, b in zip(*out):
+        np.testing.assert_array_equal(a, b)
