@@ -63,7 +63,9 @@ struct NewtonRows {
   const DModel& m;
   const RowLds& L;
   const ContactRows<NA, NF>& cr;
-  const float *fR, *fa;  // frictionloss rows: R, aref (= -B qvel)
+  const float *fR, *fiR, *fa;  // frictionloss rows: R, 1/R, aref (= -B qvel)
+  // (1/R of contacts and limits: the record's F_IARD / L_IARD slot, written for Newton by the
+  // row build; divisions by R are multiplications by it throughout)
   int nlim, nl, ncon;
 
   // does the subsystem over dofs [LO, HI) own a contact of class fl?  (full range: all of them)
@@ -117,7 +119,7 @@ struct NewtonRows {
         for (int q = 0; q < 3; q++)
 #pragma unroll
           for (int i = CL; i < CH; i++) jc[q][i] = L.at(c, 12 * q + i);
-        const float mu = L.at(c, F_MU), D = 1.f / L.at(c, F_R);
+        const float mu = L.at(c, F_MU), D = L.at(c, F_IARD);
         float y[3] = {0.f, 0.f, 0.f};
 #pragma unroll
         for (int q = 0; q < 3; q++)
@@ -180,7 +182,7 @@ struct NewtonRows {
           for (int i = 0; i < NV; i++) J[i] = cr.J(r, i), x = fmaf(J[i], a[i], x);
           sig = sig * 2u + (x < 0.f ? 1u : 0u);
           if (x < 0.f) {
-            const float D = 1.f / cr.S(r, 1), f = -x * D;
+            const float D = cr.S(r, 2), f = -x * D;
             cost += 0.5f * x * x * D;
 #pragma unroll
             for (int i = 0; i < NV; i++) jtf[i] += J[i] * f;
@@ -209,7 +211,7 @@ struct NewtonRows {
       // frictionloss rows (J = e_i)
 #pragma unroll
       for (int i = 0; i < NA; i++) {
-        const float fl = m.dof_frictionloss[i], R = fR[i];
+        const float fl = m.dof_frictionloss[i], R = fR[i], iR = fiR[i];
         const float x = a[i] - fa[i];
         float f, c;
         bool q = false;
@@ -218,30 +220,30 @@ struct NewtonRows {
         } else if (x >= R * fl) {
           f = -fl, c = fl * x - 0.5f * R * fl * fl;
         } else {
-          f = -x / R, c = 0.5f * x * x / R, q = fl > 0.f;
+          f = -x * iR, c = 0.5f * x * x * iR, q = fl > 0.f;
         }
         cost += c;
         jtf[i] += f;
         sig = sig * 3u + (q ? 1u : (x < 0.f ? 2u : 0u));
         if constexpr (WANT_H)
-          if (q) H[hidx(i, i)] += 1.f / R;
+          if (q) H[hidx(i, i)] += iR;
       }
       // joint limits (J = sign e_dof)
       for (int l = 0; l < nlim; l++) {
         const int d = (int)L.lm(l, L_DOF);
-        const float sg = L.lm(l, L_SGN), R = L.lm(l, L_R);
+        const float sg = L.lm(l, L_SGN), iR = L.lm(l, L_IARD);
         float ad = 0.f;
 #pragma unroll
         for (int i = 0; i < NA; i++) ad = i == d ? a[i] : ad;
         const float x = sg * ad - L.lm(l, L_AREF);
         sig = sig * 2u + (x < 0.f ? 1u : 0u);
         if (x < 0.f) {
-          cost += 0.5f * x * x / R;
-          const float f = -x / R;
+          cost += 0.5f * x * x * iR;
+          const float f = -x * iR;
 #pragma unroll
           for (int i = 0; i < NA; i++) {
             jtf[i] += i == d ? sg * f : 0.f;
-            if constexpr (WANT_H) H[hidx(i, i)] += i == d ? 1.f / R : 0.f;
+            if constexpr (WANT_H) H[hidx(i, i)] += i == d ? iR : 0.f;
           }
         }
       }
@@ -266,11 +268,11 @@ struct NewtonRows {
       for (int i = 0; i < NA; i++) {
         const float fl = m.dof_frictionloss[i], R = fR[i], x0 = a[i] - fa[i];
         const bool live = fl > 0.f && p[i] != 0.f;
-        const float rp = 1.f / p[i];
+        const float rp = __builtin_amdgcn_rcpf(p[i]);  // (kinks to ~1 ulp: see ls_eval)
         fr.x0[i] = x0;
         fr.k1[i] = live ? (-R * fl - x0) * rp : 3.0e38f;
         fr.k2[i] = live ? (R * fl - x0) * rp : 3.0e38f;
-        fr.piR[i] = p[i] / R;
+        fr.piR[i] = p[i] * fiR[i];
       }
     } else {
       (void)fr;
@@ -294,7 +296,7 @@ struct NewtonRows {
           const float x0 = ya[0] + s * ya[t] - L.at(c, F_AREF + ed), v = yp[0] + s * yp[t];
           L.ex(XS_LIST + LS_STRIDE * c + ed) = x0;
           L.ex(XS_LIST + LS_STRIDE * c + 4 + ed) = v;
-          L.ex(XS_LIST + LS_STRIDE * c + 8 + ed) = v != 0.f ? -x0 / v : 3.0e38f;
+          L.ex(XS_LIST + LS_STRIDE * c + 8 + ed) = v != 0.f ? -x0 * __builtin_amdgcn_rcpf(v) : 3.0e38f;
         }
       }
       if constexpr (LO == 0 && HI == NV)
@@ -323,7 +325,7 @@ struct NewtonRows {
       for (int c = ql(); c < nl; c += QL) {
         if (!owns<LO, HI>((int)L.at(c, F_FLAGS))) continue;
         mine = true;
-        const float D = 1.f / L.at(c, F_R);
+        const float D = L.at(c, F_IARD);
 #pragma unroll
         for (int ed = 0; ed < 4; ed++) {
           const float v = L.ex(XS_LIST + LS_STRIDE * c + 4 + ed);
@@ -335,7 +337,7 @@ struct NewtonRows {
       if constexpr (LO == 0 && HI == NV)
         for (int r = 4 * nl + ql(); r < 4 * ncon; r += QL) {
           mine = true;
-          const float D = 1.f / cr.S(r, 1), v = cr.W(r, 1), x0 = cr.W(r, 0);
+          const float D = cr.S(r, 2), v = cr.W(r, 1), x0 = cr.W(r, 0);
           const float x = fmaf(al, v, x0);
           if (x < 0.f) c1 += x * v * D, c2 += v * v * D;
           if (v != 0.f) kink(-x0 * __builtin_amdgcn_rcpf(v), cl, cr_);
@@ -359,12 +361,12 @@ struct NewtonRows {
       }
       for (int l = 0; l < nlim; l++) {
         const int d = (int)L.lm(l, L_DOF);
-        const float sg = L.lm(l, L_SGN), R = L.lm(l, L_R);
+        const float sg = L.lm(l, L_SGN), iR = L.lm(l, L_IARD);
         float ad = 0.f, pd = 0.f;
 #pragma unroll
         for (int i = 0; i < NA; i++) ad = i == d ? a[i] : ad, pd = i == d ? p[i] : pd;
         const float x0 = sg * ad - L.lm(l, L_AREF), v = sg * pd, x = fmaf(al, v, x0);
-        if (x < 0.f) d1 += x * v / R, d2 += v * v / R;
+        if (x < 0.f) d1 += x * v * iR, d2 += v * v * iR;
         if (v != 0.f) kink(-x0 * __builtin_amdgcn_rcpf(v), bl, br);
       }
     }

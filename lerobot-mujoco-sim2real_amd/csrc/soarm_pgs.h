@@ -391,6 +391,8 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
           const float ard = Mi.a(i, i) + R;
           L.lm(nlim, L_ARD) = ard;
           L.lm(nlim, L_IARD) = 1.f / ard;
+        } else {
+          L.lm(nlim, L_IARD) = 1.f / R;  // Newton: the row's 1/R
         }
         nlim++;
       }
@@ -478,6 +480,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
         wrec(c, F_MU, mu, split);
         wrec(c, F_R, Rpy, split);
         wrec(c, F_FLAGS, (float)flags, split);
+        if constexpr (NEWT) wrec(c, F_IARD, 1.f / Rpy, split);  // Newton: the pyramid's 1/R
       }
       // Gram matrix G = [Jn; Jt1; Jt2] M^-1 [Jn; Jt1; Jt2]' and the three velocities:
       // every pyramid edge J_e = J_n + s J_tk (s = +-mu) follows from them.  Full
@@ -527,7 +530,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
           }
           cr.S(r, 0) = ar;
           cr.S(r, 1) = Rpy;
-          if constexpr (!NEWT) cr.S(r, 2) = ard;
+          cr.S(r, 2) = NEWT ? 1.f / Rpy : ard;  // (Newton: 1/R)
         }
       }
   };
@@ -623,7 +626,10 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   RP_STORE;
   const int nl = ncon < LDS_CON ? ncon : LDS_CON;
   if constexpr (SOL == SIM_SOL_NEWTON) {  // MuJoCo's default solver on the same rows (soarm_newton.h)
-    const NewtonRows<NA, NF, CON> nr{m, L, cr, fR, fa, nlim, nl, ncon};
+    float fiR[NA];
+#pragma unroll
+    for (int i = 0; i < NA; i++) fiR[i] = 1.f / fR[i];
+    const NewtonRows<NA, NF, CON> nr{m, L, cr, fR, fiR, fa, nlim, nl, ncon};
 #ifdef SOARM_PHASE_PROF
     if (e < 65536) g_pgs_prof[8 * e + 6] = g_pgs_prof[8 * e + 7] = g_pgs_prof[8 * e] = clock64();
     PSTAMP(8);
