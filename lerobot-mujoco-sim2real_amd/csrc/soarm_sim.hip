@@ -343,7 +343,9 @@ __global__ __launch_bounds__(256, SOARM_COLLIDE_WAVES) void k_collide(const DMod
   load_pose(gpose, n, e, m.pair_geom2[p], P2);
   PairOut o{cbuf, n, e, m.pair_slot[p], m.pair_cap[p], 0};
   collide_pair(m, p, P1, P2, o);
-  soa(ccount, p, n, e) = o.n;
+  // (no per-pair count is stored: the pair mask bit and, for multi-contact pairs, its 2-bit
+  // count word carry it -- an empty pair costs no store)
+  (void)ccount;
   if (o.n > 0) {
     atomicOr(&pmask[(size_t)(p >> 5) * n + e], 1u << (p & 31));
     const int cq = m.pair_cq[p];
@@ -363,11 +365,11 @@ static void launch_collide(const sim_batch* b, hipStream_t q, unsigned long long
 }
 
 // walk the pairs in order and append their contacts (deterministic indexing)
-DEVI int gather_contacts(const DModel& m, int n, int e, const float* __restrict__ cbuf,
-                         const int* __restrict__ ccount, const ConLds& C, int& status) {
+DEVI int gather_contacts(const DModel& m, int n, int e, const float* __restrict__ cbuf, const PairMask& pm,
+                         const ConLds& C, int& status) {
   int ncon = 0;
   for (int p = 0; p < m.npair; p++) {
-    const int c = ccount[(size_t)p * n + e];
+    const int c = (pm.w[p >> 5] >> (p & 31)) & 1u ? pm.count(m, p) : 0;
     const int s0 = m.pair_slot[p];
     for (int k = 0; k < c; k++) {
       if (ncon >= SIM_MAXCON) {
@@ -413,7 +415,6 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
       load_pose(gpose_in, n, e, m.pair_geom2[p], P2);
       PairOut o{const_cast<float*>(cbuf), n, e, m.pair_slot[p], m.pair_cap[p], 0};
       collide_pair(m, p, P1, P2, o);
-      soa(const_cast<int*>(ccount), p, n, e) = o.n;
       if (o.n > 0) {
         atomicOr(&pmask[(size_t)(p >> 5) * n + e], 1u << (p & 31));
         const int cq = m.pair_cq[p];
@@ -578,11 +579,13 @@ __global__ __launch_bounds__(64) void k_gather(const DModel* __restrict__ dm, in
                                                float* __restrict__ out, int* __restrict__ nout) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
+  PairMask pm;
+  pm.load(pmask, *dm, n, e);  // the pairs with contacts (and multi-contact counts)
   for (int w = 0; w < pmask_words(*dm); w++) soa(pmask, w, n, e) = 0u;
   __shared__ float s_con[SIM_MAXCON * 8][64];
   const ConLds C{s_con, (int)threadIdx.x};
   int status = 0;
-  const int nc = gather_contacts(*dm, n, e, cbuf, ccount, C, status);
+  const int nc = gather_contacts(*dm, n, e, cbuf, pm, C, status);
   for (int c = 0; c < nc; c++)
     for (int f = 0; f < 8; f++) out[((size_t)e * SIM_MAXCON + c) * 8 + f] = s_con[c * 8 + f][threadIdx.x];
   nout[e] = nc;
