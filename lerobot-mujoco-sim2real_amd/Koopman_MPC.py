@@ -47,7 +47,13 @@ class KoopmanMPCTracking:
         self.sim.enable_qfrc_applied()
         self.H = controller.H
         zref = controller.lift_reference(self.state_all_ref)
-        self.ff = controller.feedforward(zref)  # [T, u, n]
+        if controller.bilinear:
+            # DBKN: the QP depends on each frame's lifted state, so the lifted reference is kept
+            # (zero rows past the end, :199-205) and each frame solves its n QPs
+            self.zpad = torch.cat([zref, torch.zeros((self.H,) + zref.shape[1:], dtype=zref.dtype, device=dev)])
+            self.ff = None
+        else:
+            self.ff = controller.feedforward(zref)  # [T, u, n]
         self.u_prev = torch.zeros((controller.u_dim, self.n), dtype=torch.float64, device=dev)
         self.action = torch.empty((self.n, controller.u_dim), dtype=torch.float32, device=dev)
         self.traj_index = 0
@@ -70,7 +76,10 @@ class KoopmanMPCTracking:
             raise IndexError(f"runFunc: frame {k} is past the trajectory's {self.total_frames} frames "
                              "(return-home playback is not built)")
         self.sim.bias(out=self.sim.qfrc_applied)
-        self.ctl.step(self.state, self.ff[k], self.u_prev, self.action)
+        if self.ff is None:
+            self.ctl.step_bilinear(self.state, self.zpad[k + 1:k + 1 + self.H], self.u_prev, self.action)
+        else:
+            self.ctl.step(self.state, self.ff[k], self.u_prev, self.action)
         self.state = self.sim.step(self.action)
         if self.communicator is not None:  # sim -> real (Koopman_MPC.py:186-190)
             stream_env(self.sim, self.communicator, self.stream_env_id)

@@ -33,6 +33,7 @@ class Args:
         # Koopman-MPC tracking: model kind (:13), MPC form (:75)
         p.add_argument("--model", type=str, default="DKUC", choices=["DKUC", "DBKN"])
         p.add_argument("--MPC_type", type=str, default="delta_mpc", choices=["mpc", "delta_mpc"])
+        p.add_argument("--u_z", action="store_true", default=False)  # DBKN kron order (:43)
         self.args = p.parse_args([] if argv is None else argv)
         self.process_args()
 

@@ -11,6 +11,11 @@ computed once on the host in float64) and every per-env evaluation runs in the H
 * :meth:`feedforward`  — Gr · lifted reference window for every frame (``sim_koopman_feedforward``)
 * :meth:`step`         — one control step for n envs (``sim_koopman_mpc_step``)
 
+A bilinear DBKN model (``net.H``, ``KoopmanBase.py:62-110``) linearises its input matrix at each
+frame's lifted state (``linearize_B``, ``:46-63``), so the QP differs per env and frame:
+:meth:`step_bilinear` lifts the state in the HIP library and solves the n QPs batched in float64
+on the device (``control/koopman.bilinear_first_move``).
+
 There is no CPU path: without the library or a GPU, construction raises.
 """
 import ctypes as C
@@ -18,7 +23,7 @@ import ctypes as C
 import numpy as np
 
 from .. import abi
-from .koopman import condensed_gains
+from .koopman import bilinear_first_move, condensed_gains
 
 Q_WEIGHT, R_WEIGHT = 50.0, 0.5  # state_full weights (MPC_Controler.py:39-40)
 
@@ -33,8 +38,7 @@ class MPCController:
 
         if not torch.cuda.is_available():
             raise RuntimeError("MPCController needs a ROCm GPU (torch.cuda.is_available() is False)")
-        if hasattr(net, "H"):
-            raise NotImplementedError("bilinear Koopman (DBKN) models: see control/koopman.py")
+        self.bilinear = isinstance(getattr(net, "H", None), torch.nn.Module)
         self.torch = torch
         self.in_dim, self.u_dim = args.x_dim, args.u_dim
         self.net = net
@@ -54,6 +58,12 @@ class MPCController:
         self.Q = Q_WEIGHT * np.eye(self.Nkoopman)
         self.R = R_WEIGHT * np.eye(self.u_dim)
         self.Gr, self.Gz, self.Gu = condensed_gains(self.Ad, self.Bd, self.H, self.MPC_type, Q_WEIGHT, R_WEIGHT)
+        if self.bilinear:  # (the gains above are the z0 = 0 linearisation; step_bilinear does not use them)
+            self.H_hat_list = net.get_Hi_numpy()
+            dev = dict(dtype=torch.float64, device=self.device)
+            self._A = torch.as_tensor(self.Ad, **dev)
+            self._B = torch.as_tensor(self.Bd, **dev)
+            self._Hhat = torch.as_tensor(np.stack(self.H_hat_list), **dev)
 
         layers = net.encoder_layers()
         widths = [layers[0][0].shape[1]] + [W.shape[0] for W, _ in layers]
@@ -121,6 +131,22 @@ class MPCController:
                                                           _ptr(action), self._stream()))
         return action
 
+    def step_bilinear(self, x, window, u_prev, action=None, z0=None):
+        """DBKN control step for n envs (in place): z0 = Psi_o(x) (or given [nz, n]), the QP of
+        each env with B_total = Bd + Σ_j z0_j Ĥ_j solved exactly; u_prev <- u0; returns
+        action = clip(u0) [n, u_dim] float32.  window [H, nz, n]: lifted reference rows."""
+        torch = self.torch
+        if z0 is None:
+            z0 = self.encode(x)
+        u0 = bilinear_first_move(self._A, self._B, self._Hhat, z0, window, u_prev, self.MPC_type, self.H,
+                                 Q_WEIGHT, R_WEIGHT)
+        u_prev.copy_(u0)
+        a = torch.clamp(u0, -self.u_clip, self.u_clip).T.to(torch.float32)
+        if action is None:
+            return a.contiguous()
+        action.copy_(a)
+        return action
+
     # ------------------------------------------------------- reference single-env API
     def Psi_o(self, s):
         """Lifted state of s ([1, x_dim] tensor or array) as a (Nkoopman, 1) numpy column (:154-167)."""
@@ -140,11 +166,15 @@ class MPCController:
         z0 = p[H * nz:H * nz + nz]
         u_prev = p[H * nz + nz:H * nz + nz + self.u_dim] if self.MPC_type == "delta_mpc" else self.u_prev
         dev = dict(dtype=torch.float64, device=self.device)
-        zref = torch.zeros((H + 1, nz, 1), **dev)  # frame 0 unused: the window starts at f + 1
-        zref[1:, :, 0] = torch.as_tensor(ref, **dev)
-        ff = self.feedforward(zref, nframe=1)[0]
         up = torch.as_tensor(np.asarray(u_prev, np.float64).reshape(self.u_dim, 1), **dev).contiguous()
-        a = self.step(None, ff, up, z0=torch.as_tensor(z0.reshape(nz, 1), **dev).contiguous())
+        zc = torch.as_tensor(z0.reshape(nz, 1), **dev).contiguous()
+        if self.bilinear:
+            self.step_bilinear(None, torch.as_tensor(ref, **dev).reshape(H, nz, 1), up, z0=zc)
+        else:
+            zref = torch.zeros((H + 1, nz, 1), **dev)  # frame 0 unused: the window starts at f + 1
+            zref[1:, :, 0] = torch.as_tensor(ref, **dev)
+            ff = self.feedforward(zref, nframe=1)[0]
+            self.step(None, ff, up, z0=zc)
         u0 = up[:, 0].cpu().numpy() + self.u_eso
         a = np.clip(u0, -self.u_clip, self.u_clip)  # float64, as :149 (the device action is its f32 copy)
         if self.MPC_type == "delta_mpc":

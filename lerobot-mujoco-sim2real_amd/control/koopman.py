@@ -9,9 +9,10 @@ is kept: the encoder ``x_encoder(x) = cat([x, MLP(x)])``, the Koopman matrices `
 ``models/losses.py``) is out of scope; a user's own trained state_dict loads with
 ``load_state_dict`` as usual.
 
-The bilinear ``DBKN`` model (``KoopmanBlinear``, ``:62-110``) makes the MPC's input matrix depend
-on the lifted state (``MPC_Controler.py:46-63``), i.e. a different QP Hessian per env and frame;
-it is not built here.
+The bilinear ``DBKN`` model (``KoopmanBlinear``, ``:62-110``) adds ``H (z ⊗ u)`` to the step;
+the MPC linearises it at the frame's lifted state, ``B_total = Bd + Σ_j z0_j Ĥ_j``
+(``MPC_Controler.py:46-63``), so its QP differs per env and frame: :func:`bilinear_first_move`
+solves those QPs batched in float64 on the device.
 """
 import numpy as np
 import torch
@@ -65,14 +66,98 @@ class Koopmanlinear(nn.Module):
                 for m in self.x_encode_net if isinstance(m, nn.Linear)]
 
 
+class KoopmanBlinear(Koopmanlinear):
+    """DBKN (``KoopmanBase.py:62-110``): z_{k+1} = lA z + lB u + H vec(z ⊗ u) (``u_z``: vec(u ⊗ z)),
+    H: Linear(Nkoopman * u_dim -> Nkoopman), zero-initialised."""
+
+    def __init__(self, x_dim, u_dim, encode_layers, u_z=False):
+        super().__init__(x_dim, u_dim, encode_layers)
+        self.H = nn.Linear(self.Nkoopman * self.u_dim, self.Nkoopman, bias=False)
+        nn.init.zeros_(self.H.weight)
+        self.u_z = u_z
+
+    def koopman_operation(self, x_emb, u_emb):
+        lin = self.lA(x_emb) + self.lB(u_emb)
+        if self.u_z:
+            kron = torch.einsum("bi,bj->bij", u_emb, x_emb).reshape(x_emb.shape[0], -1)
+        else:
+            kron = torch.einsum("bi,bj->bij", x_emb, u_emb).reshape(x_emb.shape[0], -1)
+        return lin + self.H(kron)
+
+    def build_permutation_matrix(self, n, m):
+        """P with P vec(u ⊗ z) = vec(z ⊗ u) when u_z (identity otherwise), ``:84-95``."""
+        if not self.u_z:
+            return np.eye(n * m)
+        P = np.zeros((n * m, n * m))
+        for i in range(n):
+            for j in range(m):
+                P[j * n + i, i * m + j] = 1
+        return P
+
+    def get_Hi_numpy(self):
+        """[Ĥ_j (Nkoopman x u_dim) for j < Nkoopman]: H vec(z ⊗ u) = Σ_j z_j Ĥ_j u (``:104-110``)."""
+        P = self.build_permutation_matrix(self.u_dim, self.Nkoopman)
+        Hd = self.H.weight.detach().double().cpu().numpy() @ P.T
+        return [Hd[:, j * self.u_dim:(j + 1) * self.u_dim].copy() for j in range(self.Nkoopman)]
+
+
 def init_model(args):
-    """``models/init_model.py:2-21``: DKUC only (see the module docstring for DBKN)."""
+    """``models/init_model.py:2-21``: DKUC (linear) or DBKN (bilinear, ``args.u_z``)."""
     if args.model == "DKUC":
         return Koopmanlinear(args.x_dim, args.u_dim, args.layers)
     if args.model == "DBKN":
-        raise NotImplementedError("DBKN (bilinear Koopman): the MPC's input matrix depends on z0 "
-                                  "(MPC_Controler.py:46-63); only the linear DKUC model is built")
+        return KoopmanBlinear(args.x_dim, args.u_dim, args.layers, bool(getattr(args, "u_z", False)))
     raise ValueError(f"Model {args.model} not implemented!")
+
+
+def bilinear_first_move(A, B, Hhat, z0, window, u_prev, kind, H, q=50.0, r=0.5):
+    """First move u0 of the DBKN MPC for n envs (``MPC_Controler.py:46-141``, state_full), float64
+    torch tensors on one device: B_total = B + Σ_j z0_j Ĥ_j per env (the reference's
+    linearize_B), then the unconstrained QP of the condensed prediction solved exactly.
+
+    A [nz, nz], B [nz, nu], Hhat [nz(j), nz, nu], z0 [nz, n], window [H, nz, n] (lifted reference
+    rows k+1 .. k+H, zero past the end), u_prev [nu, n].  Returns u0 = v*_0 + u_prev [nu, n].
+
+    Block structure (no [H nz, H nu] matrix per env): with M_k = A^k B_total, the prediction's
+    input blocks are X_{t-s} (X = M for 'mpc', the running sums C_k = Σ_{i<=k} M_i for
+    'delta_mpc'), so Hess[s1, s2] = q Σ_{t >= max(s1, s2)} X_{t-s1}' X_{t-s2} + r I and
+    rhs[s] = q Σ_{t >= s} X_{t-s}' e_t with e_t = ref_t - A^{t+1} z0 - c_t u_prev (c_t = C_t for
+    'delta_mpc': u_prev held, else 0)."""
+    import torch
+
+    nz, nu = B.shape
+    n = z0.shape[1]
+    Bt = B.unsqueeze(0) + torch.einsum("jn,jrk->nrk", z0, Hhat)           # [n, nz, nu]
+    P = [torch.eye(nz, dtype=A.dtype, device=A.device)]
+    for _ in range(H):
+        P.append(A @ P[-1])
+    P = torch.stack(P)                                                   # A^0 .. A^H
+    M = torch.einsum("kab,nbc->nkac", P[:H], Bt)                         # [n, H, nz, nu]
+    C = torch.cumsum(M, dim=1)
+    if kind == "delta_mpc":
+        X, cu = C, C
+    elif kind == "mpc":
+        X, cu = M, None
+    else:
+        raise ValueError(f"MPC_type {kind!r}: 'mpc' or 'delta_mpc'")
+    W = torch.einsum("nkab,nlac->nklbc", X, X)                           # X_k' X_l [n, H, H, nu, nu]
+    Hs = torch.zeros((n, H * nu, H * nu), dtype=A.dtype, device=A.device)
+    for s1 in range(H):
+        for s2 in range(H):
+            t0 = max(s1, s2)
+            blk = sum(W[:, t - s1, t - s2] for t in range(t0, H))
+            Hs[:, s1 * nu:(s1 + 1) * nu, s2 * nu:(s2 + 1) * nu] = q * blk
+    Hs += r * torch.eye(H * nu, dtype=A.dtype, device=A.device)
+    Az = torch.einsum("tab,bn->nta", P[1:H + 1], z0)                    # A^{t+1} z0 [n, H, nz]
+    e = window.permute(2, 0, 1) - Az                                     # [n, H, nz]
+    if cu is not None:
+        e = e - torch.einsum("ntab,bn->nta", cu, u_prev)
+    rhs = torch.zeros((n, H * nu), dtype=A.dtype, device=A.device)
+    for s in range(H):
+        rhs[:, s * nu:(s + 1) * nu] = q * sum(torch.einsum("nab,na->nb", X[:, t - s], e[:, t]) for t in range(s, H))
+    L = torch.linalg.cholesky(Hs)
+    v = torch.cholesky_solve(rhs.unsqueeze(-1), L)[..., 0]
+    return v[:, :nu].T + u_prev
 
 
 def condensed_gains(A, B, H, kind, q=50.0, r=0.5):

@@ -10,8 +10,9 @@ What it restates, following the reference's own code order:
   ``MPCController.Psi_o`` (``control/MPC_Controler.py:154-167``) returns it as a column.
 * ``MPCController.setup_mpc`` / ``setup_delta_mpc`` (``control/MPC_Controler.py:65-141``) with
   ``state_full = True`` (``:35-40``: the test ``args.model == 'IBKN' or 'IKN'`` is always true,
-  so Q = 50 I_Nkoopman and R = 0.5 I_u) and the linear model (DKUC: no ``H`` layer, so
-  ``B_total = Bd``, ``:46-63``).  The cost loop is restated literally: z and u_t are carried
+  so Q = 50 I_Nkoopman and R = 0.5 I_u); for the linear model (DKUC: no ``H`` layer)
+  ``B_total = Bd``, for the bilinear DBKN ``B_total = Bd + sum_j z0_j H_hat_j`` at the frame's
+  lifted state (``linearize_B``, ``:46-63``; :func:`get_control_bilinear`).  The cost loop is restated literally: z and u_t are carried
   as affine functions of the decision vector through ``z_next = Ad z + B u_t`` in the loop's
   order, and the quadratic it builds is minimised exactly (normal equations).  ``nlpsol`` is
   called with no bounds (``:145``), so this minimiser is the point IPOPT converges to.
@@ -126,6 +127,31 @@ def get_control(A, B, z0, ref, u_prev, kind="delta_mpc", H=10, u_eso=None, qp=No
     """(u0, a) of MPCController.get_control (:143-152) for n envs."""
     v = solve(A, B, z0, ref, u_prev, kind, H, qp=qp)
     u0 = v[:, 0] + np.atleast_2d(u_prev) + (0.0 if u_eso is None else u_eso)
+    return u0, np.clip(u0, -U_CLIP, U_CLIP)
+
+
+def b_total(B, Hhat, z0):
+    """linearize_B (MPC_Controler.py:46-63): B_total = Bd + sum_j z0[j] * H_hat_j for ONE env.
+    Hhat: the DBKN model's get_Hi_numpy() list (KoopmanBase.py:104-110), z0 [nz]."""
+    Bt = np.asarray(B, np.float64).copy()
+    for j, Hj in enumerate(Hhat):
+        Bt += float(z0[j]) * np.asarray(Hj, np.float64)
+    return Bt
+
+
+def get_control_bilinear(A, B, Hhat, z0, ref, u_prev, kind="delta_mpc", H=10):
+    """(u0, a) of get_control for a DBKN model, n envs: each env's QP is built by the reference's
+    cost loop with its own B_total(z0) (setup_mpc / setup_delta_mpc pass z0 as a parameter and
+    linearise B at it once, :72-73 / :107-108)."""
+    z0 = np.atleast_2d(z0)
+    n = z0.shape[0]
+    ref = np.asarray(ref, np.float64).reshape(n, H, -1)
+    u_prev = np.atleast_2d(u_prev)
+    u0 = np.zeros((n, np.asarray(B).shape[1]))
+    for e in range(n):
+        Bt = b_total(B, Hhat, z0[e])
+        v = solve(A, Bt, z0[e:e + 1], ref[e:e + 1], u_prev[e:e + 1], kind, H)
+        u0[e] = v[0, 0] + u_prev[e]
     return u0, np.clip(u0, -U_CLIP, U_CLIP)
 
 

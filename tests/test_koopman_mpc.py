@@ -105,6 +105,61 @@ def test_condensed_gains_equal_oracle_minimiser(kind):
     np.testing.assert_allclose(u0, want, rtol=1e-9, atol=1e-9)
 
 
+def make_bnet(seed=0, u_z=False, scale=0.02):
+    """DBKN (KoopmanBlinear) with a random bilinear layer (the reference zero-initialises it)."""
+    import torch
+    from lerobot_mujoco_sim2real_amd.control.koopman import KoopmanBlinear
+    torch.manual_seed(seed)
+    net = KoopmanBlinear(8, 5, LAYERS, u_z).double()
+    with torch.no_grad():
+        net.H.weight.normal_(0.0, scale)
+    return net
+
+
+@pytest.mark.parametrize("u_z", [False, True])
+def test_bilinear_model_is_its_linearisation(u_z):
+    """KoopmanBlinear.koopman_operation (KoopmanBase.py:68-80) == A z + (Bd + Σ_j z_j Ĥ_j) u with
+    Ĥ_j from get_Hi_numpy (:104-110): the identity linearize_B (MPC_Controler.py:46-63) relies on,
+    for both Kronecker orders."""
+    import torch
+    net = make_bnet(7, u_z)
+    A, B, layers = net_mats(net)
+    Hhat = net.get_Hi_numpy()
+    z = KO.encode(layers, sample_states(16))
+    u = RNG.uniform(-0.5, 0.5, (16, 5))
+    got = net.koopman_operation(torch.as_tensor(z), torch.as_tensor(u)).detach().numpy()
+    want = np.stack([A @ z[i] + KO.b_total(B, Hhat, z[i]) @ u[i] for i in range(16)])
+    np.testing.assert_allclose(got, want, rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.parametrize("kind", ["delta_mpc", "mpc"])
+def test_bilinear_first_move_equals_oracle(kind):
+    """control/koopman.bilinear_first_move (block-structured batched QP, torch float64; here on the
+    CPU as a unit test of its algebra) == the oracle's per-env restatement of the reference's cost
+    loop with B_total(z0); the oracle's minimiser is pinned by the literal cost's gradient."""
+    import torch
+    from lerobot_mujoco_sim2real_amd.control.koopman import bilinear_first_move
+    net = make_bnet(8)
+    A, B, layers = net_mats(net)
+    Hhat = net.get_Hi_numpy()
+    n, H = 24, 10
+    z0 = KO.encode(layers, sample_states(n))
+    ref = KO.encode(layers, sample_states(n * H)).reshape(n, H, -1)
+    up = RNG.uniform(-0.5, 0.5, (n, 5))
+    u0 = bilinear_first_move(torch.as_tensor(A), torch.as_tensor(B), torch.as_tensor(np.stack(Hhat)),
+                             torch.as_tensor(z0.T.copy()), torch.as_tensor(ref.transpose(1, 2, 0).copy()),
+                             torch.as_tensor(up.T.copy()), kind, H).numpy().T
+    want, _ = KO.get_control_bilinear(A, B, Hhat, z0, ref, up, kind, H)
+    np.testing.assert_allclose(u0, want, rtol=1e-9, atol=1e-9)
+    # the oracle's answer minimises the reference's cost with env 0's B_total
+    Bt = KO.b_total(B, Hhat, z0[0])
+    v = KO.solve(A, Bt, z0[:1], ref[:1], up[:1], kind)[0].ravel()
+    h = 1e-6
+    g = np.array([(KO.cost(A, Bt, v + h * e, z0[0], ref[0], up[0], kind) -
+                   KO.cost(A, Bt, v - h * e, z0[0], ref[0], up[0], kind)) / (2 * h) for e in np.eye(v.size)])
+    assert np.abs(g).max() < 1e-5 * max(1.0, abs(KO.cost(A, Bt, v, z0[0], ref[0], up[0], kind)))
+
+
 def test_koopman_create_validates_before_device():
     """Bad shapes -> SIM_E_MODEL; a good controller without a GPU -> SIM_E_NODEVICE (no CPU path)."""
     from lerobot_mujoco_sim2real_amd import abi, build
@@ -194,6 +249,35 @@ def test_get_control_single_env(gpu_lib):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["delta_mpc", "mpc"])
+def test_bilinear_control_gpu(gpu_lib, kind):
+    """DBKN: step_bilinear for n envs (HIP lift + batched float64 QPs on the device) and
+    get_control(p) == the oracle's per-env restatement."""
+    import torch
+    net = make_bnet(9)
+    ctl = _ctl(net, kind)
+    assert ctl.bilinear
+    A, B, layers = net_mats(net)
+    Hhat = net.get_Hi_numpy()
+    n, H = 512, 10
+    x = sample_states(n).astype(np.float32)
+    ref = KO.encode(layers, sample_states(n * H)).reshape(n, H, -1)
+    up0 = RNG.uniform(-0.5, 0.5, (n, 5))
+    up = torch.as_tensor(up0.T.copy(), device=ctl.device)
+    win = torch.as_tensor(ref.transpose(1, 2, 0).copy(), device=ctl.device)
+    a = ctl.step_bilinear(torch.as_tensor(x, device=ctl.device), win, up).cpu().numpy()
+    u0, aw = KO.get_control_bilinear(A, B, Hhat, KO.encode(layers, x.astype(np.float64)), ref, up0, kind, H)
+    np.testing.assert_allclose(up.cpu().numpy().T, u0, rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(a, aw.astype(np.float32), atol=1e-6)
+    z0 = KO.encode(layers, sample_states(1))[0]
+    ctl.u_prev = RNG.uniform(-0.3, 0.3, 5)
+    p = np.concatenate([ref[0].ravel(), z0, ctl.u_prev]).reshape(-1, 1)
+    g0, _ = ctl.get_control(p)
+    w0, _ = KO.get_control_bilinear(A, B, Hhat, z0[None], ref[:1], p[-5:, 0][None], kind, H)
+    np.testing.assert_allclose(g0, w0[0], rtol=1e-9, atol=1e-9)
+
+
+@pytest.mark.gpu
 def test_bias_matches_oracle(gpu_lib, arm_model, cube_model):
     from test_gpu_parity import load_state, random_states, to_np, make_sim
     for cm in (arm_model, cube_model):
@@ -280,6 +364,36 @@ def test_tracking_loop_matches_oracle(gpu_lib, arm_model):
     # past the last frame the reference plays back its return-home path (out of scope): a clear error
     with pytest.raises(IndexError, match="past the trajectory"):
         run.runFunc()
+
+
+@pytest.mark.gpu
+def test_bilinear_tracking_loop(gpu_lib, arm_model):
+    """KoopmanMPCTracking with a DBKN model: every frame's action equals the oracle's bilinear MPC
+    on the GPU's own state and u_prev (its QP linearised at that frame's lifted state)."""
+    import torch
+    from lerobot_mujoco_sim2real_amd.Koopman_MPC import KoopmanMPCTracking
+    net = make_bnet(10)
+    ctl = _ctl(net)
+    A, B, layers = net_mats(net)
+    Hhat = net.get_Hi_numpy()
+    T, n = 12, 32
+    t = np.linspace(0, 2 * np.pi, T)
+    phase = RNG.uniform(0, 2 * np.pi, n)
+    cart = np.stack([0.3 + 0.0 * t[:, None] + 0 * phase, 0.1 * np.cos(t[:, None] + phase),
+                     0.15 + 0.05 * np.sin(t[:, None] + phase)], -1)
+    jq = RNG.uniform(-0.3, 0.3, (1, n, 5)) + 0.1 * np.sin(t[:, None, None] + phase[None, :, None])
+    run = KoopmanMPCTracking(ctl, arm_model, cart, jq)
+    sref = run.state_all_ref.cpu().numpy().astype(np.float64)
+    zref = KO.encode(layers, sref.reshape(T * n, 8)).reshape(T, n, -1)
+    run.runBefore()
+    for k in range(T):
+        x = run.state.cpu().numpy().astype(np.float64)
+        up = run.u_prev.cpu().numpy().T.copy()
+        run.runFunc()
+        u0, aw = KO.get_control_bilinear(A, B, Hhat, KO.encode(layers, x), KO.lifted_window(zref, k, 10), up)
+        np.testing.assert_allclose(run.u_prev.cpu().numpy().T, u0, rtol=1e-9, atol=1e-9)
+        np.testing.assert_allclose(run.action.cpu().numpy(), aw.astype(np.float32), atol=1e-6)
+    assert torch.isfinite(run.sim.qpos).all()
 
 
 class _Sink:
