@@ -6,7 +6,7 @@ SO-ARM101 envs per GPU with contacts (config 3: the build-defined pick scene,
 table + cube, PGS, chirp actions).  One step = one ``SOARM101Env.step()`` for
 every env = 10 physics substeps of 2 ms (``SOARM101_Env.py:39-40,131-132``).
 
-    python bench.py [--gpus N --steps K --warmup W --config contact|nocontact|dr|rollout|mpc|plumbing]
+    python bench.py [--gpus N --steps K --warmup W --config contact|nocontact|dr|rollout|mpc|mpc_dbkn|plumbing]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 One process per GPU; envs shard by global env id (rank r owns
@@ -37,7 +37,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--envs", type=int, default=None, help="envs per GPU (default 4096; 8192 for dr)")
     p.add_argument("--config", default="contact",
-                   choices=["contact", "nocontact", "dr", "rollout", "mpc", "plumbing"])
+                   choices=["contact", "nocontact", "dr", "rollout", "mpc", "mpc_dbkn", "plumbing"])
     p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal on one GPU)")
     p.add_argument("--solver", default="pgs", choices=["pgs", "newton"],
                    help="constraint solver: PGS (BASELINE config 3) or MuJoCo's default Newton")
@@ -113,9 +113,10 @@ def cpu_baseline(cfg_name, seconds, seed, solver="pgs"):
     mpc = None
     if cfg["action"] == "koopman_mpc":
         import koopman_mpc as KO
-        net, _ = _mpc_net(seed)
+        net, _ = _mpc_net(seed, cfg.get("koopman", "DKUC"))
         A, B = net.lA.weight.detach().numpy(), net.lB.weight.detach().numpy()
-        mpc = (KO, A, B, net.encoder_layers(), KO.prepare(A, B))
+        Hhat = net.get_Hi_numpy() if hasattr(net, "get_Hi_numpy") else None
+        mpc = (KO, A, B, net.encoder_layers(), KO.prepare(A, B), Hhat)
 
     def run_chunk(ids, nthreads):
         n = len(ids)
@@ -131,14 +132,17 @@ def cpu_baseline(cfg_name, seconds, seed, solver="pgs"):
         phase = W.ik_phase(ids, seed)
         qstar = q.astype(np.float64)
         if mpc:  # Koopman_MPC.py loop on the oracle (joint refs: the start pose)
-            KO, A, B, layers, qp = mpc
+            KO, A, B, layers, qp, Hhat = mpc
             cart = np.stack([W.fig8_targets(t - 1.0, phase) for t in range(T)])
             sref = np.concatenate([cart, np.repeat(q[None, :, :5].astype(np.float64), T, 0)], -1)
             zref = KO.encode(layers, sref.reshape(T * n, 8)).reshape(T, n, -1)
             x, up = sref[0], np.zeros((n, 5))
         for t in range(T):
             if mpc:
-                up, a = KO.get_control(A, B, KO.encode(layers, x), KO.lifted_window(zref, t, 10), up, qp=qp)
+                if Hhat is None:
+                    up, a = KO.get_control(A, B, KO.encode(layers, x), KO.lifted_window(zref, t, 10), up, qp=qp)
+                else:
+                    up, a = KO.get_control_bilinear(A, B, Hhat, KO.encode(layers, x), KO.lifted_window(zref, t, 10), up)
                 x = orc.step(st, a, nthreads=nthreads, applied=orc.bias(st)).astype(np.float32).astype(np.float64)
                 continue
             if cfg["action"] == "chirp":
@@ -191,14 +195,20 @@ def cpu_baseline(cfg_name, seconds, seed, solver="pgs"):
             "cpu_model": cpu_name, "nproc": os.cpu_count(), "mujoco": mj}
 
 
-def _mpc_net(seed):
-    """Random-init DKUC Koopman model of the reference's architecture (control/koopman.py)."""
+def _mpc_net(seed, kind="DKUC"):
+    """Random-init Koopman model of the reference's architecture (control/koopman.py): DKUC, or
+    DBKN with its bilinear layer drawn N(0, 0.02^2) (the reference zero-initialises it, which
+    would make the bilinear MPC the linear one)."""
     import torch
     from lerobot_mujoco_sim2real_amd.args import Args
-    from lerobot_mujoco_sim2real_amd.control.koopman import Koopmanlinear
+    from lerobot_mujoco_sim2real_amd.control.koopman import init_model
     torch.manual_seed(seed)
-    a = Args()
-    return Koopmanlinear(a.x_dim, a.u_dim, a.layers).double(), a
+    a = Args(["--model", kind])
+    net = init_model(a).double()
+    if kind == "DBKN":
+        with torch.no_grad():
+            net.H.weight.normal_(0.0, 0.02)
+    return net, a
 
 
 def main():
@@ -259,7 +269,7 @@ def main():
         # sim_bias -> qfrc_applied, k_mpc_step, sim_step (all on device)
         from lerobot_mujoco_sim2real_amd.control.MPC_Controler import MPCController
         from lerobot_mujoco_sim2real_amd.Koopman_MPC import KoopmanMPCTracking
-        net, margs = _mpc_net(args.seed)
+        net, margs = _mpc_net(args.seed, cfg.get("koopman", "DKUC"))
         ctl = MPCController(net, margs, device=gpu)
         phase = torch.as_tensor(W.ik_phase(ids, args.seed), dtype=torch.float32, device=dev)
         cart, jq = W.reference_trajectory(sim, phase, args.warmup + args.steps)
@@ -379,7 +389,8 @@ def main():
     # the timed region -- state, action stream and step index restored from the snapshot
     roof = None
     costs = json.load(open(os.path.join(ROOT, "profiles", "algorithmic_cost.json")))
-    cost = costs.get(name if args.solver == "pgs" else f"{name}_newton", costs[name])
+    base = name if name in costs else "mpc"  # (mpc_dbkn: the same physics per env-step as mpc)
+    cost = costs.get(name if args.solver == "pgs" else f"{name}_newton", costs[base])
     if not args.no_profile:
         kp = args.steps
         restore_timed()

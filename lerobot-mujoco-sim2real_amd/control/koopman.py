@@ -110,6 +110,43 @@ def init_model(args):
     raise ValueError(f"Model {args.model} not implemented!")
 
 
+_TOEPLITZ = {}
+
+
+def _toeplitz_index(H, device):
+    """Index tensors of bilinear_first_move's block sums (cached per H and device)."""
+    import torch
+
+    key = (H, str(device))
+    if key not in _TOEPLITZ:
+        D = 2 * H - 1
+        da = np.zeros((D, H), np.int64)
+        db = np.zeros((D, H), np.int64)
+        dm = np.zeros((D, H))
+        for di, d in enumerate(range(-(H - 1), H)):
+            for a in range(H):
+                b = a - d
+                if 0 <= b < H:
+                    da[di, a], db[di, a], dm[di, a] = a, b, 1.0
+        hd = np.zeros((H, H), np.int64)
+        ha = np.zeros((H, H), np.int64)
+        for s1 in range(H):
+            for s2 in range(H):
+                hd[s1, s2] = (s2 - s1) + H - 1
+                ha[s1, s2] = H - 1 - s1  # (terms with a < max(0, d) are zero-masked)
+        ra = np.zeros((H, H), np.int64)
+        rt = np.zeros((H, H), np.int64)
+        rm = np.zeros((H, H))
+        for s in range(H):
+            for j, t in enumerate(range(s, H)):
+                ra[s, j], rt[s, j], rm[s, j] = t - s, t, 1.0
+        T = lambda x: torch.as_tensor(x, device=device)  # noqa: E731
+        _TOEPLITZ[key] = {"da": T(da), "db": T(db), "dm": T(dm).double()[None, :, :, None, None],
+                          "hd": T(hd), "ha": T(ha), "ra": T(ra), "rt": T(rt),
+                          "rm": T(rm).double()[None, :, :, None]}
+    return _TOEPLITZ[key]
+
+
 def bilinear_first_move(A, B, Hhat, z0, window, u_prev, kind, H, q=50.0, r=0.5):
     """First move u0 of the DBKN MPC for n envs (``MPC_Controler.py:46-141``, state_full), float64
     torch tensors on one device: B_total = B + Σ_j z0_j Ĥ_j per env (the reference's
@@ -140,21 +177,23 @@ def bilinear_first_move(A, B, Hhat, z0, window, u_prev, kind, H, q=50.0, r=0.5):
         X, cu = M, None
     else:
         raise ValueError(f"MPC_type {kind!r}: 'mpc' or 'delta_mpc'")
+    idx = _toeplitz_index(H, A.device)
     W = torch.einsum("nkab,nlac->nklbc", X, X)                           # X_k' X_l [n, H, H, nu, nu]
-    Hs = torch.zeros((n, H * nu, H * nu), dtype=A.dtype, device=A.device)
-    for s1 in range(H):
-        for s2 in range(H):
-            t0 = max(s1, s2)
-            blk = sum(W[:, t - s1, t - s2] for t in range(t0, H))
-            Hs[:, s1 * nu:(s1 + 1) * nu, s2 * nu:(s2 + 1) * nu] = q * blk
-    Hs += r * torch.eye(H * nu, dtype=A.dtype, device=A.device)
+    # Hess[s1, s2] = q Σ_{t >= max(s1, s2)} W[t - s1, t - s2]: running sums along each diagonal
+    # d = s2 - s1 of W (a = t - s1 runs from max(0, d) to H - 1 - s1), gathered per block
+    Wd = W[:, idx["da"], idx["db"]] * idx["dm"]                          # [n, 2H-1, H, nu, nu]
+    Sd = torch.cumsum(Wd, dim=2)
+    Hs = q * Sd[:, idx["hd"], idx["ha"]]                                 # [n, H, H, nu, nu] (s1, s2)
+    Hs = Hs.permute(0, 1, 3, 2, 4).reshape(n, H * nu, H * nu)
+    Hs = Hs + r * torch.eye(H * nu, dtype=A.dtype, device=A.device)
     Az = torch.einsum("tab,bn->nta", P[1:H + 1], z0)                    # A^{t+1} z0 [n, H, nz]
     e = window.permute(2, 0, 1) - Az                                     # [n, H, nz]
     if cu is not None:
         e = e - torch.einsum("ntab,bn->nta", cu, u_prev)
-    rhs = torch.zeros((n, H * nu), dtype=A.dtype, device=A.device)
-    for s in range(H):
-        rhs[:, s * nu:(s + 1) * nu] = q * sum(torch.einsum("nab,na->nb", X[:, t - s], e[:, t]) for t in range(s, H))
+    # rhs[s] = q Σ_{t >= s} X_{t-s}' e_t
+    Y = torch.einsum("nkab,nta->nktb", X, e)                             # X_k' e_t [n, H(k), H(t), nu]
+    rhs = q * (Y[:, idx["ra"], idx["rt"]] * idx["rm"]).sum(2)            # [n, H(s), nu]
+    rhs = rhs.reshape(n, H * nu)
     L = torch.linalg.cholesky(Hs)
     v = torch.cholesky_solve(rhs.unsqueeze(-1), L)[..., 0]
     return v[:, :nu].T + u_prev

@@ -49,6 +49,9 @@ CONFIGS = {
     "mpc": dict(xml=SCENE_XML, disable_contact=False, action="koopman_mpc", dr=False,
                 desc="Koopman-MPC Fig8 tracking (Koopman_MPC.py loop, SURVEY 8f rank 2): per env and frame "
                      "gravity compensation + f64 MFMA encoder/MPC + env step, 4096 envs"),
+    "mpc_dbkn": dict(xml=SCENE_XML, disable_contact=False, action="koopman_mpc", dr=False, koopman="DBKN",
+                     desc="Koopman-MPC Fig8 tracking with the bilinear DBKN model: per env and frame its QP "
+                          "linearised at the lifted state and solved in f64 on the device, 4096 envs"),
 }
 
 
