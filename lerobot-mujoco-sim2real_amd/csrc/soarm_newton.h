@@ -131,13 +131,13 @@ struct NewtonRows {
           const float s = (ed & 1) ? -mu : mu;
           const int t = 1 + (ed >> 1);
           const float x = y[0] + s * y[t] - L.at(c, F_AREF + ed);
-          sig = sig * 2u + (x < 0.f ? 1u : 0u);
-          if (x < 0.f) {
-            cost += 0.5f * x * x * D;
-            const float f = -x * D;
-            F[0] += f, F[t] += s * f;
-            K[0] += D, K[t] += s * D, K[t == 1 ? 3 : 5] += s * s * D;
-          }
+          const bool act = x < 0.f;
+          sig = sig * 2u + (act ? 1u : 0u);
+          const float xa = act ? x : 0.f, Da = act ? D : 0.f;  // (branch-free)
+          cost += 0.5f * xa * xa * D;
+          const float f = -xa * D;
+          F[0] += f, F[t] += s * f;
+          K[0] += Da, K[t] += s * Da, K[t == 1 ? 3 : 5] += s * s * Da;
         }
 #pragma unroll
         for (int i = CL; i < CH; i++) jtf[i] += jc[0][i] * F[0] + jc[1][i] * F[1] + jc[2][i] * F[2];
@@ -211,22 +211,16 @@ struct NewtonRows {
       // frictionloss rows (J = e_i)
 #pragma unroll
       for (int i = 0; i < NA; i++) {
+        // (branch-free: the zone decides values, not control flow)
         const float fl = m.dof_frictionloss[i], R = fR[i], iR = fiR[i];
-        const float x = a[i] - fa[i];
-        float f, c;
-        bool q = false;
-        if (x <= -R * fl) {
-          f = fl, c = -fl * x - 0.5f * R * fl * fl;
-        } else if (x >= R * fl) {
-          f = -fl, c = fl * x - 0.5f * R * fl * fl;
-        } else {
-          f = -x * iR, c = 0.5f * x * x * iR, q = fl > 0.f;
-        }
-        cost += c;
-        jtf[i] += f;
+        const float x = a[i] - fa[i], Rfl = R * fl;
+        const bool lin = fabsf(x) >= Rfl;  // linear zones x <= -R fl, x >= R fl (all of it when fl = 0)
+        const bool q = !lin;               // (fl > 0 here)
+        const float flx = x < 0.f ? fl : -fl;
+        jtf[i] += lin ? flx : -x * iR;
+        cost += lin ? fmaf(fl, fabsf(x), -0.5f * Rfl * fl) : 0.5f * x * x * iR;
         sig = sig * 3u + (q ? 1u : (x < 0.f ? 2u : 0u));
-        if constexpr (WANT_H)
-          if (q) H[hidx(i, i)] += iR;
+        if constexpr (WANT_H) H[hidx(i, i)] += q ? iR : 0.f;
       }
       // joint limits (J = sign e_dof)
       for (int l = 0; l < nlim; l++) {
