@@ -67,6 +67,7 @@ struct PairOut {
   float* cbuf;
   int nenv, e, s0, cap;  // env count / env, first slot and slot count of the pair
   int n;                 // contacts written
+  int xc = 0;            // diagnostic (SOARM_COLLIDE_STATS): which test decided the pair
 };
 
 // hill-climbing support on a mesh hull; returns the local vertex.  Opens at the cube-map
@@ -256,8 +257,11 @@ DEVI void expand(MSup p[4], const MSup& v4) {
   sel(p[2], !c1 && c3, v4);
   sel(p[3], c1 && !c2, v4);
 }
-// -1 separated, 0 portal, 1 origin on v1, 2 origin on segment v0-v1
-DEVI int discover(const MPair& P, MSup p[4]) {
+// -1 separated, 0 portal, 1 origin on v1, 2 origin on segment v0-v1.  On a separated exit
+// found by a support query, sep = that query's direction (the Minkowski difference lies
+// on its negative side: a separating axis); otherwise sep is left as it was.
+DEVI void setsep(float sep[3], const float d[3]) { sep[0] = d[0], sep[1] = d[1], sep[2] = d[2]; }
+DEVI int discover(const MPair& P, MSup p[4], float sep[3]) {
   float c1[3], c2[3], d[3], va[3], vb[3];
   geom_center(P.m, P.g1, P.P1, c1);
   geom_center(P.m, P.g2, P.P2, c2);
@@ -268,7 +272,10 @@ DEVI int discover(const MPair& P, MSup p[4]) {
   nrm(d);
   P.sup(d, p[1]);
   float dt = dot3(p[1].v, d);
-  if (fz(dt) || dt < 0.f) return -1;
+  if (fz(dt) || dt < 0.f) {
+    setsep(sep, d);
+    return -1;
+  }
   cross(d, p[0].v, p[1].v);
   if (fz(dot3(d, d))) {
     if (fz(p[1].v[0]) && fz(p[1].v[1]) && fz(p[1].v[2])) return 1;
@@ -277,7 +284,10 @@ DEVI int discover(const MPair& P, MSup p[4]) {
   nrm(d);
   P.sup(d, p[2]);
   dt = dot3(p[2].v, d);
-  if (fz(dt) || dt < 0.f) return -1;
+  if (fz(dt) || dt < 0.f) {
+    setsep(sep, d);
+    return -1;
+  }
   sub(va, p[1].v, p[0].v);
   sub(vb, p[2].v, p[0].v);
   cross(d, va, vb);
@@ -291,7 +301,10 @@ DEVI int discover(const MPair& P, MSup p[4]) {
   for (int guard = 0; guard < 1000; guard++) {
     P.sup(d, p[3]);
     dt = dot3(p[3].v, d);
-    if (fz(dt) || dt < 0.f) return -1;
+    if (fz(dt) || dt < 0.f) {
+      setsep(sep, d);
+      return -1;
+    }
     cross(va, p[1].v, p[3].v);
     dt = dot3(va, p[0].v);
     const bool r2 = dt < 0.f && !fz(dt);
@@ -387,10 +400,11 @@ DEVI void portal_pos(const MSup p[4], float pos[3]) {
 #pragma unroll
   for (int k = 0; k < 3; k++) pos[k] = 0.5f * (s1[k] + s2[k]) * inv;
 }
-// returns 1 with depth/dir(geom1->geom2)/pos when penetrating
-DEVI int mpr(const MPair& P, float& depth, float dir[3], float pos[3]) {
+// returns 1 with depth/dir(geom1->geom2)/pos when penetrating; sep = a separating axis
+// when it proved the pair apart by a support query (else unchanged)
+DEVI int mpr(const MPair& P, float& depth, float dir[3], float pos[3], float sep[3]) {
   MSup p[4];
-  const int res = discover(P, p);
+  const int res = discover(P, p, sep);
   if (res < 0 || res == 1) return 0;
   if (res == 2) {
     depth = sqrtf(dot3(p[1].v, p[1].v));
@@ -409,7 +423,11 @@ DEVI int mpr(const MPair& P, float& depth, float dir[3], float pos[3]) {
     MSup v4;
     P.sup(d, v4);
     const float d4 = dot3(v4.v, d);
-    if (!(fz(d4) || d4 > 0.f) || reach_tol(p, v4, d)) return 0;
+    if (!(fz(d4) || d4 > 0.f)) {
+      setsep(sep, d);
+      return 0;
+    }
+    if (reach_tol(p, v4, d)) return 0;
     expand(p, v4);
   }
   // penetration: expand towards the boundary
@@ -788,9 +806,54 @@ DEVI bool midphase(const DModel& m, int p, const GeomPose& P1, const GeomPose& P
   return true;
 }
 
+// Separating-axis cache of one env's candidate pairs, [pair*3 + k][env]: the axis of the last
+// MPR run that proved the pair apart (zero: none).  A pair whose cached axis still separates it
+// (the support bounds along it leave a gap > SEP_MARGIN) is apart, exactly as MPR would find --
+// any separating axis is a proof -- so the cache changes which pairs skip MPR, never a contact.
+// Between substeps the geoms move by millimetres: a persistently separated near pair (the
+// wrist/jaw meshes, the jaw above the cube) skips its MPR run on nearly every substep.
+struct SepCache {
+  float* a;  // null: no cache (the fused-collide build)
+  int n, e;
+  DEVI void load(int p, float d[3]) const {
+#pragma unroll
+    for (int k = 0; k < 3; k++) d[k] = a ? soa(a, 3 * p + k, n, e) : 0.f;
+  }
+  DEVI void store(int p, const float d[3]) const {
+    if (!a) return;
+#pragma unroll
+    for (int k = 0; k < 3; k++) soa(a, 3 * p + k, n, e) = d[k];
+  }
+};
+// upper bound on geom g's support value along the local direction l (box: exact)
+DEVI float support_ub_any(const DModel& m, int g, const float l[3]) {
+  if (m.geom_type[g] == SIM_GEOM_BOX)
+    return fabsf(l[0]) * m.geom_size[g][0] + fabsf(l[1]) * m.geom_size[g][1] + fabsf(l[2]) * m.geom_size[g][2];
+  return support_ub(m, g, l);
+}
+// upper bound on max over (geom1 - geom2) of x.d: below zero proves the pair apart along d
+DEVI float minkowski_ub(const DModel& m, int g1, int g2, const GeomPose& P1, const GeomPose& P2, const float d[3]) {
+  float l1[3], l2[3];
+  mtv(l1, P1.R, d);
+  mtv(l2, P2.R, d);
+  l2[0] = -l2[0], l2[1] = -l2[1], l2[2] = -l2[2];
+  return (P1.p[0] - P2.p[0]) * d[0] + (P1.p[1] - P2.p[1]) * d[1] + (P1.p[2] - P2.p[2]) * d[2] +
+         support_ub_any(m, g1, l1) + support_ub_any(m, g2, l2);
+}
+// the cached axis of pair p still separates it
+DEVI bool cached_apart(const DModel& m, int p, int g1, int g2, const GeomPose& P1, const GeomPose& P2,
+                       const SepCache& sc) {
+  float d[3];
+  sc.load(p, d);
+  if (d[0] == 0.f && d[1] == 0.f && d[2] == 0.f) return false;
+  return minkowski_ub(m, g1, g2, P1, P2, d) < -(m.pair_margin[p] + SEP_MARGIN);
+}
+
 // narrowphase of a pair that passed the midphase (geom types are uniform over a pair)
-DEVI void narrowphase(const DModel& m, int p, const GeomPose& P1, const GeomPose& P2, PairOut& o) {
+DEVI void narrowphase(const DModel& m, int p, const GeomPose& P1, const GeomPose& P2, PairOut& o,
+                      const SepCache& sc) {
   o.n = 0;
+  o.xc = 6;
   const int g1 = m.pair_geom1[p], g2 = m.pair_geom2[p];
   const int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
   if (t1 == SIM_GEOM_PLANE) {
@@ -830,12 +893,13 @@ DEVI void narrowphase(const DModel& m, int p, const GeomPose& P1, const GeomPose
                           P2.R[2] * nd[0] + P2.R[5] * nd[1] + P2.R[8] * nd[2]};
       const float lo = -support_ub(m, g2, l) + (P2.p[0] - P1.p[0]) * ax[0] + (P2.p[1] - P1.p[1]) * ax[1] +
                        (P2.p[2] - P1.p[2]) * ax[2] - h;  // <= the hull's distance beyond the face
-      if (lo > m.pair_margin[p] + SEP_MARGIN) return;
+      if (lo > m.pair_margin[p] + SEP_MARGIN) return (void)(o.xc = 1);
     }
+    if (cached_apart(m, p, g1, g2, P1, P2, sc)) return (void)(o.xc = 2);
     float sp[3];
     support(m, g2, P2, nd, sp);
     const float dist = (sp[0] - P1.p[0]) * ax[0] + (sp[1] - P1.p[1]) * ax[1] + (sp[2] - P1.p[2]) * ax[2] - h;
-    if (dist > m.pair_margin[p]) return;
+    if (dist > m.pair_margin[p]) return (void)(o.xc = 1);
   }
   if (t1 == SIM_GEOM_MESH && t2 == SIM_GEOM_MESH) {
     // MPR's first test on support bounds: along d = c2 - c1 (MPR's first search direction) the
@@ -859,20 +923,28 @@ DEVI void narrowphase(const DModel& m, int p, const GeomPose& P1, const GeomPose
                            -(P2.R[2] * d[0] + P2.R[5] * d[1] + P2.R[8] * d[2])};
       const float ub = (P1.p[0] - P2.p[0]) * d[0] + (P1.p[1] - P2.p[1]) * d[1] + (P1.p[2] - P2.p[2]) * d[2] +
                        support_ub(m, g1, l1) + support_ub(m, g2, l2);
-      if (ub < -SEP_MARGIN) return;
+      if (ub < -SEP_MARGIN) return (void)(o.xc = 1);
     }
+    if (cached_apart(m, p, g1, g2, P1, P2, sc)) return (void)(o.xc = 2);
   }
   MPair mp{m, g1, g2, P1, P2};
-  float depth, dir[3], pos[3];
-  if (mpr(mp, depth, dir, pos)) emit(o, -depth, pos, dir);
+  float depth, dir[3], pos[3], sep[3] = {0.f, 0.f, 0.f};
+  if (mpr(mp, depth, dir, pos, sep)) {
+    emit(o, -depth, pos, dir);
+    o.xc = 5;
+  } else {
+    o.xc = (sep[0] != 0.f || sep[1] != 0.f || sep[2] != 0.f) ? 3 : 4;
+  }
+  sc.store(p, sep);
 }
 
 }  // namespace soarm
 
 namespace soarm {
 // midphase + narrowphase of candidate pair p
-DEVI void collide_pair(const DModel& m, int p, const GeomPose& P1, const GeomPose& P2, PairOut& o) {
+DEVI void collide_pair(const DModel& m, int p, const GeomPose& P1, const GeomPose& P2, PairOut& o,
+                         const SepCache& sc = SepCache{nullptr, 0, 0}) {
   o.n = 0;
-  if (midphase(m, p, P1, P2)) narrowphase(m, p, P1, P2, o);
+  if (midphase(m, p, P1, P2)) narrowphase(m, p, P1, P2, o, sc);
 }
 }  // namespace soarm

@@ -131,6 +131,7 @@ struct sim_batch {
   float* d_cbuf = nullptr;     // collide output [slot*7+f][env]
   int* d_ccount = nullptr;     // contacts per pair [pair][env]
   uint32_t* d_pmask = nullptr; // pairs with contacts, bit p%32 of word p/32: [word][env]
+  float* d_sepax = nullptr;    // separating-axis cache [pair*3+k][env] (soarm_collide.h SepCache)
   // profiling (sim_profile_begin/end)
   bool prof = false;
   std::vector<hipEvent_t> ev_pool;
@@ -332,6 +333,7 @@ __global__ __launch_bounds__(256, SOARM_COLLIDE_WAVES) void k_collide(const DMod
                                                  const float* __restrict__ gpose,
                                                  float* __restrict__ cbuf, int* __restrict__ ccount,
                                                  uint32_t* __restrict__ pmask,
+                                                 float* __restrict__ sepax,
                                                  unsigned long long* __restrict__ pcyc) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   const int p = gridDim.y - 1 - blockIdx.y;  // later pairs (self / cube-arm: MPR-heavy) dispatch first
@@ -342,7 +344,7 @@ __global__ __launch_bounds__(256, SOARM_COLLIDE_WAVES) void k_collide(const DMod
   load_pose(gpose, n, e, m.pair_geom1[p], P1);
   load_pose(gpose, n, e, m.pair_geom2[p], P2);
   PairOut o{cbuf, n, e, m.pair_slot[p], m.pair_cap[p], 0};
-  collide_pair(m, p, P1, P2, o);
+  collide_pair(m, p, P1, P2, o, SepCache{sepax, n, e});
   // (no per-pair count is stored: the pair mask bit and, for multi-contact pairs, its 2-bit
   // count word carry it -- an empty pair costs no store)
   (void)ccount;
@@ -351,17 +353,23 @@ __global__ __launch_bounds__(256, SOARM_COLLIDE_WAVES) void k_collide(const DMod
     const int cq = m.pair_cq[p];
     if (cq >= 0) atomicOr(&pmask[(size_t)((m.npair + 31) >> 5) * n + e], (uint32_t)(o.n - 1) << (2 * cq));
   }
+#ifdef SOARM_COLLIDE_STATS
+  // diagnostic build: per pair, how many envs each test decided (13-bit counters: codes 0-3 in
+  // the first word, 4-7 in the second; see PairOut::xc)
+  if (pcyc) atomicAdd(&pcyc[(o.xc >> 2) * gridDim.y + p], 1ull << (13 * (o.xc & 3)));
+#else
   if (pcyc && (threadIdx.x & 63) == 0) {
     const unsigned long long dt = (unsigned long long)(clock64() - t0);
     atomicAdd(&pcyc[p], dt);
     atomicMax(&pcyc[gridDim.y + p], dt);
   }
+#endif
 }
 
 // the collide launch: (env, pair) lanes, 256-env blocks x npair
 static void launch_collide(const sim_batch* b, hipStream_t q, unsigned long long* pcyc) {
   hipLaunchKernelGGL(k_collide, dim3((b->n + 255) / 256, b->model->desc.npair), dim3(256), 0, q, b->d_model, b->n,
-                     b->d_gpose, b->d_cbuf, b->d_ccount, b->d_pmask, pcyc);
+                     b->d_gpose, b->d_cbuf, b->d_ccount, b->d_pmask, b->d_sepax, pcyc);
 }
 
 // walk the pairs in order and append their contacts (deterministic indexing)
@@ -1365,6 +1373,9 @@ int sim_batch_create(const sim_model* m, int n_envs, int device, sim_batch** out
     const size_t nw = (size_t)std::max(pmask_words(m->dm), 1);
     HIPCHECK(hipMalloc(&B->d_pmask, nw * n_envs * sizeof(uint32_t)));
     HIPCHECK(hipMemset(B->d_pmask, 0, nw * n_envs * sizeof(uint32_t)));
+    const size_t ns = (size_t)std::max(m->desc.npair, 1) * 3 * n_envs;
+    HIPCHECK(hipMalloc(&B->d_sepax, ns * sizeof(float)));
+    HIPCHECK(hipMemset(B->d_sepax, 0, ns * sizeof(float)));
   }
   *out = B;
   return SIM_OK;
@@ -1378,6 +1389,7 @@ void sim_batch_free(sim_batch* b) {
   (void)hipFree(b->d_cbuf);
   (void)hipFree(b->d_ccount);
   (void)hipFree(b->d_pmask);
+  (void)hipFree(b->d_sepax);
   for (auto e : b->ev_pool) (void)hipEventDestroy(e);
   b->drop_graphs();
   if (b->cap_stream) (void)hipStreamDestroy(b->cap_stream);

@@ -676,6 +676,38 @@ def test_full_size_shard_invariance_and_determinism(gpu_lib):
     assert float(a["ncon"].sum()) / (n * T * 10) > 3.5
 
 
+def test_separating_axis_cache_is_exact(gpu_lib):
+    """k_collide's separating-axis cache (soarm_collide.h SepCache) only lets a pair skip an MPR
+    run whose answer would be "apart": a batch whose cache was warmed over 80 env-steps of the
+    headline workload (arm-cube and arm-table contacts present) and a fresh batch (empty cache)
+    loaded with the same state find bit-identical contacts and take a bit-identical env-step."""
+    import torch
+    from lerobot_mujoco_sim2real_amd import workloads as W
+    from lerobot_mujoco_sim2real_amd.sim import BatchSim
+    cm = W.model("contact")
+    n = 4096
+    ids = np.arange(n)
+    A = BatchSim(cm, n)
+    q0 = W.initial_qpos(cm, ids, 0)
+    A.reset(init_qpos=q0[:, :5], extra_qpos=q0, seed=0)
+    tab = {k: (torch.as_tensor(v, dtype=torch.float32, device=A.device) if isinstance(v, np.ndarray) else v)
+           for k, v in W.chirp_tables(ids, 0).items()}
+    for t in range(80):
+        A.step(W.chirp_action(tab, float(t), lib=torch))
+    B = BatchSim(cm, n)
+    for k in ("qpos", "qvel", "qacc_warmstart", "ctrl", "status", "ncon"):
+        getattr(B, k).copy_(getattr(A, k))
+    ca, na = A.contacts()
+    cb, nb = B.contacts()
+    assert torch.equal(na, nb) and torch.equal(ca, cb)
+    assert int(na.sum()) > 4 * n, "no arm contacts in the sample"
+    act = W.chirp_action(tab, 80.0, lib=torch)
+    oa, ob = A.step(act).clone(), B.step(act).clone()
+    assert torch.equal(oa, ob)
+    for k in ("qpos", "qvel", "ncon"):
+        assert torch.equal(getattr(A, k), getattr(B, k)), k
+
+
 def test_contact_env_step_late_states_full_size(gpu_lib):
     """The graph-captured 10-substep contact sim_step (the headline's launch sequence) against one
     oracle env-step, from late bench states (t = 100: the cube resting, arm-table and arm-cube
