@@ -1594,14 +1594,16 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
     for (int rr = 0; rr < 3; rr++) e01 = fma2(xq.fXp[rr], splat2(D[rr]), e01), yE[2] = fmaf(xq.fX2[rr], D[rr], yE[2]);
     yE[0] = e01.x, yE[1] = e01.y;
   };
-  auto yext_row_q = [&](f2& imp, auto coupled, float& famax) {
+  // varm = false: v_arm is not read again during these sweeps (frictionloss rows retired, no F
+  // slot), so E's v_arm update is deferred to one product with its total force change
+  auto yext_row_q = [&](f2& imp, auto coupled, float& famax, auto varm) {
     float df[4];
     qchain(yE[0], yE[1], yE[2], fE, xq.eMu, xq.eRp, xq.eNia01, xq.eNia23, xq.eA10, xq.eA2030, xq.eA2131, xq.eA32, xq.eHD01, xq.eHD23,
            imp, df);
     if constexpr (!decltype(coupled)::value) famax += (fabsf(df[0]) + fabsf(df[1])) + (fabsf(df[2]) + fabsf(df[3]));
     const float mu = xq.eMu;
     const float D[3] = {(df[0] + df[1]) + (df[2] + df[3]), mu * (df[0] - df[1]), mu * (df[2] - df[3])};
-    qvarm(xq.eWp, D);
+    if constexpr (decltype(varm)::value) qvarm(xq.eWp, D);
     if constexpr (decltype(coupled)::value) {  // this lane's block contact moves by X_own,E D
 #pragma unroll
       for (int qq = 0; qq < 3; qq++) {
@@ -1747,9 +1749,10 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       yext_setup(cE, cF);
       if constexpr (PK::value) yext_preload();
     }
-    // one sweep; ARM = false leaves out the arm's rows (see below).  Returns the
-    // improvement; famax gets the sum of |df| over the arm's rows.
-    auto sweep = [&](auto arm, float& famax) {
+    // one sweep; ARM = false leaves out the arm's rows, FRIC = false only its frictionloss
+    // rows (see below).  Returns the improvement; famax gets the sum of |df| over the arm's
+    // rows (ffmax: over its frictionloss rows).
+    auto sweep = [&](auto arm, auto fric, float& famax, float& ffmax) {
       // the arm's frictionloss rows and the cube block touch disjoint dofs (M is block
       // diagonal): the two Gauss-Seidel chains commute, so their rows are interleaved in
       // program order to give the (latency-bound) issue stream independent work; the
@@ -1760,21 +1763,22 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       // (NA = 6, FC = 4: rows {0,1} c0 {2} c1 {3,4} c2 {5} c3)
 #pragma unroll
       for (int j = 0; j < FC; j++) {
-        if constexpr (decltype(arm)::value) {
+        if constexpr (decltype(arm)::value && decltype(fric)::value) {
 #pragma unroll
           for (int i = (j * NA + FC - 1) / FC; i < ((j + 1) * NA + FC - 1) / FC; i++)
-            fric_row_y(i, improvement, ext, PK{}, famax);
+            fric_row_y(i, improvement, ext, PK{}, ffmax);
         }
         yblock_contact(j, imp_b, impq, dsel, coupled, PK{});
       }
       if constexpr (FC == 0) {
 #pragma unroll
-        for (int i = 0; i < NA; i++) fric_row_y(i, improvement, ext, PK{}, famax);
+        for (int i = 0; i < NA; i++) fric_row_y(i, improvement, ext, PK{}, ffmax);
       }
       if constexpr (PK::value) {
         if constexpr (decltype(ext)::value && decltype(coupled)::value) yblock_to_e(dsel);
         if constexpr (decltype(arm)::value && decltype(ext2)::value) yf_row_q(impq, famax);
-        if constexpr (decltype(arm)::value && decltype(ext)::value) yext_row_q(impq, coupled, famax);
+        if constexpr (decltype(arm)::value && decltype(ext)::value)
+          yext_row_q(impq, coupled, famax, std::integral_constant<bool, decltype(fric)::value || decltype(ext2)::value>{});
         improvement += impq.x + impq.y;
       } else {
         improvement += imp_b;
@@ -1795,21 +1799,70 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
     // common case: frictionloss rows saturated at +-frictionloss) leave the result bit for
     // bit equal to sweeping all rows.
     constexpr bool RETIRE = PK::value && FC > 0 && !decltype(coupled)::value;
+    // Frictionloss retirement (the extra-slot variants).  The arm's 6 frictionloss rows settle
+    // within a few sweeps (saturated at +-frictionloss, or holding), while an extra contact E
+    // (arm on the table, or the gripper on the cube) keeps its Gauss-Seidel chain going for
+    // tens of sweeps -- all ~95 of them when it touches the cube, which rules out the arm
+    // retirement above.  Once one sweep moves the frictionloss forces by at most ARM_RETIRE in
+    // total on every lane, the remaining sweeps leave those rows out and run E (and F) with
+    // the block: the same threshold argument as the arm retirement, applied to the rows that
+    // have settled.
+    constexpr bool FRETIRE = PK::value && FC > 0 && decltype(ext)::value;
     int it = 0;
-    bool done = false;
+    bool done = false, fret = false;
     for (; it < m.iterations; it++) {
-      float famax = 0.f;
-      if (sweep(std::true_type{}, famax) * scale < m.tolerance) {
+      float famax = 0.f, ffmax = 0.f;
+      if (sweep(std::true_type{}, std::true_type{}, famax, ffmax) * scale < m.tolerance) {
         done = true;
         break;
       }
       if constexpr (RETIRE) {
-        if (__all(famax <= ARM_RETIRE)) {
+        if (__all(famax + ffmax <= ARM_RETIRE)) {
 #ifdef SOARM_PHASE_PROF
           armstop = it + 1;
 #endif
           it++;
           break;
+        }
+      }
+      if constexpr (FRETIRE) {
+        if (__all(ffmax <= ARM_RETIRE)) {
+          fret = true;
+          it++;
+          break;
+        }
+      }
+    }
+    if constexpr (FRETIRE) {
+      // without F, nothing reads v_arm in these sweeps: E's steps move it once afterwards
+      float fE0[4];
+#pragma unroll
+      for (int ed = 0; ed < 4; ed++) fE0[ed] = fE[ed];
+      if (fret && !done)
+        for (; it < m.iterations; it++) {
+          float famax = 0.f, ffmax = 0.f;
+          if (sweep(std::true_type{}, std::false_type{}, famax, ffmax) * scale < m.tolerance) {
+            done = true;
+            break;
+          }
+          if constexpr (RETIRE) {
+            if (__all(famax <= ARM_RETIRE)) {
+#ifdef SOARM_PHASE_PROF
+              armstop = it + 1;
+#endif
+              it++;
+              break;
+            }
+          }
+        }
+      if constexpr (!decltype(ext2)::value) {
+        if (fret) {
+          float df[4];
+#pragma unroll
+          for (int ed = 0; ed < 4; ed++) df[ed] = fE[ed] - fE0[ed];
+          const float mu = xq.eMu;
+          const float D[3] = {(df[0] + df[1]) + (df[2] + df[3]), mu * (df[0] - df[1]), mu * (df[2] - df[3])};
+          qvarm(xq.eWp, D);
         }
       }
     }
@@ -1829,8 +1882,8 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       }
       if (!done)
         for (; it < m.iterations; it++) {
-          float unused = 0.f;
-          if (sweep(std::false_type{}, unused) * scale < m.tolerance) {
+          float unused = 0.f, unused2 = 0.f;
+          if (sweep(std::false_type{}, std::false_type{}, unused, unused2) * scale < m.tolerance) {
             done = true;
             break;
           }
