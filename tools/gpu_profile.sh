@@ -4,7 +4,7 @@
 # config the rocprofv3 kernel-trace summary of the bench command plus separate PMC passes
 # (FETCH_SIZE, WRITE_SIZE, SQ instruction/wait counters) on the hot kernels.
 # Every GPU step has its own time limit; a failure or timeout ends the script.
-#   usage: tools/gpu_profile.sh [tag] [--no-tests]
+#   usage: tools/gpu_profile.sh [tag] [--no-tests]   (PART=bench | PART=prof: only that half)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-r02}
@@ -19,11 +19,12 @@ step() {  # name, limit, command...
   echo "== $name rc=$rc" >&2
   if [ $rc -ne 0 ]; then exit $rc; fi
 }
-if [ "$2" != "--no-tests" ]; then
+if [ "$2" != "--no-tests" ] && [ "$PART" != "prof" ]; then
   step pytest 600 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1
   tail -2 $O/pytest_gpu.log
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
 fi
+if [ "$PART" != "prof" ]; then
 step bench_contact 600 python bench.py > $O/bench_contact.json 2> $O/bench_contact.err
 step bench_contact_newton 600 python bench.py --solver newton --no-cpu-baseline > $O/bench_contact_newton.json 2> $O/bench_contact_newton.err
 step bench_driver 300 python bench.py --steps 20 --warmup 5 > $O/bench_contact_steps20_warmup5.json 2> $O/bench_contact_drv.err
@@ -31,6 +32,10 @@ step bench_nocontact 300 python bench.py --config nocontact --steps 200 --warmup
 step bench_dr 600 python bench.py --config dr --steps 50 --warmup 5 --cpu-seconds 8 > $O/bench_dr.json 2> $O/bench_dr.err
 step bench_rollout 600 python bench.py --config rollout --steps 100 --warmup 5 --cpu-seconds 8 > $O/bench_rollout.json 2> $O/bench_rollout.err
 step bench_mpc 600 python bench.py --config mpc --cpu-seconds 8 > $O/bench_mpc.json 2> $O/bench_mpc.err
+step bench_mpc_dbkn 600 python bench.py --config mpc_dbkn --steps 30 --warmup 5 --cpu-seconds 8 > $O/bench_mpc_dbkn.json 2> $O/bench_mpc_dbkn.err
+step bench_plumbing 300 python bench.py --config plumbing > $O/bench_plumbing.json 2> $O/bench_plumbing.err
+fi
+[ "$PART" = "bench" ] && exit 0
 KRE="k_substep|k_collide|k_step|k_geom|k_mpc_step|k_bias"
 cd /tmp
 for SPEC in contact:contact: contact_newton:contact:--solver_newton mpc:mpc:; do
