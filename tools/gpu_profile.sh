@@ -36,6 +36,8 @@ step bench_mpc_dbkn 600 python bench.py --config mpc_dbkn --steps 30 --warmup 5 
 step bench_plumbing 300 python bench.py --config plumbing > $O/bench_plumbing.json 2> $O/bench_plumbing.err
 fi
 [ "$PART" = "bench" ] && exit 0
+# the multi-rank path with real kernels: 2 self-launched ranks sharing the box's one GPU (gloo)
+step bench_gloo2 300 python bench.py --gpus 2 --dist-backend gloo --steps 10 --warmup 2 --no-cpu-baseline --no-steady --no-other-solver > $O/bench_gloo2.json 2> $O/bench_gloo2.err
 KRE="k_substep|k_collide|k_step|k_geom|k_mpc_step|k_bias"
 cd /tmp
 for SPEC in contact:contact: contact_newton:contact:--solver_newton mpc:mpc:; do
