@@ -511,7 +511,9 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (Philox-keyed initial states / chirp inputs per global env id)",
-            "config": {"workload": cfg["desc"], "config": name, "envs_per_gpu": n, "global_envs": total_envs,
+            "config": {"workload": (cfg["desc"] if args.solver == "pgs" else
+                                    cfg["desc"].replace("PGS (config 3", "Newton (config 3 scene")),
+                       "config": name, "envs_per_gpu": n, "global_envs": total_envs,
                        "frame_skip": 10, "substeps_per_s": value * 10,
                        "contacts_per_env_substep": contacts,
                        "solver": ("PGS (iterations 100, tol 1e-8, scale 1/(meaninertia nv))" if args.solver == "pgs"
