@@ -67,6 +67,15 @@ struct NewtonRows {
   // (1/R of contacts and limits: the record's F_IARD / L_IARD slot, written for Newton by the
   // row build; divisions by R are multiplications by it throughout)
   int nlim, nl, ncon;
+  // wave-uniform: some lane of the wave has a contact owned by the arm (resp. free-body)
+  // subsystem; a subsystem without one skips its contact loops (set by newton_solve)
+  bool arm_c = true, free_c = true;
+  template <int LO, int HI>
+  DEVI bool has_contacts() const {
+    if constexpr (LO == 0 && HI == NV) return true;
+    else if constexpr (HI == NA) return arm_c;
+    else return free_c;
+  }
 
   // does the subsystem over dofs [LO, HI) own a contact of class fl?  (full range: all of them)
   template <int LO, int HI>
@@ -156,7 +165,7 @@ struct NewtonRows {
               H[hidx(i - LO, j - LO)] += jc[0][i] * kj[0][j] + jc[1][i] * kj[1][j] + jc[2][i] * kj[2][j];
         }
       };
-      for (int c = ql(); c < nl; c += QL) {
+      for (int c = ql(); has_contacts<LO, HI>() && c < nl; c += QL) {
         const int fl = (int)L.at(c, F_FLAGS);
         if constexpr (LO == 0 && HI == NV) {
           mine = true;
@@ -272,7 +281,7 @@ struct NewtonRows {
       (void)fr;
     }
     if constexpr (CON) {
-      for (int c = ql(); c < nl; c += QL) {
+      for (int c = ql(); has_contacts<LO, HI>() && c < nl; c += QL) {
         if (!owns<LO, HI>((int)L.at(c, F_FLAGS))) continue;
         float ya[3] = {0.f, 0.f, 0.f}, yp[3] = {0.f, 0.f, 0.f};
 #pragma unroll
@@ -316,7 +325,7 @@ struct NewtonRows {
     if constexpr (CON) {
       float c1 = 0.f, c2 = 0.f, cl = -3.0e38f, cr_ = 3.0e38f;
       bool mine = false;
-      for (int c = ql(); c < nl; c += QL) {
+      for (int c = ql(); has_contacts<LO, HI>() && c < nl; c += QL) {
         if (!owns<LO, HI>((int)L.at(c, F_FLAGS))) continue;
         mine = true;
         const float D = L.at(c, F_IARD);
@@ -538,6 +547,17 @@ DEVI int newton_solve(Sim<NA, NF>& S, const NewtonRows<NA, NF, CON>& R) {
     for (int c = 0; c < LDS_CON; c++)
       coupled |= __any(c < R.nl && (int)R.L.at(c < R.nl ? c : 0, F_FLAGS) == (TOUCH_ARM | TOUCH_FREE));
   }
+  NewtonRows<NA, NF, CON> Rs = R;  // (+ the per-subsystem contact flags)
+  if constexpr (NF > 0 && CON) {
+    bool arm = false, fre = false;
+#pragma unroll
+    for (int c = 0; c < LDS_CON; c++) {
+      const int fl = c < R.nl ? (int)R.L.at(c, F_FLAGS) : 0;
+      arm |= __any(c < R.nl && !(fl & TOUCH_FREE));
+      fre |= __any(c < R.nl && fl == TOUCH_FREE);
+    }
+    Rs.arm_c = arm, Rs.free_c = fre;
+  }
   int it, nls = 0;
   long long ncyc[4] = {0, 0, 0, 0};
 #ifdef SOARM_PHASE_PROF
@@ -550,11 +570,11 @@ DEVI int newton_solve(Sim<NA, NF>& S, const NewtonRows<NA, NF, CON>& R) {
     if (coupled) {
       it = newton_range<0, NV>(S, R, a, jtf, nls, ncyc);
     } else {
-      it = newton_range<0, NA>(S, R, a, jtf, nls, ncyc);
+      it = newton_range<0, NA>(S, Rs, a, jtf, nls, ncyc);
 #ifdef SOARM_PHASE_PROF
       it_arm = it, nls_arm = nls;
 #endif
-      it += newton_range<NA, NV>(S, R, a, jtf, nls, ncyc);
+      it += newton_range<NA, NV>(S, Rs, a, jtf, nls, ncyc);
     }
   }
 #ifdef SOARM_PHASE_PROF
