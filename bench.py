@@ -433,6 +433,8 @@ def main():
         capped = PEAK_FP32_TFLOPS * min(1.0, waves / 1024)
         roof = {"bound": "valu", "achieved": achieved, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                 "frac": achieved / PEAK_FP32_TFLOPS, "traffic": traffic,
+                "traffic_source": ("copied from profiles/pmc_traffic.json (rocprofv3 PMC passes of this "
+                                   "workload, guide-corrected); not measured in this run") if traffic else None,
                 "lanes_per_env": lanes, "waves_per_launch": waves, "occupancy_capped_peak": capped,
                 "frac_of_capped": achieved / capped,
                 "kernel": kind, "avg_launch_ms": avg_ms, "launches": cnt,

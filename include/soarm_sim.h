@@ -36,6 +36,11 @@
 extern "C" {
 #endif
 
+/* ---- ABI version: the leading (struct_size, abi_version) of every by-pointer struct below is
+   checked by the entry point that reads it, so a caller built against another layout gets
+   SIM_E_ARG instead of a misread.  Bumped with any layout change. ---- */
+#define SIM_ABI_VERSION 2
+
 /* ---- capacity of the compiled model (MuJoCo mjModel subset) ---- */
 #define SIM_MAXBODY 12
 #define SIM_MAXJNT 12
@@ -77,6 +82,8 @@ enum {
  * the oracle read the same numbers.  Quaternions are (w, x, y, z).
  */
 typedef struct sim_model_desc {
+  int32_t struct_size;   /* sizeof(sim_model_desc) as the caller compiled it */
+  int32_t abi_version;   /* SIM_ABI_VERSION */
   int32_t nbody, njnt, nq, nv, nu, ngeom, nsite, npair;
   int32_t nhullvert, nhulladj; /* lengths of the hull arrays passed beside */
 
@@ -90,8 +97,8 @@ typedef struct sim_model_desc {
   int32_t iterations;    /* solver: max PGS sweeps / Newton iterations */
   int32_t disable_contact; /* mjDSBL_CONTACT */
   int32_t disable_eulerdamp;
-  int32_t solver;        /* mjtSolver: SIM_SOL_PGS (the kernels) or SIM_SOL_NEWTON (MuJoCo's
-                            default; CPU oracle only — sim_model_create rejects it) */
+  int32_t solver;        /* mjtSolver: SIM_SOL_PGS (soarm_pgs.h) or SIM_SOL_NEWTON (MuJoCo's
+                            default, soarm_newton.h); SIM_SOL_CG is rejected (SIM_E_MODEL) */
 
   /* bodies (0 = world) */
   int32_t body_parentid[SIM_MAXBODY];
@@ -182,6 +189,8 @@ typedef struct sim_model_desc {
 
 /* DLS-IK options (dm_control qpos_from_site_pose semantics) */
 typedef struct sim_ik_opts {
+  int32_t struct_size;        /* sizeof(sim_ik_opts) */
+  int32_t abi_version;        /* SIM_ABI_VERSION */
   double tol;                 /* 1e-6 */
   double regularization_threshold; /* 0.1 */
   double regularization_strength;  /* 1e-2 */
@@ -231,7 +240,7 @@ void sim_model_free(sim_model* m);
 /* Compiled-model files, the MjModel.from_xml_path (SOARM101_Env.py:34) of a C / C++ caller with no
    Python at run time: mjcf.py compiles the MJCF once (CompiledModel.save) and writes the desc and
    hull arrays; sim_model_load reads them back and calls sim_model_create.  Format (little endian):
-   "SOARMMDL" | u32 version (1) | u32 sizeof(sim_model_desc) | desc | f32 hull_vert[nhullvert][3] |
+   "SOARMMDL" | u32 version (2) | u32 sizeof(sim_model_desc) | desc | f32 hull_vert[nhullvert][3] |
    i32 hull_adr[nhullvert+1] (absent when nhullvert = 0) | i32 hull_adj[nhulladj].  A file of
    another version or desc size, or a short file, is rejected (SIM_E_ARG). */
 int sim_model_save(const sim_model_desc* desc, const float* hull_vert, const int32_t* hull_adr,

@@ -18,6 +18,16 @@ GEOM_PLANE, GEOM_SPHERE, GEOM_BOX, GEOM_MESH = 0, 2, 6, 7
 ST_BADQPOS, ST_BADQVEL, ST_BADQACC, ST_CONOVERFLOW = 1, 2, 4, 8
 
 i32, f64 = C.c_int32, C.c_double
+ABI_VERSION = 2  # SIM_ABI_VERSION (include/soarm_sim.h)
+
+
+class _Versioned(C.Structure):
+    """A by-pointer ABI struct: leading (struct_size, abi_version), filled on construction."""
+
+    def __init__(self, *args, **kw):
+        super().__init__(0, 0, *args, **kw)
+        self.struct_size = C.sizeof(type(self))
+        self.abi_version = ABI_VERSION
 
 
 def _a(t, *dims):
@@ -26,8 +36,9 @@ def _a(t, *dims):
     return t
 
 
-class ModelDesc(C.Structure):
+class ModelDesc(_Versioned):
     _fields_ = [
+        ("struct_size", i32), ("abi_version", i32),
         ("nbody", i32), ("njnt", i32), ("nq", i32), ("nv", i32), ("nu", i32),
         ("ngeom", i32), ("nsite", i32), ("npair", i32), ("nhullvert", i32), ("nhulladj", i32),
         ("timestep", f64), ("gravity", _a(f64, 3)), ("impratio", f64), ("tolerance", f64),
@@ -82,8 +93,9 @@ class ModelDesc(C.Structure):
     ]
 
 
-class IkOpts(C.Structure):
+class IkOpts(_Versioned):
     _fields_ = [
+        ("struct_size", i32), ("abi_version", i32),
         ("tol", f64), ("regularization_threshold", f64), ("regularization_strength", f64),
         ("max_update_norm", f64), ("progress_thresh", f64),
         ("max_steps", i32), ("site", i32), ("ndof", i32), ("_pad", i32), ("rot_weight", f64),

@@ -6,14 +6,17 @@ Reference: ``models/KoopmanBase.py:12-60`` (``Koopmanlinear``, the ``DKUC`` mode
 is kept: the encoder ``x_encoder(x) = cat([x, MLP(x)])``, the Koopman matrices ``lA``
 (Nkoopman x Nkoopman, initialised as 0.9 x an orthogonalised Gaussian draw) and ``lB``
 (Nkoopman x u_dim), and the fixed decoder ``lC = [I | 0]``.  Training the model (``train.py``,
-``models/losses.py``) is out of scope; a user's own trained state_dict loads with
-``load_state_dict`` as usual.
+``models/losses.py``) is out of scope.  Parameter names are the reference's
+(``x_encode_net.linear_{i}``, ``lA``, ``lB``, ``lC``, DBKN's ``H``), so a state_dict the reference
+saved loads with ``load_state_dict(..., strict=True)`` (``tests/test_koopman_mpc.py``).
 
 The bilinear ``DBKN`` model (``KoopmanBlinear``, ``:62-110``) adds ``H (z ⊗ u)`` to the step;
 the MPC linearises it at the frame's lifted state, ``B_total = Bd + Σ_j z0_j Ĥ_j``
 (``MPC_Controler.py:46-63``), so its QP differs per env and frame: :func:`bilinear_first_move`
 solves those QPs batched in float64 on the device.
 """
+from collections import OrderedDict
+
 import numpy as np
 import torch
 from torch import nn
@@ -26,12 +29,14 @@ class Koopmanlinear(nn.Module):
         super().__init__()
         self.x_dim, self.u_dim = x_dim, u_dim
         self.Nkoopman = encode_layers[-1] + x_dim
-        mods = []
+        # named modules linear_{i} / relu_{i} as KoopmanBase.py:20-27, so the reference's saved
+        # state_dict (x_encode_net.linear_0.weight, ...) loads strictly (Koopman_MPC.py:262-265)
+        mods = OrderedDict()
         for i, (a, b) in enumerate(zip(encode_layers[:-1], encode_layers[1:])):
-            mods.append(nn.Linear(a, b))
+            mods[f"linear_{i}"] = nn.Linear(a, b)
             if i + 2 < len(encode_layers):
-                mods.append(nn.ReLU())
-        self.x_encode_net = nn.Sequential(*mods)
+                mods[f"relu_{i}"] = nn.ReLU()
+        self.x_encode_net = nn.Sequential(mods)
         self.u_encode_net = nn.Identity()
         nk = self.Nkoopman
         self.lA = nn.Linear(nk, nk, bias=False)

@@ -413,25 +413,6 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
   if (e >= n) return;
   PHASE_T(t0);
   const DModel& m = *dm;
-#ifdef SOARM_FUSE_COLLIDE
-  // experiment: mj_collision of this env on its own lanes (pairs split over the
-  // quad) instead of the (env, pair)-parallel k_collide launch before this one
-  if (ccount != nullptr) {
-    for (int p = (int)threadIdx.x % lpe<NF>(); p < m.npair; p += lpe<NF>()) {
-      GeomPose P1, P2;
-      load_pose(gpose_in, n, e, m.pair_geom1[p], P1);
-      load_pose(gpose_in, n, e, m.pair_geom2[p], P2);
-      PairOut o{const_cast<float*>(cbuf), n, e, m.pair_slot[p], m.pair_cap[p], 0};
-      collide_pair(m, p, P1, P2, o);
-      if (o.n > 0) {
-        atomicOr(&pmask[(size_t)(p >> 5) * n + e], 1u << (p & 31));
-        const int cq = m.pair_cq[p];
-        if (cq >= 0) atomicOr(&pmask[(size_t)((m.npair + 31) >> 5) * n + e], (uint32_t)(o.n - 1) << (2 * cq));
-      }
-    }
-    __threadfence_block();
-  }
-#endif
   Sim<NA, NF> S(dm, pp.mass_scale ? pp.mass_scale[e] : 1.f, pp.friction ? pp.friction[e] : -1.f,
                 pp.damping_scale ? pp.damping_scale[e] : 1.f);
   load_state(S, st, n, e);
@@ -1128,15 +1109,26 @@ static int upload_model(const sim_model* m, int device, DModel** out) {
   *out = D->d_model;
   return SIM_OK;
 }
+// the (struct_size, abi_version) header every by-pointer struct carries (soarm_sim.h)
+template <class T>
+static int check_struct(const T* p, const char* what) {
+  if (p->struct_size != (int32_t)sizeof(T) || p->abi_version != SIM_ABI_VERSION)
+    return fail(SIM_E_ARG, std::string(what) + ": struct_size / abi_version do not match this library (built for abi " +
+                               std::to_string(SIM_ABI_VERSION) + ", sizeof " + std::to_string(sizeof(T)) + ")");
+  return SIM_OK;
+}
+
 // ============================================================== C ABI
 extern "C" {
 
 const char* sim_last_error(void) { return g_err.c_str(); }
-const char* sim_version(void) { return "soarm_sim 0.1.0 gfx950"; }
+const char* sim_version(void) { return "soarm_sim 0.2.0 gfx950 (abi 2)"; }
+
 
 int sim_model_create(const sim_model_desc* desc, const float* hull_vert, const int32_t* hull_adr,
                      const int32_t* hull_adj, sim_model** out) {
   if (!desc || !out) return fail(SIM_E_ARG, "null argument");
+  if (int rc = check_struct(desc, "sim_model_desc")) return rc;
   sim_model* M = new sim_model();
   M->desc = *desc;
   int rc = validate_and_build(*desc, M);
@@ -1290,11 +1282,12 @@ int sim_model_create(const sim_model_desc* desc, const float* hull_vert, const i
 
 // compiled-model files (soarm_sim.h): the desc and hull arrays as sim_model_create takes them
 static const char kModelMagic[8] = {'S', 'O', 'A', 'R', 'M', 'M', 'D', 'L'};
-static const uint32_t kModelVersion = 1;
+static const uint32_t kModelVersion = 2;  // 2: desc carries (struct_size, abi_version)
 
 int sim_model_save(const sim_model_desc* desc, const float* hull_vert, const int32_t* hull_adr,
                    const int32_t* hull_adj, const char* path) {
   if (!desc || !path) return fail(SIM_E_ARG, "null argument");
+  if (int rc = check_struct(desc, "sim_model_desc")) return rc;
   if (desc->nhullvert < 0 || desc->nhulladj < 0) return fail(SIM_E_ARG, "bad hull sizes");
   if (desc->nhullvert > 0 && (!hull_vert || !hull_adr || !hull_adj)) return fail(SIM_E_ARG, "hull arrays missing");
   FILE* f = fopen(path, "wb");
@@ -1466,14 +1459,12 @@ int sim_step(sim_batch* b, const sim_state* s, const float* action, int frame_sk
       }
       prof_mark(b, -1, q);
       for (int sub = 0; sub < frame_skip; sub++) {
-#ifndef SOARM_FUSE_COLLIDE
         if (np > 0) {
           prof_mark(b, 1, q);
           const TraceRange tr_("collide");
           launch_collide(b, q, nullptr);
           prof_mark(b, -1, q);
         }
-#endif
         const bool last = sub == frame_skip - 1;
         const TraceRange tr_("substep");
         prof_mark(b, 2, q);
@@ -1652,6 +1643,8 @@ int sim_observe(sim_batch* b, const sim_state* s, float* obs, void* stream) {
 int sim_ik_dls_pose(sim_batch* b, const float* target, const float* target_quat, float* q, int32_t* ok,
                     int32_t* iters, const sim_ik_opts* opts, void* stream) {
   const TraceRange tr_("sim_ik_dls");
+  if (opts)
+    if (int rc = check_struct(opts, "sim_ik_opts")) return rc;
   if (!b || !target || !q || !opts) return fail(SIM_E_ARG, "null argument");
   if (opts->ndof < 1 || opts->ndof > 6 || opts->max_steps < 0) return fail(SIM_E_ARG, "bad ik options");
   hipStream_t st = (hipStream_t)stream;

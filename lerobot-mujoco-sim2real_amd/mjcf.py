@@ -290,9 +290,9 @@ def compile_mjcf(xml_path=SCENE_XML, kv=None, disable_contact=False, iterations=
                  solver="PGS"):
     """Compile an MJCF file into a :class:`CompiledModel`.
 
-    solver: "PGS" (what the HIP kernels run, per BASELINE.json north_star) or "Newton"
-    (MuJoCo's default, which the reference scene's missing <option> selects; only the CPU
-    oracle runs it — sim_model_create rejects it)."""
+    solver: "PGS" (the north star's and BASELINE config 3's solver, the headline) or "Newton"
+    (MuJoCo's default, which the reference scene's missing <option> selects): both run on the
+    device (soarm_pgs.h / soarm_newton.h) and in the oracle; only CG is rejected."""
     if not os.path.exists(xml_path):
         raise FileNotFoundError(f"MuJoCo XML file not found: {xml_path}")
     root = _load_tree(xml_path)

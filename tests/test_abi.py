@@ -82,11 +82,37 @@ def test_model_file_round_trip_and_rejects(tmp_path):
         return lib.sim_last_error()
 
     assert b"not a compiled" in rejected(b"XOARMMDL" + raw[8:], "magic")
-    assert b"version" in rejected(raw[:8] + (2).to_bytes(4, "little") + raw[12:], "version")
+    assert b"version" in rejected(raw[:8] + (1).to_bytes(4, "little") + raw[12:], "version")
     assert b"version" in rejected(raw[:12] + (C.sizeof(d) + 4).to_bytes(4, "little") + raw[16:], "layout")
     assert b"truncated" in rejected(raw[:-4], "truncated")
     assert b"truncated" in rejected(raw + b"\0", "trailing bytes")
     assert lib.sim_model_load(str(tmp_path / "missing.soarm").encode(), C.byref(model)) == -1
+
+
+def test_struct_header_is_checked():
+    """Every by-pointer struct leads with (struct_size, abi_version) (SIM_ABI_VERSION): a caller
+    built against another layout gets SIM_E_ARG from sim_model_create / sim_model_save /
+    sim_ik_dls instead of a field-by-field misread."""
+    import soarm_pkg  # noqa: F401
+    from lerobot_mujoco_sim2real_amd import mjcf
+    hdr = open(os.path.join(ROOT, "include", "soarm_sim.h")).read()
+    assert f"#define SIM_ABI_VERSION {abi.ABI_VERSION}" in hdr
+    lib = abi.load_lib()
+    assert f"abi {abi.ABI_VERSION}" in lib.sim_version().decode()
+    cm = mjcf.compile_mjcf(mjcf.SCENE_XML)
+    assert cm.desc.struct_size == C.sizeof(abi.ModelDesc) and cm.desc.abi_version == abi.ABI_VERSION
+    for field, val in (("struct_size", C.sizeof(abi.ModelDesc) - 8), ("abi_version", abi.ABI_VERSION - 1)):
+        d = abi.ModelDesc.from_buffer_copy(cm.desc)
+        setattr(d, field, val)
+        model = C.c_void_p()
+        assert lib.sim_model_create(C.byref(d), None, None, None, C.byref(model)) == -1 and not model
+        assert b"struct_size / abi_version" in lib.sim_last_error()
+        assert lib.sim_model_save(C.byref(d), None, None, None, b"/nonexistent/x") == -1
+    o = abi.IkOpts(1e-6, 0.1, 1e-2, 2.0, 20.0, 100, 0, 5, 0, 0.5)
+    assert o.struct_size == C.sizeof(abi.IkOpts) and o.tol == 1e-6 and o.rot_weight == 0.5
+    o.struct_size -= 8  # the r03 layout (no rot_weight)
+    assert lib.sim_ik_dls(None, None, None, None, None, C.byref(o), None) == -1
+    assert b"sim_ik_opts" in lib.sim_last_error()
 
 
 def test_model_validation_rejects_unsupported():

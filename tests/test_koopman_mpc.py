@@ -160,6 +160,50 @@ def test_bilinear_first_move_equals_oracle(kind):
     assert np.abs(g).max() < 1e-5 * max(1.0, abs(KO.cost(A, Bt, v, z0[0], ref[0], up[0], kind)))
 
 
+def _reference_state_dict_layout(layers, x_dim, u_dim, bilinear):
+    """{key: shape} of the state_dict the reference's classes save, restated from their source:
+    x_encode_net is nn.Sequential(OrderedDict(linear_i, relu_i)) (models/KoopmanBase.py:20-27;
+    ReLU has no parameters), lA [Nk, Nk] (:31), lB [Nk, u_dim] (:35), lC [x_dim, Nk] (:38),
+    DBKN's H [Nk, Nk*u_dim] (:66); Nk = layers[-1] + x_dim (:16)."""
+    nk = layers[-1] + x_dim
+    keys = {}
+    for i in range(len(layers) - 1):
+        keys[f"x_encode_net.linear_{i}.weight"] = (layers[i + 1], layers[i])
+        keys[f"x_encode_net.linear_{i}.bias"] = (layers[i + 1],)
+    keys["lA.weight"] = (nk, nk)
+    keys["lB.weight"] = (nk, u_dim)
+    keys["lC.weight"] = (x_dim, nk)
+    if bilinear:
+        keys["H.weight"] = (nk, nk * u_dim)
+    return keys
+
+
+@pytest.mark.parametrize("model", ["DKUC", "DBKN"])
+def test_reference_state_dict_loads_strict(model):
+    """Koopman_MPC.py:262-265 — init_model(args); model.double(); model.load_state_dict(sd) —
+    runs unchanged against this build's classes with a state_dict of the reference's key set
+    (strict loading: no missing or unexpected keys), and the loaded weights are the ones used."""
+    import torch
+    from lerobot_mujoco_sim2real_amd.args import Args
+    from lerobot_mujoco_sim2real_amd.control.koopman import init_model
+    args = Args()
+    args.model = model
+    layout = _reference_state_dict_layout(list(args.layers), args.x_dim, args.u_dim, model == "DBKN")
+    g = torch.Generator().manual_seed(5)
+    sd = {k: torch.randn(s, generator=g, dtype=torch.float64) for k, s in layout.items()}
+    net = init_model(args)
+    net.double()
+    res = net.load_state_dict(sd)  # strict=True is the default, as in the reference's call
+    assert not res.missing_keys and not res.unexpected_keys
+    assert {k: tuple(v.shape) for k, v in net.state_dict().items()} == layout
+    W0, b0 = net.encoder_layers()[0]
+    np.testing.assert_array_equal(W0, sd["x_encode_net.linear_0.weight"].numpy())
+    np.testing.assert_array_equal(b0, sd["x_encode_net.linear_0.bias"].numpy())
+    x = torch.as_tensor(sample_states(4))
+    np.testing.assert_allclose(net.x_encoder(x).detach().numpy(), KO.encode(net.encoder_layers(), x.numpy()),
+                               rtol=1e-13, atol=1e-13)
+
+
 def test_koopman_create_validates_before_device():
     """Bad shapes -> SIM_E_MODEL; a good controller without a GPU -> SIM_E_NODEVICE (no CPU path)."""
     from lerobot_mujoco_sim2real_amd import abi, build
