@@ -305,12 +305,26 @@ class SOARM101DataGenerator:
         return local.transpose(0, 1).double().cpu().numpy()
 
     def _split(self, path, split, samples, steps, input_type):
-        """One dataset file: load it if cached, else generate (sharded under torch.distributed)."""
+        """One dataset file: load it if cached, else generate (sharded under torch.distributed).
+
+        Under torch.distributed rank 0 alone decides whether the cache exists and broadcasts the
+        decision, so every rank takes the same branch into (or past) the gather collective.
+        Gather mode: rank 0 writes the file, then every rank holds the full dataset (it loads
+        the file after a barrier, or -- when the file is not visible on some rank, e.g. a
+        node-local filesystem -- receives the array from rank 0).  Shard-file mode: every rank
+        holds its own shard's rows."""
         from .. import shard
 
         rank, world = _dist()
-        if os.path.exists(path):
-            return np.load(path)
+        if world > 1:
+            import torch.distributed as dist
+            flag = [os.path.exists(path) if rank == 0 else None]
+            dist.broadcast_object_list(flag, src=0)
+            cached = bool(flag[0])
+        else:
+            cached = os.path.exists(path)
+        if cached and (world == 1 or not self.shard_files):
+            return np.load(path) if world == 1 else self._everyone_loads(path, None)
         seed = self.split_seed(split)
         if world > 1 and self.shard_files:
             base = path[:-4] if path.endswith(".npy") else path
@@ -330,7 +344,24 @@ class SOARM101DataGenerator:
         data = self.generate_physics_based_data(samples, steps, input_type, seed=seed)
         if rank == 0:
             np.save(path, data)
-        return data
+        return data if world == 1 else self._everyone_loads(path, data)
+
+    @staticmethod
+    def _everyone_loads(path, data):
+        """Collective: every rank returns rank 0's dataset `path` (rank 0 passes `data`, or None to
+        load it).  Ranks that see the file load it after the barrier that follows rank 0's save;
+        if any rank cannot see it, rank 0 broadcasts the array instead."""
+        import torch.distributed as dist
+
+        dist.barrier()
+        seen = [None] * dist.get_world_size()
+        dist.all_gather_object(seen, os.path.exists(path))
+        rank = dist.get_rank()
+        if all(seen):
+            return data if (rank == 0 and data is not None) else np.load(path)
+        box = [(data if data is not None else np.load(path)) if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        return box[0]
 
     def generate_and_save_data(self):
         """File cache / resume as the reference (``:138-181``); each split keyed by its name."""

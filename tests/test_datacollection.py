@@ -105,14 +105,24 @@ def _port():
     return p
 
 
-def _dataset_worker(rank, world, port, root, shard_files):
+def _dataset_worker(rank, world, port, root, shard_files, out=None, runs=1, hide=False):
+    """One rank of a world-`world` dataset build; with `out`, each rank saves what its generator
+    holds after every run (run 0 builds the files, run 1 finds them cached).  `hide`: rank 1
+    sees no dataset file (a node-local filesystem)."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LOCAL_RANK=str(rank))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     DC.SOARM101DataGenerator.rollout_device = _mock_rollout
+    if hide and rank == 1:
+        real = os.path.exists
+        os.path.exists = lambda p: False if str(p).endswith(".npy") else real(p)
     a = Args(["--data_root", root, "--train_samples", "37", "--train_steps", "3", "--test_samples", "11",
               "--test_steps", "4"])
-    g = DC.SOARM101DataGenerator(a, max_envs=8, shard_files=shard_files)
-    g.generate_and_save_data()
+    for run in range(runs):
+        g = DC.SOARM101DataGenerator(a, max_envs=8, shard_files=shard_files)
+        g.generate_and_save_data()
+        if out is not None:
+            np.savez(os.path.join(out, f"rank{rank}_run{run}.npz"), train=g.train_data, val=g.val_data,
+                     **{f"test_{k}": v for k, v in g.test_data_dict.items()})
     dist.barrier()
     dist.destroy_process_group()
 
@@ -136,10 +146,29 @@ def test_sharded_dataset_equals_single_rank(tmp_path, monkeypatch):
     want = {"train": ref.train_data, "val": ref.val_data, **{f"test_{k}": v for k, v in ref.test_data_dict.items()}}
     # splits are distinct streams
     assert not np.array_equal(want["val"][:, 0], want["train"][:11, 0])
-    mp.spawn(_dataset_worker, args=(2, _port(), str(tmp_path / "gather"), False), nprocs=2, join=True)
+    out = tmp_path / "held"
+    out.mkdir()
+    mp.spawn(_dataset_worker, args=(2, _port(), str(tmp_path / "gather"), False, str(out), 2), nprocs=2, join=True)
     d = tmp_path / "gather" / "SOARM101" / "data"
     for k, nm in names.items():
         np.testing.assert_array_equal(np.load(d / f"{nm}.npy"), want[k])
+    # in gather mode every rank holds the whole dataset, on the first run (built and
+    # gathered) and on the rerun (cached) alike -- never None on rank 1
+    for r in range(2):
+        for run in range(2):
+            held = np.load(out / f"rank{r}_run{run}.npz")
+            for k in names:
+                np.testing.assert_array_equal(held[k], want[k])
+    # a rank that cannot see the file (node-local storage) receives the arrays from rank 0
+    out2 = tmp_path / "held2"
+    out2.mkdir()
+    mp.spawn(_dataset_worker, args=(2, _port(), str(tmp_path / "hidden"), False, str(out2), 2, True), nprocs=2,
+             join=True)
+    for r in range(2):
+        for run in range(2):
+            held = np.load(out2 / f"rank{r}_run{run}.npz")
+            for k in names:
+                np.testing.assert_array_equal(held[k], want[k])
     mp.spawn(_dataset_worker, args=(2, _port(), str(tmp_path / "files"), True), nprocs=2, join=True)
     d = tmp_path / "files" / "SOARM101" / "data"
     for k, nm in names.items():

@@ -636,6 +636,48 @@ def test_vecenv_api(gpu_lib):
     assert tuple(o.shape) == (32, 8)
 
 
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_config1_single_env_zero_action_1000_steps(gpu_lib, seed):
+    """BASELINE.json configs[0]: one SOARM101Env (reference scene: arm + table, contacts on),
+    reset from a seeded initial state, zero action, 1000 env-steps (SOARM101_Env.py:77-142),
+    every step through the single-env numpy API, against the fp64 oracle run the same way.
+
+    Under zero action the velocity servo only damps: the arm sinks under gravity onto the table
+    within ~1 s and then rests on it, still chattering (kv h / M ~ 3) and creeping.  Per step the
+    obs must shadow the oracle within 10x the envelope of fp32-sized perturbations of the oracle
+    itself (its running max: the single-env envelope dips at random steps) plus 2e-4; the final
+    resting pose is held tighter: the gripper's height above the table within 2e-4 of the
+    oracle's, and the whole final obs within 10x the final envelope + 1e-3."""
+    from lerobot_mujoco_sim2real_amd.SOARM101 import SOARM101Env
+    env = SOARM101Env()
+    T = 1000
+    init = np.r_[np.random.default_rng(seed).uniform(-0.3, 0.3, 5), np.zeros(5)]
+    init = init.astype(np.float32).astype(np.float64)
+    og, _ = env.reset(options={"initial_state": init})
+    orc = Oracle(env.model)
+    a, b = orc.new_state(1), orc.new_state(1)
+    oa = orc.reset(a, init_qpos=init[None, :5], init_qvel=init[None, 5:])
+    orc.reset(b, init_qpos=init[None, :5], init_qvel=init[None, 5:])
+    np.testing.assert_allclose(og, oa[0], atol=2e-6)
+    zero = np.zeros(5, np.float32)
+    err, envl = np.zeros(T), np.zeros(T)
+    for t in range(T):
+        og, r, term, trunc, info = env.step(zero)
+        assert og.dtype == np.float32 and r == 0.0 and not term and not trunc and info == {}
+        oa, ob = orc.step(a, np.zeros((1, 5))), orc.step(b, np.zeros((1, 5)))
+        for k in ("qpos", "qvel", "warm"):
+            b[k][:] = b[k].astype(np.float32)
+        err[t] = np.abs(og - oa[0]).max()
+        envl[t] = np.abs(oa[0] - ob[0]).max()
+    run = np.maximum.accumulate(envl)
+    bad = np.nonzero(err > 10 * run + 2e-4)[0]
+    assert bad.size == 0, ("shadowing", bad[:5], err[bad[:5]], run[bad[:5]])
+    assert abs(float(og[2]) - float(oa[0, 2])) < 2e-4, (og[2], oa[0, 2])   # resting on the table
+    assert float(og[2]) < 0.02                                          # (it did come to rest)
+    assert np.abs(og - oa[0]).max() < 10 * envl[-20:].max() + 1e-3
+    assert int(env.sim.status.cpu().numpy()[0]) == int(a["status"][0]) == 0
+
+
 def test_full_size_shard_invariance_and_determinism(gpu_lib):
     """The headline workload at its full size (4096 envs, pick scene, chirp inputs, 25
     env-steps), checked through size-independent properties (no oracle at this size):
