@@ -58,6 +58,9 @@ enum { SIM_JNT_FREE = 0, SIM_JNT_BALL = 1, SIM_JNT_SLIDE = 2, SIM_JNT_HINGE = 3 
 enum { SIM_GEOM_PLANE = 0, SIM_GEOM_SPHERE = 2, SIM_GEOM_BOX = 6, SIM_GEOM_MESH = 7 };
 /* mjtSolver values */
 enum { SIM_SOL_PGS = 0, SIM_SOL_CG = 1, SIM_SOL_NEWTON = 2 };
+/* convex-convex narrowphase: libccd MPR (MuJoCo's classic path) or MuJoCo's native GJK/EPA
+   ("nativeccd", the default of current releases) */
+enum { SIM_CCD_MPR = 0, SIM_CCD_NATIVE = 1 };
 
 /* error codes */
 enum {
@@ -99,6 +102,8 @@ typedef struct sim_model_desc {
   int32_t disable_eulerdamp;
   int32_t solver;        /* mjtSolver: SIM_SOL_PGS (soarm_pgs.h) or SIM_SOL_NEWTON (MuJoCo's
                             default, soarm_newton.h); SIM_SOL_CG is rejected (SIM_E_MODEL) */
+  int32_t ccd;           /* SIM_CCD_*: mesh-mesh / box-mesh narrowphase (mjDSBL_NATIVECCD off = native) */
+  int32_t _pad0;
 
   /* bodies (0 = world) */
   int32_t body_parentid[SIM_MAXBODY];

@@ -13,6 +13,7 @@ MAXCON = 16
 
 JNT_FREE, JNT_BALL, JNT_SLIDE, JNT_HINGE = 0, 1, 2, 3
 SOL_PGS, SOL_CG, SOL_NEWTON = 0, 1, 2
+CCD_MPR, CCD_NATIVE = 0, 1
 GEOM_PLANE, GEOM_SPHERE, GEOM_BOX, GEOM_MESH = 0, 2, 6, 7
 
 ST_BADQPOS, ST_BADQVEL, ST_BADQACC, ST_CONOVERFLOW = 1, 2, 4, 8
@@ -44,6 +45,7 @@ class ModelDesc(_Versioned):
         ("timestep", f64), ("gravity", _a(f64, 3)), ("impratio", f64), ("tolerance", f64),
         ("meaninertia", f64),
         ("iterations", i32), ("disable_contact", i32), ("disable_eulerdamp", i32), ("solver", i32),
+        ("ccd", i32), ("_pad0", i32),
         # bodies
         ("body_parentid", _a(i32, MAXBODY)), ("body_rootid", _a(i32, MAXBODY)),
         ("body_weldid", _a(i32, MAXBODY)), ("body_jntnum", _a(i32, MAXBODY)),

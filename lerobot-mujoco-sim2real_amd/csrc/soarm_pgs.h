@@ -27,6 +27,7 @@
 // body is the hot loop of the contact scene.
 #pragma once
 #include <type_traits>
+#include <utility>
 
 #include "soarm_collide.h"
 
@@ -138,6 +139,77 @@ constexpr int XS_LIST = SIM_MAXCON;           // ext[0, XS_LIST): the env's cont
 constexpr int XS_EXT = XS_LIST + 98;           // + extra-slot scratch beyond the limit list
 enum { L_DOF = 0, L_SGN = 1, L_AREF = 2, L_R = 3, L_ARD = 4, L_IARD = 5, L_FRC = 6 };
 
+// ---- Wide block sweep (PGS, scene with a free body; the 4-wave workgroup of k_substep).
+// The pure block's ~95 Gauss-Seidel sweeps over the 16 pyramid edges of the cube's 4 resting
+// contacts are most of a pure wave's time, and at 4096 envs the quad layout (4 lanes per env,
+// 16 envs per wave) leaves 3 of a CU's 4 SIMDs idle.  The wide kernel adds 3 helper waves per
+// 16 envs: wave 0 runs the per-env code as before; once the arm's rows retire (ysweeps), it
+// hands the block to all 4 waves through LDS, and the remaining sweeps run with one lane per
+// edge -- 4 envs x 16 lanes per wave.  Lane r of an env holds edge r's scaled residual
+// s_r = -res_r / ARdiag_r, its force f_r and row r of the scaled edge-space Delassus matrix
+// C[r][q] = -(J_r M^-1 J_q' + R_r delta_rq) / ARdiag_r (the quad sweep's C01/C23).  Step q of a
+// sweep: every lane forms max(s, -f) (the projected step, valid in lane q), lane q's value is
+// broadcast within the 16-lane row (DPP row_newbcast), every lane moves its residual by C[r][q]
+// times it, and lane q adds it to its force: MuJoCo's row order, one row at a time.  The sweep's
+// improvement (mj_solPGS's stopping test) is its exact total: with r = A f + b,
+// cost(f0) - cost(f1) = sum_r ARdiag_r / 2 (f1 - f0)_r (s0 + s1)_r, summed over the row.
+constexpr int WIDE_R = 16;       // block edges = lanes per env in the wide sweep
+constexpr int WIDE_COLS = 16;    // envs per workgroup
+enum { WIDE_SKIP = 0, WIDE_WORK = 1, WIDE_EXIT = 2 };
+struct WideLds {
+  float C[WIDE_COLS][WIDE_R][WIDE_R];  // [env][row][step]
+  float s[WIDE_COLS][WIDE_R], f[WIDE_COLS][WIDE_R], hd[WIDE_COLS][WIDE_R];
+  int it[WIDE_COLS];                   // first sweep index (>= iterations: nothing to do)
+  int flag;
+};
+template <int Q>
+DEVI float rowbcast(float x) {  // lane Q of each 16-lane row
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x150 + Q, 0xF, 0xF, true));
+}
+// sum over the 16-lane row, bit-identical in all 16 lanes (the stop test must agree)
+DEVI float rowsum16(float x) {
+  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xF, 0xF, false));   // quad xor 1
+  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x4E, 0xF, 0xF, false));   // quad xor 2
+  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x124, 0xF, 0xF, false));  // row_ror:4
+  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x128, 0xF, 0xF, false));  // row_ror:8
+  return rowbcast<0>(x);
+}
+template <int Q>
+DEVI void wide_step(const float (&Cr)[WIDE_R], const float (&oh)[WIDE_R], float& s, float& f) {
+  float cand;
+  asm("v_max_f32_e64 %0, %1, -%2" : "=v"(cand) : "v"(s), "v"(f));  // max(s, -f), see max_neg
+  s = fmaf(Cr[Q], rowbcast<Q>(cand), s);
+  f = fmaf(oh[Q], cand, f);  // lane Q only (oh = one-hot of the lane's row)
+}
+template <int... Qs>
+DEVI void wide_sweep(const float (&Cr)[WIDE_R], const float (&oh)[WIDE_R], float& s, float& f,
+                     std::integer_sequence<int, Qs...>) {
+  (wide_step<Qs>(Cr, oh, s, f), ...);
+}
+// The wide sweeps of the envs handed over in W, by every thread t of the workgroup (env t / 16,
+// edge t % 16); each env continues from its own sweep index until its stopping test passes.
+DEVI void wide_sweeps(const DModel& m, WideLds& W, int t) {
+  const int c = t >> 4, r = t & 15;
+  float Cr[WIDE_R], oh[WIDE_R];
+#pragma unroll
+  for (int q = 0; q < WIDE_R; q++) Cr[q] = W.C[c][r][q], oh[q] = q == r ? 1.f : 0.f;
+  float s = W.s[c][r], f = W.f[c][r];
+  const float hd = W.hd[c][r], scale = m.pgs_scale, tol = m.tolerance;
+  int it = W.it[c];
+  const int iters = m.iterations;
+  for (; it < iters; it++) {
+    const float s0 = s, f0 = f;
+    wide_sweep(Cr, oh, s, f, std::make_integer_sequence<int, WIDE_R>{});
+    const float imp = rowsum16(hd * (f - f0) * (s0 + s));
+    if (imp * scale < tol) {
+      it++;
+      break;
+    }
+  }
+  W.f[c][r] = f;
+  if (r == 0) W.it[c] = it;
+}
+
 // Per-env LDS state, [field][column]: one column per env of the workgroup (64 / lanes per
 // env); the lanes of an env share its column (identical values, or records written by the
 // one lane that built them).
@@ -149,6 +221,7 @@ struct RowLds {
   int lane;     // thread in the workgroup
   int col;      // this env's column
   int cols;     // columns (envs per workgroup)
+  WideLds* wide = nullptr;  // the wide block sweep's hand-over area (4-wave PGS kernel), else null
   DEVI float& at(int c, int f) const { return a[(c * CF + f) * cols + col]; }
   DEVI float& lm(int l, int f) const { return lim[(l * LF + f) * cols + col]; }
   DEVI float& lraw(int k) const { return lim[k * cols + col]; }
@@ -1732,6 +1805,46 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       }
     }
   };
+  // The wide kernel's hand-over round (see WideLds): every call of this solve on wave 0 runs
+  // exactly one round, WORK from the pure / uncoupled block-only sweeps below, else SKIP, so
+  // the helper waves' barriers pair with wave 0's.  WORK: each quad lane writes its block
+  // contact's 4 rows (scaled residuals, forces, ARdiag/2, its rows of C), the 4 waves sweep,
+  // and the quad reads the 16 forces back.
+  bool wide_done = false;
+  auto wide_round = [&](int it0, auto pk) {
+    WideLds& W = *L.wide;
+    if constexpr (decltype(pk)::value && QUAD) {
+      const int col = L.col;
+#pragma unroll
+      for (int ed = 0; ed < 4; ed++) {
+        const int row = 4 * sub + ed;
+        W.s[col][row] = ed == 0 ? ro01.x : ed == 1 ? ro01.y : ed == 2 ? ro23.x : ro23.y;
+        W.f[col][row] = sub == 0 ? cfo[0][ed] : sub == 1 ? cfo[1][ed] : sub == 2 ? cfo[2][ed] : cfo[3][ed];
+        W.hd[col][row] = sub == 0 ? yhd[0][ed] : sub == 1 ? yhd[1][ed] : sub == 2 ? yhd[2][ed] : yhd[3][ed];
+#pragma unroll
+        for (int j = 0; j < FC; j++)
+#pragma unroll
+          for (int d = 0; d < 4; d++) {
+            const f2 cc = ed < 2 ? C01[j][d] : C23[j][d];
+            W.C[col][row][4 * j + d] = (ed & 1) ? cc.y : cc.x;
+          }
+      }
+      if (sub == 0) W.it[col] = it0;
+      W.flag = WIDE_WORK;
+      __syncthreads();
+      wide_sweeps(m, W, L.lane);
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < FC; k++)
+#pragma unroll
+        for (int ed = 0; ed < 4; ed++) cfo[k][ed] = W.f[col][4 * k + ed];
+    } else {
+      W.flag = WIDE_SKIP;
+      __syncthreads();
+      __syncthreads();
+    }
+    wide_done = true;
+  };
   // extras in row order: F = the first of two (arm-only), E = the last one
   const int cE = npost >= 1 ? xidx(npost - 1) : LDS_CON, cF = npost == 2 ? xidx(0) : LDS_CON;
   const bool hasE = npost >= 1, hasF = npost == 2;
@@ -1880,7 +1993,13 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
         }
         vpin(ro01), vpin(ro23);
       }
-      if (!done)
+      if (L.wide) {  // wave-uniform: the 4-wave kernel sweeps the block one lane per edge
+        wide_round(done ? m.iterations : it, std::bool_constant<PK::value>{});
+#ifdef SOARM_PHASE_PROF
+        it = L.wide->it[L.col] - 1;
+        done = it + 1 < m.iterations || done;
+#endif
+      } else if (!done)
         for (; it < m.iterations; it++) {
           float unused = 0.f, unused2 = 0.f;
           if (sweep(std::false_type{}, std::false_type{}, unused, unused2) * scale < m.tolerance) {
@@ -1945,6 +2064,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   } else {
     sweeps(std::false_type{});
   }
+  if (L.wide && !wide_done) wide_round(0, std::false_type{});  // (SKIP: see wide_round)
   if constexpr (NF == 1 && CON) {  // the block's forces back to their records (for J' f)
 #pragma unroll
     for (int k = 0; k < FC; k++)

@@ -399,8 +399,11 @@ DEVI int gather_contacts(const DModel& m, int n, int e, const float* __restrict_
 
 // one substep with contacts: gather -> forward -> Euler -> next substep's geom poses
 // (AP: st.qfrc_applied is set, as in k_step)
-template <int NA, int NF, bool AP, int SOL>
-__global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, int n, sim_state st,
+// WIDE (PGS, free-body scene, n % 16 == 0, n <= 4096): 4 waves per 16 envs -- wave 0 runs the
+// per-env code, waves 1-3 only join the wide block sweep (WideLds in soarm_pgs.h) and wait
+// at the workgroup barrier otherwise, so 4096 envs occupy all 1024 SIMDs in that phase.
+template <int NA, int NF, bool AP, int SOL, bool WIDE = false>
+__global__ __launch_bounds__(WIDE ? 256 : 64) void k_substep(const DModel* __restrict__ dm, int n, sim_state st,
                                                 const float* __restrict__ action,
                                                 float* __restrict__ obs, sim_params pp,
                                                 float* __restrict__ scratch,
@@ -410,7 +413,20 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
                                                 float* __restrict__ gpose, const float* gpose_in) {
   // lpe<NF>() lanes per env (soarm_pgs.h): they run the same per-env code
   const int e = blockIdx.x * (64 / lpe<NF>()) + (int)threadIdx.x / lpe<NF>();
-  if (e >= n) return;
+  __shared__ std::conditional_t<WIDE, WideLds, char> s_wide;
+  if constexpr (WIDE) {
+    static_assert(NF == 1 && SOL == SIM_SOL_PGS && 64 / lpe<NF>() == WIDE_COLS, "wide kernel: PGS, quad, 16 envs");
+    if (threadIdx.x >= 64) {  // helper waves: one wide sweep per WORK round until wave 0 ends
+      for (;;) {
+        __syncthreads();
+        const int fl = s_wide.flag;
+        if (fl == WIDE_EXIT) return;
+        if (fl == WIDE_WORK) wide_sweeps(*dm, s_wide, (int)threadIdx.x);
+        __syncthreads();
+      }
+    }
+  }
+  if (!WIDE && e >= n) return;  // (the wide launch covers whole workgroups: n % 16 == 0)
   PHASE_T(t0);
   const DModel& m = *dm;
   Sim<NA, NF> S(dm, pp.mass_scale ? pp.mass_scale[e] : 1.f, pp.friction ? pp.friction[e] : -1.f,
@@ -427,8 +443,9 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
   __shared__ float s_keep[keep_floats<NA, NF>()][COLS];
   // contact list (quad), y-sweep slots; Newton: its line-search rows (8 per LDS contact)
   __shared__ float s_ext[NF == 1 ? XS_EXT : (lpe<NF>() == 4 ? XS_LIST + (SOL == SIM_SOL_NEWTON ? 12 * LDS_CON : 0) : 1)][COLS];
-  const RowLds L{&s_rows[0][0], &s_lim[0][0], NF == 1 ? &s_keep[0][0] : nullptr, &s_ext[0][0], (int)threadIdx.x,
-                 (int)threadIdx.x / lpe<NF>(), COLS};
+  RowLds L{&s_rows[0][0], &s_lim[0][0], NF == 1 ? &s_keep[0][0] : nullptr, &s_ext[0][0], (int)threadIdx.x,
+           (int)threadIdx.x / lpe<NF>(), COLS};
+  if constexpr (WIDE) L.wide = (WideLds*)&s_wide;
   const ContactRows<NA, NF> cr{scratch + e, n};
   const float ncon_prev = st.ncon ? st.ncon[e] : 0.f;  // issued early: consumed at the end
   const int st0 = S.status;
@@ -559,6 +576,10 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
     }
   }
 #endif
+  if constexpr (WIDE) {  // release the helper waves
+    ((WideLds*)&s_wide)->flag = WIDE_EXIT;
+    __syncthreads();
+  }
 }
 
 // diagnostic: compacted contact list [N][SIM_MAXCON][8] (dist, pos, normal, pair) + count
@@ -1420,6 +1441,18 @@ int sim_reset(sim_batch* b, const sim_state* s, const float* init_qpos, const fl
   return SIM_OK;
 }
 
+// the 4-wave wide PGS substep (k_substep<..., WIDE>): whole 16-env workgroups, and at most one
+// wave per SIMD in total (its waves hold 512 registers: 4096 envs = 1024 waves); larger batches
+// keep the one-wave kernel, whose 64-lane workgroups already fill the SIMDs.  SOARM_WIDE=0
+// disables it (A/B).
+static bool wide_ok(const sim_batch* b) {
+  static const bool on = [] {
+    const char* v = getenv("SOARM_WIDE");
+    return !(v && v[0] == '0');
+  }();
+  return on && b->n % WIDE_COLS == 0 && b->n <= 4096;
+}
+
 int sim_step(sim_batch* b, const sim_state* s, const float* action, int frame_skip, float* obs,
              void* stream) {
   const TraceRange tr_("sim_step");
@@ -1469,7 +1502,14 @@ int sim_step(sim_batch* b, const sim_state* s, const float* action, int frame_sk
         const TraceRange tr_("substep");
         prof_mark(b, 2, q);
         auto kern = s->qfrc_applied ? k_substep<NA, NF, true, SOL> : k_substep<NA, NF, false, SOL>;
-        hipLaunchKernelGGL(kern, dim3((b->n + 64 / lpe<NF>() - 1) / (64 / lpe<NF>())), dim3(64), 0, q,
+        int threads = 64;
+        if constexpr (NF == 1 && SOL == SIM_SOL_PGS) {
+          if (wide_ok(b)) {
+            kern = s->qfrc_applied ? k_substep<NA, NF, true, SOL, true> : k_substep<NA, NF, false, SOL, true>;
+            threads = 256;
+          }
+        }
+        hipLaunchKernelGGL(kern, dim3((b->n + 64 / lpe<NF>() - 1) / (64 / lpe<NF>())), dim3(threads), 0, q,
                            b->d_model, b->n, *s,
                            sub == 0 ? action : nullptr, last ? obs : nullptr, b->params, b->d_scratch,
                            b->d_cbuf, np > 0 ? b->d_ccount : nullptr, np > 0 ? b->d_pmask : nullptr,

@@ -287,8 +287,12 @@ def _load_hulls(path=None):
 def compile_mjcf(xml_path=SCENE_XML, kv=None, disable_contact=False, iterations=100,
                  tolerance=1e-8, obs_site="gripperframe",
                  obs_joints=("shoulder_pan", "shoulder_lift", "elbow_flex", "wrist_flex", "wrist_roll"),
-                 solver="PGS"):
+                 solver="PGS", ccd="mpr"):
     """Compile an MJCF file into a :class:`CompiledModel`.
+
+    ccd: the convex-convex narrowphase, "native" (MuJoCo's GJK/EPA, the default of current
+    releases) or "mpr" (libccd MPR, MuJoCo's classic path); an explicit
+    ``<option><flag nativeccd="disable"/></option>`` in the MJCF selects MPR.
 
     solver: "PGS" (the north star's and BASELINE config 3's solver, the headline) or "Newton"
     (MuJoCo's default, which the reference scene's missing <option> selects): both run on the
@@ -341,6 +345,14 @@ def compile_mjcf(xml_path=SCENE_XML, kv=None, disable_contact=False, iterations=
     if str(solver).lower() not in sol:
         raise ValueError(f"solver must be PGS or Newton, not {solver!r}")
     d.solver = sol[str(solver).lower()]
+    ccds = {"mpr": abi.CCD_MPR, "native": abi.CCD_NATIVE}
+    if str(ccd).lower() not in ccds:
+        raise ValueError(f"ccd must be 'native' or 'mpr', not {ccd!r}")
+    d.ccd = ccds[str(ccd).lower()]
+    for o in root.iter("option"):
+        for fl in o.iter("flag"):
+            if fl.get("nativeccd") == "disable":
+                d.ccd = abi.CCD_MPR
     d.disable_contact = int(bool(disable_contact))
 
     # ---- walk bodies depth-first; worldbody sections merged in order

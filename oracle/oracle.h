@@ -125,6 +125,7 @@ int orc_hull_support_ex(const orc_model* om, int g, const double l[3], int use_g
 int orc_hull_support_flat(const sim_model_desc* m, const float* hv, const int32_t* hadr,
                           const int32_t* hadj, int g, const double* dirs, int n, int use_graph,
                           int32_t* out);
+void orc_geom_frames(const sim_model_desc* m, const double* qpos, double* xpos, double* xmat);
 void orc_collision_stats(double* out /*[8 + 2*SIM_MAXPAIR]*/, int reset);
 int orc_collide_pair(const orc_model* om, const orc_data* d, int g1, int g2, orc_contact* out,
                      int maxout);

@@ -46,6 +46,8 @@ def lib():
         L.orc_debug_forward.restype = C.c_int
         L.orc_collide_geoms.argtypes = [vp] * 5 + [C.c_int, C.c_int, vp, C.c_int]
         L.orc_collide_geoms.restype = C.c_int
+        L.orc_geom_frames.argtypes = [vp] * 4
+        L.orc_geom_frames.restype = None
         L.orc_ik_dls.argtypes = [vp, C.c_int, vp, vp, vp, vp, vp] + [C.c_double] * 6 + [C.c_int] * 3
         L.orc_ik_dls.restype = None
         L.orc_hull_support_flat.argtypes = [vp] * 4 + [C.c_int, vp, C.c_int, C.c_int, vp]
@@ -177,6 +179,13 @@ class Oracle:
         lib().orc_hull_support_flat(self._desc_p, _p(self.hv), _p(self.hadr), _p(self.hadj), g,
                                     _p(d), len(d), int(use_graph), _p(out))
         return out
+
+    def geom_frames(self, qpos):
+        """World (xpos [ngeom, 3], xmat [ngeom, 3, 3]) of every geom at qpos."""
+        ng = self.desc.ngeom
+        xp, xm = np.zeros(3 * ng), np.zeros(9 * ng)
+        lib().orc_geom_frames(self._desc_p, _p(np.ascontiguousarray(qpos, np.float64)), _p(xp), _p(xm))
+        return xp.reshape(ng, 3), xm.reshape(ng, 3, 3)
 
     def collide(self, qpos, g1, g2, maxout=8):
         out = np.zeros(7 * 8)

@@ -7,10 +7,12 @@
  *  - candidate pairs come pre-filtered and pre-ordered from the compiler
  *    (sim_model_desc.pair_geom1/2); the midphase is MuJoCo's bounding-sphere
  *    test about the geom's collision centre (rbound + margin);
- *  - convex-convex (mesh hull / box vs mesh hull) is MPR penetration with
- *    tolerance 1e-6 and 50 iterations (MuJoCo mpr_tolerance/mpr_iterations
- *    defaults), one contact per pair, dist = -depth, normal = MPR direction
- *    (geom1 -> geom2), pos = midpoint of the two witness points;
+ *  - convex-convex (mesh hull / box vs mesh hull): native GJK/EPA (MuJoCo's
+ *    nativeccd, sim_model_desc.ccd = SIM_CCD_NATIVE, the default of current
+ *    releases; see below) or MPR (libccd, SIM_CCD_MPR) penetration with
+ *    tolerance 1e-6 and 50 iterations (MuJoCo's defaults), one contact per
+ *    pair, dist = -depth, normal geom1 -> geom2, pos = midpoint of the two
+ *    witness points;
  *  - box-box: separating-axis test over 15 axes, reference-face clipping of
  *    the incident face (<= 4 contacts, deepest kept) or one edge-edge contact;
  *  - plane-box: penetrating corners (<= 4); plane-convex: deepest hull vertex.
@@ -437,6 +439,259 @@ static int mpr_penetration(const mpair* P, double* depth, double dir[3], double 
   }
 }
 
+/* ----------------------------------------------------- native GJK / EPA */
+/* [ext] MuJoCo engine_collision_gjk.c (mjc_ccd, "nativeccd": the convex-convex default of
+   current MuJoCo releases; opt.ccd_tolerance 1e-6, opt.ccd_iterations 50), restated by
+   algorithm: GJK on the Minkowski difference A - B (support s = sA(d) - sB(-d)) from the
+   difference of the shapes' centres, stopping as soon as a support plane separates the
+   origin (no contact: margin 0) or a tetrahedron encloses it; then EPA (expanding polytope)
+   from that tetrahedron: per iteration the face closest to the origin (a lower bound of the
+   penetration depth) is expanded by the support point along its normal (an upper bound),
+   until upper - lower < tolerance.  Contact: depth = the closest face's distance, normal = its
+   outward normal (geom1 -> geom2), witness points x1, x2 = the barycentric weights of the
+   origin's projection on that face applied to the two shapes' support points, pos = (x1+x2)/2.
+   Touching configurations (the origin on the boundary of the final simplex) give no contact. */
+#define CCD_TOL 1e-6
+#define CCD_ITER 50
+#define EPA_MAXV (4 + CCD_ITER)
+#define EPA_MAXF (2 * EPA_MAXV)
+
+typedef struct {
+  int a, b, c, live;
+  double n[3], d;
+} epa_face;
+
+/* closest point to the origin on the simplex p[0..n-1] (n <= 3); keeps in p only the vertices
+   of the sub-simplex that carries it (Ericson's Voronoi-region tests).  Returns its size. */
+static int gjk_reduce(msup* p, int n, double x[3]) {
+  if (n == 1) {
+    memcpy(x, p[0].v, sizeof(double) * 3);
+    return 1;
+  }
+  if (n == 2) {
+    double ab[3], t;
+    sub3(ab, p[1].v, p[0].v);
+    t = -dot3(p[0].v, ab);
+    double l2 = dot3(ab, ab);
+    if (t <= 0 || l2 <= 0) {
+      memcpy(x, p[0].v, sizeof(double) * 3);
+      return 1;
+    }
+    if (t >= l2) {
+      p[0] = p[1];
+      memcpy(x, p[0].v, sizeof(double) * 3);
+      return 1;
+    }
+    t /= l2;
+    for (int k = 0; k < 3; k++) x[k] = p[0].v[k] + t * ab[k];
+    return 2;
+  }
+  /* triangle: regions of a, b, c, edges, face */
+  const double *a = p[0].v, *b = p[1].v, *c = p[2].v;
+  double ab[3], ac[3], ap[3] = {-a[0], -a[1], -a[2]};
+  sub3(ab, b, a);
+  sub3(ac, c, a);
+  double d1 = dot3(ab, ap), d2 = dot3(ac, ap);
+  if (d1 <= 0 && d2 <= 0) {
+    memcpy(x, a, sizeof(double) * 3);
+    return 1;
+  }
+  double bp[3] = {-b[0], -b[1], -b[2]};
+  double d3 = dot3(ab, bp), d4 = dot3(ac, bp);
+  if (d3 >= 0 && d4 <= d3) {
+    p[0] = p[1];
+    memcpy(x, b, sizeof(double) * 3);
+    return 1;
+  }
+  double vc = d1 * d4 - d3 * d2;
+  if (vc <= 0 && d1 >= 0 && d3 <= 0) {
+    double t = d1 / (d1 - d3);
+    for (int k = 0; k < 3; k++) x[k] = a[k] + t * ab[k];
+    return 2; /* a, b */
+  }
+  double cp[3] = {-c[0], -c[1], -c[2]};
+  double d5 = dot3(ab, cp), d6 = dot3(ac, cp);
+  if (d6 >= 0 && d5 <= d6) {
+    p[0] = p[2];
+    memcpy(x, c, sizeof(double) * 3);
+    return 1;
+  }
+  double vb = d5 * d2 - d1 * d6;
+  if (vb <= 0 && d2 >= 0 && d6 <= 0) {
+    double t = d2 / (d2 - d6);
+    for (int k = 0; k < 3; k++) x[k] = a[k] + t * ac[k];
+    p[1] = p[2];
+    return 2; /* a, c */
+  }
+  double va = d3 * d6 - d5 * d4;
+  if (va <= 0 && (d4 - d3) >= 0 && (d5 - d6) >= 0) {
+    double t = (d4 - d3) / ((d4 - d3) + (d5 - d6));
+    for (int k = 0; k < 3; k++) x[k] = b[k] + t * (c[k] - b[k]);
+    p[0] = p[2]; /* b, c */
+    return 2;
+  }
+  double den = 1.0 / (va + vb + vc), v = vb * den, w = vc * den;
+  for (int k = 0; k < 3; k++) x[k] = a[k] + ab[k] * v + ac[k] * w;
+  return 3;
+}
+
+/* 1 if the origin lies inside tetrahedron p[0..3] (strictly, up to rounding); else the index
+   of a face whose plane separates it: the simplex is reduced to that face (returned 3-simplex
+   with the origin on its outer side) */
+static int tet_contains(msup* p, double x[3], int* nout) {
+  /* face k = the three vertices other than k; outward = away from vertex k */
+  static const int F[4][3] = {{1, 2, 3}, {0, 3, 2}, {0, 1, 3}, {0, 2, 1}};
+  double best = 0;
+  int bk = -1;
+  for (int k = 0; k < 4; k++) {
+    const double *a = p[F[k][0]].v, *b = p[F[k][1]].v, *c = p[F[k][2]].v;
+    double ab[3], ac[3], n[3];
+    sub3(ab, b, a);
+    sub3(ac, c, a);
+    cross3(n, ab, ac);
+    double ak[3];
+    sub3(ak, p[k].v, a);
+    if (dot3(n, ak) > 0) for (int q = 0; q < 3; q++) n[q] = -n[q];
+    double ln = norm3(n);
+    if (ln <= 0) return -1; /* flat */
+    double s = -dot3(n, a) / ln; /* > 0: origin outside this face */
+    if (s > best) {
+      best = s;
+      bk = k;
+    }
+  }
+  if (bk < 0) return 1;
+  msup t[3] = {p[F[bk][0]], p[F[bk][1]], p[F[bk][2]]};
+  p[0] = t[0], p[1] = t[1], p[2] = t[2];
+  *nout = gjk_reduce(p, 3, x);
+  return 0;
+}
+
+/* GJK: 1 with p[0..3] a tetrahedron enclosing the origin, 0 if apart or touching */
+static int gjk_enclose(const mpair* P, msup* p) {
+  double c1[3], c2[3], x[3];
+  geom_center(P->om, P->d, P->g1, c1);
+  geom_center(P->om, P->d, P->g2, c2);
+  sub3(x, c1, c2);
+  if (dot3(x, x) == 0) x[0] = 1e-9;
+  int n = 0;
+  for (int it = 0; it < CCD_ITER; it++) {
+    double dir[3] = {-x[0], -x[1], -x[2]};
+    msup s;
+    msupport(P, dir, &s);
+    if (dot3(x, s.v) > 0) return 0; /* the plane x.p = x.s separates the origin: apart */
+    /* no progress toward the origin: it lies (within tolerance) on the boundary */
+    double xx = dot3(x, x);
+    if (xx - dot3(x, s.v) <= CCD_TOL * CCD_TOL) return 0;
+    p[n++] = s;
+    if (n == 4) {
+      int r = tet_contains(p, x, &n);
+      if (r == 1) return 1;
+      if (r < 0) return 0;
+    } else {
+      n = gjk_reduce(p, n, x);
+    }
+    if (dot3(x, x) < 1e-30) return 0; /* origin on a lower-dimensional simplex: touching */
+  }
+  return 0;
+}
+
+static void epa_face_set(epa_face* f, const msup* V, int a, int b, int c) {
+  double ab[3], ac[3];
+  sub3(ab, V[b].v, V[a].v);
+  sub3(ac, V[c].v, V[a].v);
+  cross3(f->n, ab, ac);
+  normalize3(f->n);
+  f->a = a, f->b = b, f->c = c, f->live = 1;
+  f->d = dot3(f->n, V[a].v);
+}
+
+/* EPA from the enclosing tetrahedron V[0..3]: 1 with depth, normal, pos */
+static int epa(const mpair* P, msup* V, double* depth, double dir[3], double pos[3]) {
+  epa_face F[EPA_MAXF];
+  int nv = 4, nf = 0;
+  static const int T[4][3] = {{1, 2, 3}, {0, 3, 2}, {0, 1, 3}, {0, 2, 1}};
+  for (int k = 0; k < 4; k++) {
+    epa_face_set(&F[nf], V, T[k][0], T[k][1], T[k][2]);
+    double ak[3];
+    sub3(ak, V[k].v, V[T[k][0]].v);
+    if (dot3(F[nf].n, ak) > 0) epa_face_set(&F[nf], V, T[k][0], T[k][2], T[k][1]); /* outward */
+    nf++;
+  }
+  int best = -1;
+  double upper = 1e300;
+  for (int it = 0; it < CCD_ITER; it++) {
+    best = -1;
+    for (int i = 0; i < nf; i++)
+      if (F[i].live && (best < 0 || F[i].d < F[best].d)) best = i;
+    if (best < 0) return 0;
+    msup w;
+    msupport(P, F[best].n, &w);
+    double dw = dot3(F[best].n, w.v);
+    if (dw < upper) upper = dw;
+    if (upper - F[best].d < CCD_TOL || nv == EPA_MAXV) break;
+    /* faces seen from w go; their boundary (edges not shared by two of them) is the horizon */
+    int E[3 * EPA_MAXF][2], ne = 0;
+    for (int i = 0; i < nf; i++) {
+      if (!F[i].live) continue;
+      double aw[3];
+      sub3(aw, w.v, V[F[i].a].v);
+      if (dot3(F[i].n, aw) <= 0) continue;
+      F[i].live = 0;
+      const int ed[3][2] = {{F[i].a, F[i].b}, {F[i].b, F[i].c}, {F[i].c, F[i].a}};
+      for (int q = 0; q < 3; q++) {
+        int dup = -1;
+        for (int r = 0; r < ne; r++)
+          if (E[r][0] == ed[q][1] && E[r][1] == ed[q][0]) dup = r;
+        if (dup >= 0) {
+          E[dup][0] = E[ne - 1][0], E[dup][1] = E[ne - 1][1];
+          ne--;
+        } else {
+          E[ne][0] = ed[q][0], E[ne][1] = ed[q][1];
+          ne++;
+        }
+      }
+    }
+    if (ne == 0) break;
+    /* compact the face list, then add one face per horizon edge */
+    int m = 0;
+    for (int i = 0; i < nf; i++)
+      if (F[i].live) F[m++] = F[i];
+    nf = m;
+    if (nf + ne > EPA_MAXF) break;
+    V[nv] = w;
+    for (int r = 0; r < ne; r++) epa_face_set(&F[nf++], V, E[r][0], E[r][1], nv);
+    nv++;
+  }
+  /* witness points of the closest face */
+  const epa_face* f = &F[best];
+  double pr[3] = {f->d * f->n[0], f->d * f->n[1], f->d * f->n[2]};
+  const double *a = V[f->a].v, *b = V[f->b].v, *c = V[f->c].v;
+  double v0[3], v1[3], v2[3];
+  sub3(v0, b, a);
+  sub3(v1, c, a);
+  sub3(v2, pr, a);
+  double d00 = dot3(v0, v0), d01 = dot3(v0, v1), d11 = dot3(v1, v1), d20 = dot3(v2, v0), d21 = dot3(v2, v1);
+  double den = d00 * d11 - d01 * d01;
+  if (den <= 0) return 0;
+  double lb = (d11 * d20 - d01 * d21) / den, lc = (d00 * d21 - d01 * d20) / den, la = 1 - lb - lc;
+  for (int k = 0; k < 3; k++) {
+    double x1 = la * V[f->a].v1[k] + lb * V[f->b].v1[k] + lc * V[f->c].v1[k];
+    double x2 = la * V[f->a].v2[k] + lb * V[f->b].v2[k] + lc * V[f->c].v2[k];
+    pos[k] = 0.5 * (x1 + x2);
+    dir[k] = f->n[k];
+  }
+  *depth = f->d;
+  g_cflops += 0; /* (counted by msupport) */
+  return f->d > 0;
+}
+
+static int ccd_penetration(const mpair* P, double* depth, double dir[3], double pos[3]) {
+  msup V[EPA_MAXV];
+  if (!gjk_enclose(P, V)) return 0;
+  return epa(P, V, depth, dir, pos);
+}
+
 /* ----------------------------------------------------------- primitives */
 static void make_frame(double f[9]) {
   normalize3(f);
@@ -735,7 +990,8 @@ int orc_collide_pair(const orc_model* om, const orc_data* d, int g1, int g2, orc
   mpair P = {om, d, g1, g2};
   double depth, dir[3], pos[3];
   g_cstat[2] += 1;
-  if (!mpr_penetration(&P, &depth, dir, pos)) return 0;
+  if (m->ccd == SIM_CCD_NATIVE ? !ccd_penetration(&P, &depth, dir, pos) : !mpr_penetration(&P, &depth, dir, pos))
+    return 0;
   g_cstat[3] += 1;
   out->dist = -depth;
   memcpy(out->pos, pos, sizeof(pos));
@@ -798,6 +1054,19 @@ int orc_collide_geoms(const sim_model_desc* m, const float* hv, const int32_t* h
     for (int k = 0; k < 3; k++) out[7 * i + 4 + k] = c[i].frame[k];
   }
   return n;
+}
+
+/* world frames of every geom at qpos (kinematics only): xpos [ngeom][3], xmat [ngeom][9] */
+void orc_geom_frames(const sim_model_desc* m, const double* qpos, double* xpos, double* xmat) {
+  orc_model om = {m, NULL, NULL, NULL, NULL, 1.0, -1.0, 1.0};
+  static __thread orc_data d;
+  orc_reset_data(&om, &d);
+  for (int i = 0; i < m->nq; i++) d.qpos[i] = qpos[i];
+  orc_kinematics(&om, &d);
+  for (int g = 0; g < m->ngeom; g++) {
+    for (int k = 0; k < 3; k++) xpos[3 * g + k] = d.geom_xpos[g][k];
+    for (int k = 0; k < 9; k++) xmat[9 * g + k] = d.geom_xmat[g][k];
+  }
 }
 
 int orc_hull_support_flat(const sim_model_desc* m, const float* hv, const int32_t* hadr,
