@@ -41,6 +41,8 @@ def parse():
     p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal on one GPU)")
     p.add_argument("--solver", default="pgs", choices=["pgs", "newton"],
                    help="constraint solver: PGS (BASELINE config 3) or MuJoCo's default Newton")
+    p.add_argument("--ccd", default="mpr", choices=["native", "mpr"],
+                   help="convex-convex narrowphase: MuJoCo's native GJK/EPA or libccd MPR")
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -93,7 +95,7 @@ def launch_ranks(args):
     return bad[0] if bad else 0
 
 
-def cpu_baseline(cfg_name, seconds, seed, solver="pgs"):
+def cpu_baseline(cfg_name, seconds, seed, solver="pgs", ccd="mpr"):
     """The float64 oracle (C restatement of mj_step; for `mpc` plus the numpy MPC restatement)
     on the host cores, a bounded sample of the same workload: chunks of envs x T env-steps."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -102,7 +104,7 @@ def cpu_baseline(cfg_name, seconds, seed, solver="pgs"):
     from lerobot_mujoco_sim2real_amd import workloads as W
 
     cfg = W.CONFIGS[cfg_name]
-    cm = W.model(cfg_name, solver=solver)
+    cm = W.model(cfg_name, solver=solver, ccd=ccd)
     orc = Oracle(cm)
     try:
         cores = len(os.sched_getaffinity(0))
@@ -250,7 +252,7 @@ def main():
     cfg = W.CONFIGS[name]
     n = args.envs or cfg.get("envs", 4096)
     ids = np.arange(rank * n, (rank + 1) * n)
-    cm = W.model(name, solver=args.solver)
+    cm = W.model(name, solver=args.solver, ccd=args.ccd)
     sim = BatchSim(cm, n, gpu)
     q0 = W.initial_qpos(cm, ids, args.seed)
     sim.reset(init_qpos=q0[:, :5], extra_qpos=q0, seed=args.seed, env_offset=rank * n)
@@ -473,7 +475,7 @@ def main():
     other_solver = None
     if not args.no_other_solver and name in ("contact", "dr"):
         other = "newton" if args.solver == "pgs" else "pgs"
-        cm2 = W.model(name, solver=other)
+        cm2 = W.model(name, solver=other, ccd=args.ccd)
         sim2 = BatchSim(cm2, n, gpu)
         sim2.reset(init_qpos=q0[:, :5], extra_qpos=q0, seed=args.seed, env_offset=rank * n)
         if cfg["dr"]:
@@ -519,7 +521,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(name, args.cpu_seconds, args.seed, args.solver)
+        cpu = cpu_baseline(name, args.cpu_seconds, args.seed, args.solver, args.ccd)
 
     if rank == 0:
         line = {
@@ -534,6 +536,8 @@ def main():
                        "contacts_per_env_substep": contacts,
                        "solver": ("PGS (iterations 100, tol 1e-8, scale 1/(meaninertia nv))" if args.solver == "pgs"
                                   else "Newton (MuJoCo's default: iterations 100, tol 1e-8, exact line search)"),
+                       "narrowphase": ("native GJK/EPA (MuJoCo nativeccd)" if args.ccd == "native"
+                                       else "MPR (libccd)"),
                        "parallelism": f"env-sharded x{world} (no per-step collective)"},
             "steady_state": steady,
             "other_solver": other_solver,

@@ -80,6 +80,18 @@ int sim_koopman_feedforward(sim_koopman* k, int nframe, int nref, int n, const d
 int sim_koopman_mpc_step(sim_koopman* k, int n, const float* x, const double* z0, const double* ff,
                          double* u_prev, float* action, void* stream);
 
+/* The bilinear DBKN model (models/KoopmanBase.py:62-110): its input matrix is linearised at each
+   env's lifted state, B_total = B + sum_j z0_j Hhat_j (linearize_B, MPC_Controler.py:46-63), so
+   the condensed QP of MPC_Controler.py:65-141 (state_full: Q = q I, R = r I) is solved per env and
+   frame.  set_bilinear: A [nz][nz], B [nz][u_dim], Hhat [nz (j)][nz][u_dim] (get_Hi_numpy), delta
+   (1 = 'delta_mpc', 0 = 'mpc'), q = 50, r = 0.5.  bilinear_step: z0 [nz][n], window [H][nz][n]
+   (lifted reference rows k+1 .. k+H, zero past the end), u_prev [u_dim][n] in/out (u_prev <- u0),
+   action [n][u_dim] = clip(u0) float32.  Replaces the casadi solve of get_control for DBKN. */
+int sim_koopman_set_bilinear(sim_koopman* k, const double* A, const double* B, const double* Hhat, int delta,
+                             double q, double r);
+int sim_koopman_bilinear_step(sim_koopman* k, int n, const double* z0, const double* window, double* u_prev,
+                              float* action, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -137,7 +137,7 @@ EXPORTS = [
     "sim_model_save", "sim_model_load",
     # include/koopman_mpc.h
     "sim_koopman_create", "sim_koopman_free", "sim_koopman_encode", "sim_koopman_feedforward",
-    "sim_koopman_mpc_step",
+    "sim_koopman_mpc_step", "sim_koopman_set_bilinear", "sim_koopman_bilinear_step",
 ]
 PROF_KINDS = ["step_fused", "collide", "substep", "geom"]
 
@@ -185,6 +185,8 @@ def load_lib(path=None):
     lib.sim_koopman_encode.argtypes = [vp, ip, vp, vp, vp]
     lib.sim_koopman_feedforward.argtypes = [vp, ip, ip, ip, vp, vp, vp]
     lib.sim_koopman_mpc_step.argtypes = [vp, ip, vp, vp, vp, vp, vp, vp]
+    lib.sim_koopman_set_bilinear.argtypes = [vp, vp, vp, vp, ip, C.c_double, C.c_double]
+    lib.sim_koopman_bilinear_step.argtypes = [vp, ip, vp, vp, vp, vp, vp]
     for name in EXPORTS:
         if not hasattr(lib, name):
             raise RuntimeError(f"{p} does not export {name}")

@@ -13,8 +13,9 @@ computed once on the host in float64) and every per-env evaluation runs in the H
 
 A bilinear DBKN model (``net.H``, ``KoopmanBase.py:62-110``) linearises its input matrix at each
 frame's lifted state (``linearize_B``, ``:46-63``), so the QP differs per env and frame:
-:meth:`step_bilinear` lifts the state in the HIP library and solves the n QPs batched in float64
-on the device (``control/koopman.bilinear_first_move``).
+:meth:`step_bilinear` lifts the state in the HIP library and solves the n QPs in float64 on the
+device, one wave per env (``sim_koopman_bilinear_step``, ``koopman_mpc.hip`` ``k_bilinear``;
+``control/koopman.bilinear_first_move`` is the same algebra in torch, kept as its CPU cross-check).
 
 There is no CPU path: without the library or a GPU, construction raises.
 """
@@ -23,7 +24,7 @@ import ctypes as C
 import numpy as np
 
 from .. import abi
-from .koopman import bilinear_first_move, condensed_gains
+from .koopman import condensed_gains
 
 Q_WEIGHT, R_WEIGHT = 50.0, 0.5  # state_full weights (MPC_Controler.py:39-40)
 
@@ -60,10 +61,6 @@ class MPCController:
         self.Gr, self.Gz, self.Gu = condensed_gains(self.Ad, self.Bd, self.H, self.MPC_type, Q_WEIGHT, R_WEIGHT)
         if self.bilinear:  # (the gains above are the z0 = 0 linearisation; step_bilinear does not use them)
             self.H_hat_list = net.get_Hi_numpy()
-            dev = dict(dtype=torch.float64, device=self.device)
-            self._A = torch.as_tensor(self.Ad, **dev)
-            self._B = torch.as_tensor(self.Bd, **dev)
-            self._Hhat = torch.as_tensor(np.stack(self.H_hat_list), **dev)
 
         layers = net.encoder_layers()
         widths = [layers[0][0].shape[1]] + [W.shape[0] for W, _ in layers]
@@ -80,6 +77,13 @@ class MPCController:
         abi.check(self.lib, self.lib.sim_koopman_create(C.byref(d), self._w.ctypes.data_as(C.c_void_p),
                                                         self._g.ctypes.data_as(C.c_void_p), device,
                                                         C.byref(self._h)))
+        if self.bilinear:  # the per-env QP kernel (koopman_mpc.hip k_bilinear)
+            self._Ah = np.ascontiguousarray(self.Ad, np.float64)
+            self._Bh = np.ascontiguousarray(self.Bd, np.float64)
+            self._Hh = np.ascontiguousarray(np.stack(self.H_hat_list), np.float64)  # [j][nz][nu]
+            abi.check(self.lib, self.lib.sim_koopman_set_bilinear(
+                self._h, self._Ah.ctypes.data_as(C.c_void_p), self._Bh.ctypes.data_as(C.c_void_p),
+                self._Hh.ctypes.data_as(C.c_void_p), int(self.MPC_type == "delta_mpc"), Q_WEIGHT, R_WEIGHT))
 
     def __del__(self):
         try:
@@ -136,15 +140,17 @@ class MPCController:
         each env with B_total = Bd + Σ_j z0_j Ĥ_j solved exactly; u_prev <- u0; returns
         action = clip(u0) [n, u_dim] float32.  window [H, nz, n]: lifted reference rows."""
         torch = self.torch
+        if self.MPC_type not in ("mpc", "delta_mpc"):
+            raise ValueError(f"MPC_type {self.MPC_type!r}: 'mpc' or 'delta_mpc'")
         if z0 is None:
             z0 = self.encode(x)
-        u0 = bilinear_first_move(self._A, self._B, self._Hhat, z0, window, u_prev, self.MPC_type, self.H,
-                                 Q_WEIGHT, R_WEIGHT)
-        u_prev.copy_(u0)
-        a = torch.clamp(u0, -self.u_clip, self.u_clip).T.to(torch.float32)
+        n = u_prev.shape[1]
         if action is None:
-            return a.contiguous()
-        action.copy_(a)
+            action = torch.empty((n, self.u_dim), dtype=torch.float32, device=self.device)
+        z0 = z0.contiguous()
+        window = window.contiguous()
+        abi.check(self.lib, self.lib.sim_koopman_bilinear_step(self._h, n, _ptr(z0), _ptr(window), _ptr(u_prev),
+                                                               _ptr(action), self._stream()))
         return action
 
     # ------------------------------------------------------- reference single-env API

@@ -20,6 +20,7 @@ struct DModel {
   int nq, nv, nu, ngeom, npair, nact, obs_site, obs_nq;
   int obs_qadr[SIM_MAXOBSQ];
   int iterations, disable_contact, eulerdamp, nhullvert;
+  int ccd, _pad_ccd[3];  // SIM_CCD_* (convex-convex narrowphase)
   float timestep, impratio, tolerance, pgs_scale;  // pgs_scale = 1 / (meaninertia * max(1, nv))
   float gravity[4];
 

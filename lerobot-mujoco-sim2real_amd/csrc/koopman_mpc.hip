@@ -253,6 +253,176 @@ __global__ __launch_bounds__(256) void k_feedforward(KDev K, const double* __res
   }
 }
 
+// ---------------------------------------------------------------- DBKN (bilinear) first move
+// The bilinear model's input matrix depends on the lifted state: B_total = B + sum_j z0_j Hhat_j
+// (linearize_B, MPC_Controler.py:46-63), so the condensed QP (MPC_Controler.py:100-141, state_full:
+// Q = q I, R = r I) differs per env and frame.  One wave per env, float64, everything in LDS:
+//   M_0 = B_total, M_k = A M_{k-1}; X_k = M_k ('mpc') or C_k = sum_{i<=k} M_i ('delta_mpc');
+//   Hess[s1][s2] = q sum_{t >= max(s1,s2)} X_{t-s1}' X_{t-s2} + r I -- along each block diagonal
+//     d = s2 - s1 a running sum of W[b+d][b] = X_{b+d}' X_b (one lane per (d, c1, c2));
+//   rhs[s] = q sum_{t >= s} X_{t-s}' e_t, e_t = ref_t - A^{t+1} z0 - [delta] C_t u_prev;
+//   v = Hess^-1 rhs by an in-LDS Cholesky (right-looking; the trailing update spread over the
+//   wave's lanes) and two triangular solves; u0 = v_0 + u_prev, action = clip(u0).
+// Shapes: nz <= 64, nu <= 8, N = H nu <= 64.  Per env LDS: X [H][nz*nu], M [nz*nu], Hess [N][N],
+// y / e [nz] each (35 KB at nz 32, nu 5, H 10); BL_EPW envs (waves) per workgroup.
+struct BDev {
+  int nz, nu, H, N, delta, per_env;  // per_env: doubles of LDS per env
+  double q, r, uclip;
+};
+// LDS written by other lanes of this wave is read after this (the wave's LDS operations complete
+// in order once issued; the fence keeps the compiler from moving them across)
+DEVI void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+constexpr int BL_EPW = 4;
+__global__ __launch_bounds__(64 * BL_EPW) void k_bilinear(BDev K, const double* __restrict__ A,
+                                                          const double* __restrict__ Bm,
+                                                          const double* __restrict__ HhT, int n,
+                                                          const double* __restrict__ z0g,
+                                                          const double* __restrict__ win,
+                                                          double* __restrict__ uprev, float* __restrict__ action) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int e = blockIdx.x * BL_EPW + w;
+  if (e >= n) return;  // (whole waves: no workgroup barrier below)
+  const int nz = K.nz, nu = K.nu, H = K.H, N = K.N, zu = nz * nu;
+  double* X = lds + (size_t)w * K.per_env;  // [H][zu]
+  double* M = X + H * zu;                   // [zu]
+  double* Hs = M + zu;                      // [N][N]
+  double* zb = Hs + N * N;                  // [nz]: z0, then A^t z0
+  double* eb = zb + nz;                     // [nz]: e_t
+  for (int i = lane; i < nz; i += 64) zb[i] = z0g[(size_t)i * n + e];
+  double up[8];
+#pragma unroll
+  for (int c = 0; c < 8; c++) up[c] = c < nu ? uprev[(size_t)c * n + e] : 0.0;
+  wsync();
+  // B_total = B + sum_j z0_j Hhat_j  (HhT [(i nu + c)][j])
+  for (int o = lane; o < zu; o += 64) {
+    double s = Bm[o];
+    const double* h = HhT + (size_t)o * nz;
+    for (int j = 0; j < nz; j++) s = fma(h[j], zb[j], s);
+    M[o] = s, X[o] = s;
+  }
+  wsync();
+  // M_k = A M_{k-1}; X_k = M_k or X_{k-1} + M_k  (zu <= 512: 8 outputs per lane)
+  for (int k = 1; k < H; k++) {
+    double nm[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const int o = lane + 64 * q;
+      nm[q] = 0.0;
+      if (o < zu) {
+        const int i = o / nu, c = o - i * nu;
+        double s = 0.0;
+        const double* a = A + (size_t)i * nz;
+        for (int j = 0; j < nz; j++) s = fma(a[j], M[j * nu + c], s);
+        nm[q] = s;
+      }
+    }
+    wsync();  // (every lane has read M_{k-1})
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const int o = lane + 64 * q;
+      if (o < zu) {
+        M[o] = nm[q];
+        X[k * zu + o] = K.delta ? X[(k - 1) * zu + o] + nm[q] : nm[q];
+      }
+    }
+    wsync();
+  }
+  // Hessian: lane per (d, c1, c2); Hs[s1][s1 + d](c1, c2) = q S_d(H - 1 - s1 - d),
+  // S_d(m) = sum_{b <= m} W[b + d][b](c1, c2)
+  for (int tr = lane; tr < H * nu * nu; tr += 64) {
+    const int d = tr / (nu * nu), c1 = (tr / nu) % nu, c2 = tr % nu;
+    double S = 0.0;
+    for (int b = 0; b + d < H; b++) {
+      const double* xa = X + (b + d) * zu + c1;  // X_{b+d}[:, c1]
+      const double* xb = X + b * zu + c2;        // X_b[:, c2]
+      double wv = 0.0;
+      for (int i = 0; i < nz; i++) wv = fma(xa[i * nu], xb[i * nu], wv);
+      S += wv;
+      const int s1 = H - 1 - b - d, s2 = s1 + d;  // the block whose sum ends at b
+      const double hv = K.q * S + ((d == 0 && c1 == c2) ? K.r : 0.0);
+      Hs[(s1 * nu + c1) * N + s2 * nu + c2] = hv;
+      Hs[(s2 * nu + c2) * N + s1 * nu + c1] = hv;
+    }
+  }
+  // rhs (lane l = s nu + c): e_t = ref_t - A^{t+1} z0 - [delta] C_t u_prev, rhs[s] += q X_{t-s}' e_t
+  double rhs = 0.0;
+  const int ls = lane / nu, lc = lane - ls * nu;
+  for (int t = 0; t < H; t++) {
+    double yn = 0.0;
+    if (lane < nz) {
+      const double* a = A + (size_t)lane * nz;
+      for (int j = 0; j < nz; j++) yn = fma(a[j], zb[j], yn);
+    }
+    wsync();
+    if (lane < nz) {
+      zb[lane] = yn;
+      double ev = win[((size_t)t * nz + lane) * n + e] - yn;
+      if (K.delta) {
+#pragma unroll
+        for (int c = 0; c < 8; c++)
+          if (c < nu) ev = fma(-X[t * zu + lane * nu + c], up[c], ev);
+      }
+      eb[lane] = ev;
+    }
+    wsync();
+    if (lane < N && ls <= t) {
+      const double* xk = X + (t - ls) * zu + lc;
+      double s = 0.0;
+      for (int i = 0; i < nz; i++) s = fma(xk[i * nu], eb[i], s);
+      rhs = fma(K.q, s, rhs);
+    }
+    wsync();
+  }
+  // Cholesky Hs = L L' in place (lower triangle); the trailing update over (i, k) pairs
+  for (int j = 0; j < N; j++) {
+    const double dj = sqrt(Hs[j * N + j]);
+    wsync();
+    for (int i = j + 1 + lane; i < N; i += 64) Hs[i * N + j] /= dj;
+    if (lane == 0) Hs[j * N + j] = dj;
+    wsync();
+    const int m = N - j - 1;  // trailing size; pairs (i >= k) in [j+1, N)
+    for (int p = lane; p < m * (m + 1) / 2; p += 64) {
+      int ii = (int)((sqrt(8.0 * p + 1.0) - 1.0) * 0.5);  // row of pair p in the packed triangle
+      while ((ii + 1) * (ii + 2) / 2 <= p) ii++;
+      while (ii * (ii + 1) / 2 > p) ii--;
+      const int kk = p - ii * (ii + 1) / 2;
+      const int i = j + 1 + ii, k2 = j + 1 + kk;
+      Hs[i * N + k2] = fma(-Hs[i * N + j], Hs[k2 * N + j], Hs[i * N + k2]);
+    }
+    wsync();
+  }
+  // L y = rhs, L' v = y: lane i holds row i's value
+  double y = rhs;
+  for (int j = 0; j < N; j++) {
+    if (lane == j) eb[0] = y / Hs[j * N + j];
+    wsync();
+    const double yj = eb[0];
+    if (lane == j) y = yj;
+    if (lane > j && lane < N) y = fma(-Hs[lane * N + j], yj, y);
+    wsync();
+  }
+  for (int j = N - 1; j >= 0; j--) {
+    if (lane == j) eb[0] = y / Hs[j * N + j];
+    wsync();
+    const double vj = eb[0];
+    if (lane == j) y = vj;
+    if (lane < j) y = fma(-Hs[j * N + lane], vj, y);
+    wsync();
+  }
+  if (lane < nu) {  // u0 = v_0 + u_prev (get_control, MPC_Controler.py:147-149)
+    double upl = 0.0;
+#pragma unroll
+    for (int c = 0; c < 8; c++) upl = lane == c ? up[c] : upl;
+    const double u0 = y + upl;
+    uprev[(size_t)lane * n + e] = u0;
+    action[(size_t)e * nu + lane] = (float)fmin(fmax(u0, -K.uclip), K.uclip);
+  }
+}
+
 typedef void (*EncodeFn)(KDev, const double*, int, const float*, double*);
 typedef void (*StepFn)(KDev, const double*, int, const float*, const double*, const double*, double*, float*);
 const EncodeFn ENCODE[4] = {k_encode<1>, k_encode<2>, k_encode<3>, k_encode<4>};
@@ -266,6 +436,9 @@ struct sim_koopman {
   KDev kd;
   double* d_frag = nullptr;    // encoder + [Gz | Gu] fragments, biases
   double* d_grfrag = nullptr;  // Gr fragments
+  // DBKN (sim_koopman_set_bilinear): A [nz][nz], B [nz][nu], Hhat as [(i nu + c)][j]
+  BDev bd{};
+  double *d_A = nullptr, *d_B = nullptr, *d_HhT = nullptr;
 };
 
 #define KCHECK(x)                                                                                  \
@@ -373,7 +546,50 @@ void sim_koopman_free(sim_koopman* k) {
   (void)hipSetDevice(k->device);
   (void)hipFree(k->d_frag);
   (void)hipFree(k->d_grfrag);
+  (void)hipFree(k->d_A);
+  (void)hipFree(k->d_B);
+  (void)hipFree(k->d_HhT);
   delete k;
+}
+
+int sim_koopman_set_bilinear(sim_koopman* k, const double* A, const double* B, const double* Hhat, int delta,
+                             double q, double r) {
+  if (!k || !A || !B || !Hhat) return soarm_set_error(SIM_E_ARG, "null argument");
+  const int nz = k->kd.nz, nu = k->kd.ud, H = k->kd.H, N = H * nu;
+  if (nz > 64 || nu > 8 || N > 64) return soarm_set_error(SIM_E_MODEL, "bilinear MPC: nz <= 64, u_dim <= 8, H * u_dim <= 64");
+  if (!(q > 0.0) || !(r > 0.0)) return soarm_set_error(SIM_E_ARG, "bilinear MPC: q and r must be positive");
+  BDev b{};
+  b.nz = nz, b.nu = nu, b.H = H, b.N = N, b.delta = delta ? 1 : 0, b.q = q, b.r = r, b.uclip = k->kd.uclip;
+  b.per_env = (H * nz * nu + nz * nu + N * N + 2 * nz + 1) & ~1;
+  if ((size_t)b.per_env * BL_EPW * 8 > 160 * 1024) return soarm_set_error(SIM_E_MODEL, "bilinear MPC does not fit in LDS");
+  std::vector<double> hht((size_t)nz * nu * nz);
+  for (int j = 0; j < nz; j++)
+    for (int i = 0; i < nz; i++)
+      for (int c = 0; c < nu; c++) hht[((size_t)i * nu + c) * nz + j] = Hhat[((size_t)j * nz + i) * nu + c];
+  KCHECK(hipSetDevice(k->device));
+  (void)hipFree(k->d_A), (void)hipFree(k->d_B), (void)hipFree(k->d_HhT);
+  k->d_A = k->d_B = k->d_HhT = nullptr;
+  KCHECK(hipMalloc(&k->d_A, (size_t)nz * nz * 8));
+  KCHECK(hipMalloc(&k->d_B, (size_t)nz * nu * 8));
+  KCHECK(hipMalloc(&k->d_HhT, hht.size() * 8));
+  KCHECK(hipMemcpy(k->d_A, A, (size_t)nz * nz * 8, hipMemcpyHostToDevice));
+  KCHECK(hipMemcpy(k->d_B, B, (size_t)nz * nu * 8, hipMemcpyHostToDevice));
+  KCHECK(hipMemcpy(k->d_HhT, hht.data(), hht.size() * 8, hipMemcpyHostToDevice));
+  KCHECK(hipFuncSetAttribute((const void*)k_bilinear, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  k->bd = b;
+  return SIM_OK;
+}
+
+int sim_koopman_bilinear_step(sim_koopman* k, int n, const double* z0, const double* window, double* u_prev,
+                              float* action, void* stream) {
+  if (!k || !z0 || !window || !u_prev || !action || n < 0) return soarm_set_error(SIM_E_ARG, "bad argument");
+  if (!k->d_A) return soarm_set_error(SIM_E_ARG, "sim_koopman_set_bilinear was not called");
+  if (n == 0) return SIM_OK;
+  hipLaunchKernelGGL(k_bilinear, dim3((n + BL_EPW - 1) / BL_EPW), dim3(64 * BL_EPW),
+                     (size_t)k->bd.per_env * BL_EPW * sizeof(double), (hipStream_t)stream, k->bd, k->d_A, k->d_B,
+                     k->d_HhT, n, z0, window, u_prev, action);
+  KCHECK(hipGetLastError());
+  return SIM_OK;
 }
 
 int sim_koopman_encode(sim_koopman* k, int m, const float* x, double* z, void* stream) {

@@ -450,6 +450,272 @@ DEVI int mpr(const MPair& P, float& depth, float dir[3], float pos[3], float sep
   }
 }
 
+// ------------------------------------------------------- native GJK / EPA
+// MuJoCo's nativeccd (engine_collision_gjk.c; the oracle's ccd_penetration restates the same
+// algorithm in float64): GJK on the Minkowski difference from the centres' difference until a
+// support plane separates the origin (apart: sep = that axis) or a tetrahedron encloses it, then
+// EPA from that tetrahedron -- the polytope face closest to the origin is expanded by the support
+// point along its normal until the support distance is within the tolerance of the face's.
+// Depth = the closest face's distance, normal = its outward normal (geom1 -> geom2), pos = the
+// midpoint of the witness points (barycentric weights of the origin's projection on that face).
+// The simplex lives in registers (value selects: a lane-varying index would put it in scratch);
+// the polytope, which only penetrating pairs build (a few envs per pair and substep), in private
+// arrays: EPA_KV vertices (v and the geom1 support point; geom2's is v1 - v), EPA_KF faces.
+constexpr int CCD_ITERS = 50;
+constexpr int EPA_KV = 32, EPA_KF = 64, EPA_KE = 48;
+DEVI void copy3(float d[3], const float s[3]) { d[0] = s[0], d[1] = s[1], d[2] = s[2]; }
+// closest point of simplex p[0..n) (n <= 3) to the origin; the carrying sub-simplex moves to the front
+DEVI int gjk_reduce(MSup p[4], int n, float x[3]) {
+  if (n == 1) {
+    copy3(x, p[0].v);
+    return 1;
+  }
+  if (n == 2) {
+    float ab[3];
+    sub(ab, p[1].v, p[0].v);
+    float t = -dot3(p[0].v, ab);
+    const float l2 = dot3(ab, ab);
+    if (t <= 0.f || l2 <= 0.f) {
+      copy3(x, p[0].v);
+      return 1;
+    }
+    if (t >= l2) {
+      p[0] = p[1];
+      copy3(x, p[0].v);
+      return 1;
+    }
+    t /= l2;
+#pragma unroll
+    for (int k = 0; k < 3; k++) x[k] = p[0].v[k] + t * ab[k];
+    return 2;
+  }
+  float ab[3], ac[3];
+  sub(ab, p[1].v, p[0].v);
+  sub(ac, p[2].v, p[0].v);
+  const float ap[3] = {-p[0].v[0], -p[0].v[1], -p[0].v[2]};
+  const float d1 = dot3(ab, ap), d2 = dot3(ac, ap);
+  if (d1 <= 0.f && d2 <= 0.f) {
+    copy3(x, p[0].v);
+    return 1;
+  }
+  const float bp[3] = {-p[1].v[0], -p[1].v[1], -p[1].v[2]};
+  const float d3 = dot3(ab, bp), d4 = dot3(ac, bp);
+  if (d3 >= 0.f && d4 <= d3) {
+    p[0] = p[1];
+    copy3(x, p[0].v);
+    return 1;
+  }
+  const float vc = d1 * d4 - d3 * d2;
+  if (vc <= 0.f && d1 >= 0.f && d3 <= 0.f) {
+    const float t = d1 / (d1 - d3);
+#pragma unroll
+    for (int k = 0; k < 3; k++) x[k] = p[0].v[k] + t * ab[k];
+    return 2;
+  }
+  const float cp[3] = {-p[2].v[0], -p[2].v[1], -p[2].v[2]};
+  const float d5 = dot3(ab, cp), d6 = dot3(ac, cp);
+  if (d6 >= 0.f && d5 <= d6) {
+    p[0] = p[2];
+    copy3(x, p[0].v);
+    return 1;
+  }
+  const float vb = d5 * d2 - d1 * d6;
+  if (vb <= 0.f && d2 >= 0.f && d6 <= 0.f) {
+    const float t = d2 / (d2 - d6);
+#pragma unroll
+    for (int k = 0; k < 3; k++) x[k] = p[0].v[k] + t * ac[k];
+    p[1] = p[2];
+    return 2;
+  }
+  const float va = d3 * d6 - d5 * d4;
+  if (va <= 0.f && (d4 - d3) >= 0.f && (d5 - d6) >= 0.f) {
+    const float t = (d4 - d3) / ((d4 - d3) + (d5 - d6));
+#pragma unroll
+    for (int k = 0; k < 3; k++) x[k] = p[1].v[k] + t * (p[2].v[k] - p[1].v[k]);
+    p[0] = p[2];
+    return 2;
+  }
+  const float den = 1.f / (va + vb + vc), v = vb * den, w = vc * den;
+#pragma unroll
+  for (int k = 0; k < 3; k++) x[k] = p[0].v[k] + ab[k] * v + ac[k] * w;
+  return 3;
+}
+// tetrahedron faces: face k = the vertices other than k
+__device__ constexpr int TETF[4][3] = {{1, 2, 3}, {0, 3, 2}, {0, 1, 3}, {0, 2, 1}};
+// 1: origin inside tetrahedron p; 0: reduced to the face the origin lies beyond (n, x set);
+// -1: flat tetrahedron
+DEVI int tet_contains(MSup p[4], float x[3], int& n) {
+  float best = 0.f;
+  int bk = -1;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const float *a = p[TETF[k][0]].v, *b = p[TETF[k][1]].v, *c = p[TETF[k][2]].v;
+    float ab[3], ac[3], nn[3], ak[3];
+    sub(ab, b, a);
+    sub(ac, c, a);
+    cross(nn, ab, ac);
+    sub(ak, p[k].v, a);
+    const float sg = dot3(nn, ak) > 0.f ? -1.f : 1.f;
+    const float ln = sqrtf(dot3(nn, nn));
+    if (!(ln > 0.f)) return -1;
+    const float sd = -sg * dot3(nn, a) / ln;
+    if (sd > best) best = sd, bk = k;
+  }
+  if (bk < 0) return 1;
+  MSup t[3];
+#pragma unroll
+  for (int j = 0; j < 3; j++) {
+    t[j] = p[TETF[0][j]];
+#pragma unroll
+    for (int k = 1; k < 4; k++) sel(t[j], bk == k, p[TETF[k][j]]);
+  }
+  p[0] = t[0], p[1] = t[1], p[2] = t[2];
+  n = gjk_reduce(p, 3, x);
+  return 0;
+}
+// GJK: true with p a tetrahedron enclosing the origin; false apart (sep = a separating axis when
+// a support plane proved it) or touching
+DEVI bool gjk_enclose(const MPair& P, MSup p[4], float sep[3]) {
+  float c1[3], c2[3], x[3];
+  geom_center(P.m, P.g1, P.P1, c1);
+  geom_center(P.m, P.g2, P.P2, c2);
+  sub(x, c1, c2);
+  if (dot3(x, x) == 0.f) x[0] = 1e-9f;
+  int n = 0;
+  for (int it = 0; it < CCD_ITERS; it++) {
+    const float d[3] = {-x[0], -x[1], -x[2]};
+    MSup s;
+    P.sup(d, s);
+    const float xs = dot3(x, s.v);
+    if (xs > 0.f) {  // every point of A - B has x.p >= x.s > 0: -x separates
+      float a[3] = {-x[0], -x[1], -x[2]};
+      nrm(a);
+      setsep(sep, a);
+      return false;
+    }
+    if (dot3(x, x) - xs <= 1e-12f) return false;  // no progress: the origin is on the boundary
+#pragma unroll
+    for (int k = 0; k < 4; k++) sel(p[k], k == n, s);
+    n++;
+    if (n == 4) {
+      const int r = tet_contains(p, x, n);
+      if (r == 1) return true;
+      if (r < 0) return false;
+    } else {
+      n = gjk_reduce(p, n, x);
+    }
+    if (dot3(x, x) < 1e-30f) return false;  // origin on a lower-dimensional simplex: touching
+  }
+  return false;
+}
+struct EpaFace {
+  uint32_t abc;  // vertex ids, 8 bits each
+  float n[3], d;
+};
+DEVI void epa_face(EpaFace& f, const float (*V)[6], int a, int b, int c) {
+  float ab[3], ac[3];
+  sub(ab, V[b], V[a]);
+  sub(ac, V[c], V[a]);
+  cross(f.n, ab, ac);
+  nrm(f.n);
+  f.abc = (uint32_t)a | ((uint32_t)b << 8) | ((uint32_t)c << 16);
+  f.d = dot3(f.n, V[a]);
+}
+// EPA from the enclosing tetrahedron p: 1 with depth / dir / pos
+DEVI int epa(const MPair& P, const MSup p[4], float& depth, float dir[3], float pos[3]) {
+  float V[EPA_KV][6];  // v (3), geom1 support point (3)
+  EpaFace F[EPA_KF];
+  uint8_t E[EPA_KE][2];
+#pragma unroll
+  for (int k = 0; k < 4; k++) copy3(V[k], p[k].v), copy3(V[k] + 3, p[k].v1);
+  int nv = 4, nf = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    epa_face(F[nf], V, TETF[k][0], TETF[k][1], TETF[k][2]);
+    float ak[3];
+    sub(ak, p[k].v, V[TETF[k][0]]);
+    if (dot3(F[nf].n, ak) > 0.f) epa_face(F[nf], V, TETF[k][0], TETF[k][2], TETF[k][1]);
+    nf++;
+  }
+  int best = 0;
+  float upper = 3.0e38f;
+  for (int it = 0; it < CCD_ITERS; it++) {
+    best = 0;
+    for (int i = 1; i < nf; i++)
+      if (F[i].d < F[best].d) best = i;
+    MSup w;
+    P.sup(F[best].n, w);
+    upper = fminf(upper, dot3(F[best].n, w.v));
+    if (upper - F[best].d < MPR_TOLF || nv == EPA_KV) break;
+    // faces seen from w go; the edges they do not share bound the hole (the horizon)
+    int ne = 0, m = 0;
+    bool full = false;
+    for (int i = 0; i < nf; i++) {
+      const int a = F[i].abc & 255, b = (F[i].abc >> 8) & 255, c = (F[i].abc >> 16) & 255;
+      float aw[3];
+      sub(aw, w.v, V[a]);
+      if (dot3(F[i].n, aw) <= 0.f) {
+        F[m++] = F[i];
+        continue;
+      }
+      const int ed[3][2] = {{a, b}, {b, c}, {c, a}};
+#pragma unroll
+      for (int q = 0; q < 3; q++) {
+        int dup = -1;
+        for (int r = 0; r < ne; r++)
+          if (E[r][0] == ed[q][1] && E[r][1] == ed[q][0]) dup = r;
+        if (dup >= 0) {
+          E[dup][0] = E[ne - 1][0], E[dup][1] = E[ne - 1][1];
+          ne--;
+        } else if (ne < EPA_KE) {
+          E[ne][0] = (uint8_t)ed[q][0], E[ne][1] = (uint8_t)ed[q][1];
+          ne++;
+        } else {
+          full = true;
+        }
+      }
+    }
+    if (ne == 0 || full || m + ne > EPA_KF) {  // (budget exhausted: keep the best face so far)
+      nf = m > 0 ? nf : nf;
+      break;
+    }
+    nf = m;
+    copy3(V[nv], w.v), copy3(V[nv] + 3, w.v1);
+    for (int r = 0; r < ne; r++) epa_face(F[nf++], V, E[r][0], E[r][1], nv);
+    nv++;
+    best = -1;
+  }
+  if (best < 0) {  // (a horizon pass compacted the faces: find the closest again)
+    best = 0;
+    for (int i = 1; i < nf; i++)
+      if (F[i].d < F[best].d) best = i;
+  }
+  const EpaFace f = F[best];
+  const int a = f.abc & 255, b = (f.abc >> 8) & 255, c = (f.abc >> 16) & 255;
+  const float pr[3] = {f.d * f.n[0], f.d * f.n[1], f.d * f.n[2]};
+  float v0[3], v1[3], v2[3];
+  sub(v0, V[b], V[a]);
+  sub(v1, V[c], V[a]);
+  sub(v2, pr, V[a]);
+  const float d00 = dot3(v0, v0), d01 = dot3(v0, v1), d11 = dot3(v1, v1), d20 = dot3(v2, v0), d21 = dot3(v2, v1);
+  const float den = d00 * d11 - d01 * d01;
+  if (!(den > 0.f)) return 0;
+  const float lb = (d11 * d20 - d01 * d21) / den, lc = (d00 * d21 - d01 * d20) / den, la = 1.f - lb - lc;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const float x1 = la * V[a][3 + k] + lb * V[b][3 + k] + lc * V[c][3 + k];
+    pos[k] = x1 - 0.5f * pr[k];  // (x1 + x2) / 2 with x2 = x1 - pr
+    dir[k] = f.n[k];
+  }
+  depth = f.d;
+  return f.d > 0.f;
+}
+DEVI int ccd_native(const MPair& P, float& depth, float dir[3], float pos[3], float sep[3]) {
+  MSup p[4];
+  if (!gjk_enclose(P, p, sep)) return 0;
+  return epa(P, p, depth, dir, pos);
+}
+
 // ------------------------------------------------------------- primitives
 // append one contact (dropped past the pair's slot count)
 DEVI void emit(PairOut& o, float dist, const float pos[3], const float n[3]) {
@@ -929,7 +1195,7 @@ DEVI void narrowphase(const DModel& m, int p, const GeomPose& P1, const GeomPose
   }
   MPair mp{m, g1, g2, P1, P2};
   float depth, dir[3], pos[3], sep[3] = {0.f, 0.f, 0.f};
-  if (mpr(mp, depth, dir, pos, sep)) {
+  if (m.ccd == SIM_CCD_NATIVE ? ccd_native(mp, depth, dir, pos, sep) : mpr(mp, depth, dir, pos, sep)) {
     emit(o, -depth, pos, dir);
     o.xc = 5;
   } else {

@@ -155,11 +155,18 @@ enum { L_DOF = 0, L_SGN = 1, L_AREF = 2, L_R = 3, L_ARD = 4, L_IARD = 5, L_FRC =
 // cost(f0) - cost(f1) = sum_r ARdiag_r / 2 (f1 - f0)_r (s0 + s1)_r, summed over the row.
 constexpr int WIDE_R = 16;       // block edges = lanes per env in the wide sweep
 constexpr int WIDE_COLS = 16;    // envs per workgroup
-enum { WIDE_SKIP = 0, WIDE_WORK = 1, WIDE_EXIT = 2 };
+// Extra rows (the extra-slot variants, after the arm's frictionloss rows retire): F's and E's
+// 4 edges ride in a second register slot of lanes 0-7 (rows 16-19 F, 20-23 E: the quad sweep's
+// order block, F, E).  WIDE_WORK + NX selects the sweep with NX = 0, 4 (E) or 8 (F, E) extra rows.
+constexpr int WIDE_X = 8;
+constexpr int WIDE_S = WIDE_R + WIDE_X;  // steps of the longest sweep
+enum { WIDE_SKIP = 0, WIDE_WORK = 1, WIDE_EXIT = 2, WIDE_WORK4 = 3, WIDE_WORK8 = 4 };
 struct WideLds {
-  float C[WIDE_COLS][WIDE_R][WIDE_R];  // [env][row][step]
+  float C[WIDE_COLS][WIDE_R][WIDE_S];   // [env][row][step]: the block's rows
+  float C1[WIDE_COLS][WIDE_X][WIDE_S];  // the extra rows (slot 1 of lanes 0..NX-1)
   float s[WIDE_COLS][WIDE_R], f[WIDE_COLS][WIDE_R], hd[WIDE_COLS][WIDE_R];
-  int it[WIDE_COLS];                   // first sweep index (>= iterations: nothing to do)
+  float s1[WIDE_COLS][WIDE_X], f1[WIDE_COLS][WIDE_X], hd1[WIDE_COLS][WIDE_X];
+  int it[WIDE_COLS];                    // first sweep index (>= iterations: nothing to do)
   int flag;
 };
 template <int Q>
@@ -174,40 +181,70 @@ DEVI float rowsum16(float x) {
   x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x128, 0xF, 0xF, false));  // row_ror:8
   return rowbcast<0>(x);
 }
-template <int Q>
-DEVI void wide_step(const float (&Cr)[WIDE_R], const float (&oh)[WIDE_R], float& s, float& f) {
+// one row step: the stepping slot's projected step max(s, -f) is broadcast from lane Q % 16,
+// every row moves by its C entry, the stepping row's force takes the step (oh: one-hot of the
+// lane's row, so only lane Q % 16 changes)
+template <int Q, int NX>
+DEVI void wide_step(const float (&C0)[WIDE_S], const float (&C1)[WIDE_S], const float (&oh)[WIDE_R], float& s0,
+                    float& f0, float& s1, float& f1) {
+  constexpr bool X = Q >= WIDE_R;
   float cand;
-  asm("v_max_f32_e64 %0, %1, -%2" : "=v"(cand) : "v"(s), "v"(f));  // max(s, -f), see max_neg
-  s = fmaf(Cr[Q], rowbcast<Q>(cand), s);
-  f = fmaf(oh[Q], cand, f);  // lane Q only (oh = one-hot of the lane's row)
+  asm("v_max_f32_e64 %0, %1, -%2" : "=v"(cand) : "v"(X ? s1 : s0), "v"(X ? f1 : f0));  // max(s, -f), see max_neg
+  const float d = rowbcast<Q % WIDE_R>(cand);
+  s0 = fmaf(C0[Q], d, s0);
+  if constexpr (NX > 0) s1 = fmaf(C1[Q], d, s1);
+  if constexpr (X)
+    f1 = fmaf(oh[Q % WIDE_R], cand, f1);
+  else
+    f0 = fmaf(oh[Q], cand, f0);
 }
-template <int... Qs>
-DEVI void wide_sweep(const float (&Cr)[WIDE_R], const float (&oh)[WIDE_R], float& s, float& f,
-                     std::integer_sequence<int, Qs...>) {
-  (wide_step<Qs>(Cr, oh, s, f), ...);
+template <int NX, int... Qs>
+DEVI void wide_sweep(const float (&C0)[WIDE_S], const float (&C1)[WIDE_S], const float (&oh)[WIDE_R], float& s0,
+                     float& f0, float& s1, float& f1, std::integer_sequence<int, Qs...>) {
+  (wide_step<Qs, NX>(C0, C1, oh, s0, f0, s1, f1), ...);
 }
 // The wide sweeps of the envs handed over in W, by every thread t of the workgroup (env t / 16,
 // edge t % 16); each env continues from its own sweep index until its stopping test passes.
+template <int NX>
 DEVI void wide_sweeps(const DModel& m, WideLds& W, int t) {
   const int c = t >> 4, r = t & 15;
-  float Cr[WIDE_R], oh[WIDE_R];
+  const bool x = NX > 0 && r < NX;  // this lane holds an extra row in slot 1
+  float C0[WIDE_S], C1[WIDE_S], oh[WIDE_R];
 #pragma unroll
-  for (int q = 0; q < WIDE_R; q++) Cr[q] = W.C[c][r][q], oh[q] = q == r ? 1.f : 0.f;
-  float s = W.s[c][r], f = W.f[c][r];
-  const float hd = W.hd[c][r], scale = m.pgs_scale, tol = m.tolerance;
+  for (int q = 0; q < WIDE_S; q++) {
+    C0[q] = q < WIDE_R + NX ? W.C[c][r][q] : 0.f;
+    C1[q] = (q < WIDE_R + NX && x) ? W.C1[c][r & (WIDE_X - 1)][q] : 0.f;
+  }
+#pragma unroll
+  for (int q = 0; q < WIDE_R; q++) oh[q] = q == r ? 1.f : 0.f;
+  float s0 = W.s[c][r], f0 = W.f[c][r];
+  float s1 = x ? W.s1[c][r & (WIDE_X - 1)] : 0.f, f1 = x ? W.f1[c][r & (WIDE_X - 1)] : 0.f;
+  const float hd0 = W.hd[c][r], hd1 = x ? W.hd1[c][r & (WIDE_X - 1)] : 0.f;
+  const float scale = m.pgs_scale, tol = m.tolerance;
   int it = W.it[c];
   const int iters = m.iterations;
   for (; it < iters; it++) {
-    const float s0 = s, f0 = f;
-    wide_sweep(Cr, oh, s, f, std::make_integer_sequence<int, WIDE_R>{});
-    const float imp = rowsum16(hd * (f - f0) * (s0 + s));
+    const float s00 = s0, f00 = f0, s10 = s1, f10 = f1;
+    wide_sweep<NX>(C0, C1, oh, s0, f0, s1, f1, std::make_integer_sequence<int, WIDE_R + NX>{});
+    float im = hd0 * (f0 - f00) * (s00 + s0);
+    if constexpr (NX > 0) im = fmaf(hd1 * (f1 - f10), s10 + s1, im);
+    const float imp = rowsum16(im);
     if (imp * scale < tol) {
       it++;
       break;
     }
   }
-  W.f[c][r] = f;
+  W.f[c][r] = f0;
+  if (x) W.f1[c][r & (WIDE_X - 1)] = f1;
   if (r == 0) W.it[c] = it;
+}
+DEVI void wide_dispatch(const DModel& m, WideLds& W, int t, int flag) {
+  if (flag == WIDE_WORK)
+    wide_sweeps<0>(m, W, t);
+  else if (flag == WIDE_WORK4)
+    wide_sweeps<4>(m, W, t);
+  else if (flag == WIDE_WORK8)
+    wide_sweeps<8>(m, W, t);
 }
 
 // Per-env LDS state, [field][column]: one column per env of the workgroup (64 / lanes per
@@ -1832,7 +1869,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       if (sub == 0) W.it[col] = it0;
       W.flag = WIDE_WORK;
       __syncthreads();
-      wide_sweeps(m, W, L.lane);
+      wide_sweeps<0>(m, W, L.lane);
       __syncthreads();
 #pragma unroll
       for (int k = 0; k < FC; k++)

@@ -421,7 +421,7 @@ __global__ __launch_bounds__(WIDE ? 256 : 64) void k_substep(const DModel* __res
         __syncthreads();
         const int fl = s_wide.flag;
         if (fl == WIDE_EXIT) return;
-        if (fl == WIDE_WORK) wide_sweeps(*dm, s_wide, (int)threadIdx.x);
+        wide_dispatch(*dm, s_wide, (int)threadIdx.x, fl);
         __syncthreads();
       }
     }
@@ -930,6 +930,7 @@ static int validate_and_build(const sim_model_desc& d, sim_model* M) {
   if (na != 6 || nf > 1) return fail(SIM_E_MODEL, "kernels are compiled for a 6-hinge arm + <=1 free body");
   if (d.solver != SIM_SOL_PGS && d.solver != SIM_SOL_NEWTON)
     return fail(SIM_E_MODEL, "solver must be PGS or Newton");
+  if (d.ccd != SIM_CCD_MPR && d.ccd != SIM_CCD_NATIVE) return fail(SIM_E_MODEL, "ccd must be MPR or native");
   if (d.nv != na + 6 * nf || d.nq != na + 7 * nf) return fail(SIM_E_MODEL, "nq/nv mismatch");
   if (d.nu > na) return fail(SIM_E_MODEL, "more actuators than arm hinges");
   for (int a = 0; a < d.nu; a++)
@@ -955,6 +956,7 @@ static int validate_and_build(const sim_model_desc& d, sim_model* M) {
   m.obs_site = d.obs_site, m.obs_nq = d.obs_nq;
   for (int k = 0; k < SIM_MAXOBSQ; k++) m.obs_qadr[k] = d.obs_qadr[k];
   m.iterations = d.iterations, m.disable_contact = d.disable_contact;
+  m.ccd = d.ccd;
   bool anyd = false;
   for (int i = 0; i < d.nv; i++) anyd |= d.dof_damping[i] > 0;
   m.eulerdamp = (!d.disable_eulerdamp && anyd) ? 1 : 0;

@@ -166,10 +166,16 @@ def _contact_poses(cm, n):
     return q.astype(np.float32).astype(np.float64)
 
 
-def test_contacts_match_oracle(gpu_lib, arm_model, cube_model):
-    """Same contact pairs in the same order (bit-exact indexing); geometry within fp32 tolerance."""
+@pytest.mark.parametrize("ccd", ["mpr", "native"])
+def test_contacts_match_oracle(gpu_lib, arm_model, cube_model, ccd):
+    """Same contact pairs in the same order (bit-exact indexing); geometry within fp32 tolerance.
+    Both convex-convex narrowphases: libccd MPR and MuJoCo's native GJK/EPA (kernel vs oracle)."""
     import torch
-    for cm in (arm_model, cube_model):
+    from lerobot_mujoco_sim2real_amd import mjcf
+    models = (arm_model, cube_model) if ccd == "mpr" else \
+        (mjcf.compile_mjcf(mjcf.SCENE_XML, ccd="native"), mjcf.compile_mjcf(mjcf.CUBE_SCENE_XML, ccd="native"))
+    for cm in models:
+        assert cm.desc.ccd == (1 if ccd == "native" else 0)
         n = 512
         S, orc = make_sim(cm, n), Oracle(cm)
         q = _contact_poses(cm, n)
@@ -580,7 +586,18 @@ def test_golden_fixture_gpu(gpu_lib, arm_model_nocontact):
         obs.append(to_np(S.step(a.astype(np.float32))))
     obs = np.stack(obs)
     np.testing.assert_allclose(obs[:2], z["obs"][:2], atol=1e-4)
-    np.testing.assert_allclose(obs, z["obs"], atol=3e-2)
+    # later steps: the shadowing envelope (test_trajectory_shadowing) of the fixture itself -- the
+    # fp64 oracle replaying the fixture's inputs with its state re-rounded to fp32 every env-step
+    orc = Oracle(arm_model_nocontact)
+    st = orc.new_state(z["init_qpos"].shape[0])
+    env = [np.abs(orc.reset(st, init_qpos=z["init_qpos"]) - z["obs"][0])]
+    for t, a in enumerate(z["actions"]):
+        for k in ("qpos", "qvel", "warm"):
+            st[k][:] = st[k].astype(np.float32)
+        env.append(np.abs(orc.step(st, a) - z["obs"][t + 1]))
+    run = np.maximum.accumulate(np.stack(env).max(axis=(1, 2)))  # running max over steps
+    err = np.abs(obs - z["obs"]).max(axis=(1, 2))
+    assert (err <= 10 * run + 2e-4).all(), (err, run)
 
 
 def test_datacollection_layout_and_replay(gpu_lib, arm_model_nocontact):
@@ -847,7 +864,16 @@ def test_pgs_vs_reference_newton(gpu_lib):
         assert_pct(dv[~arm, 6:].max(1), 4e-5, 5e-5, 1e-4, what=f"t{t0} block envs cube qvel")
         assert_pct(dv[~arm, :6].max(1), 1e-6, 1e-6, 2e-6, what=f"t{t0} block envs arm qvel")
         if arm.any():
-            assert dv[arm, 6:].max() < 2e-2 and dv[arm, :6].max() < 1e-3, (dv[arm].max(0))
+            # arm-contact envs (3 at t = 20, 13 at t = 120 in 4096): bars at ~2x the measured
+            # PGS-vs-exact-optimum gap (r03_newton_gap.json, device PGS: cube qvel p50 3.6e-5 /
+            # max 7.1e-3, arm qvel p50 4.5e-6 / max 2.4e-4) -- the PGS algorithm's own distance,
+            # identical in the fp64 oracle PGS, which the device PGS must match within QVEL_BARS
+            assert_pct(dv[arm, 6:].max(1), 8e-5, 1.5e-2, 1.5e-2, what=f"t{t0} arm-contact envs cube qvel")
+            assert_pct(dv[arm, :6].max(1), 1e-5, 5e-4, 5e-4, what=f"t{t0} arm-contact envs arm qvel")
+            pgs = {k: v[arm].copy() for k, v in st.items()}
+            orc.step(pgs, None, nsub=1)
+            dp = np.abs(to_np(S.qvel).T[arm] - pgs["qvel"])
+            assert dp.max() <= QVEL_BARS[2], ("device PGS vs oracle PGS on arm-contact envs", dp.max(0))
 
 
 @pytest.mark.parametrize("t0", [20, 120])

@@ -295,15 +295,15 @@ def test_get_control_single_env(gpu_lib):
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind", ["delta_mpc", "mpc"])
 def test_bilinear_control_gpu(gpu_lib, kind):
-    """DBKN: step_bilinear for n envs (HIP lift + batched float64 QPs on the device) and
-    get_control(p) == the oracle's per-env restatement."""
+    """DBKN: step_bilinear for n envs (HIP lift + the per-env float64 QP kernel k_bilinear) and
+    get_control(p) == the oracle's per-env restatement of the reference's cost loop."""
     import torch
     net = make_bnet(9)
     ctl = _ctl(net, kind)
     assert ctl.bilinear
     A, B, layers = net_mats(net)
     Hhat = net.get_Hi_numpy()
-    n, H = 512, 10
+    n, H = 515, 10  # (not a whole number of 4-env workgroups)
     x = sample_states(n).astype(np.float32)
     ref = KO.encode(layers, sample_states(n * H)).reshape(n, H, -1)
     up0 = RNG.uniform(-0.5, 0.5, (n, 5))
@@ -353,13 +353,18 @@ def test_step_with_applied_force(gpu_lib, arm_model_nocontact, arm_model):
         og = to_np(S.step(a))
         app64 = app.astype(np.float32).astype(np.float64)
         oc = orc.step(st, a.astype(np.float64), applied=app64)
-        err = np.abs(og - oc)
+        err = np.abs(og - oc).max(1)  # per env
         # a missing or mis-scaled applied force moves every env by ~h^2 |f| / M ~ 1e-3; the bulk is
         # at fp32 resolution.  A few envs whose wrist servo chatters (h kv / M ~ 3, see
-        # test_gpu_parity's shadowing tests) amplify fp32 rounding within one env-step: the max bar
-        # allows those (measured 1.8e-3 in 512 x 2 envs, r03).
-        assert np.median(err) < 1e-6 and np.percentile(err, 99) < 5e-5 and err.max() < 1e-2, (
-            np.median(err), np.percentile(err, 99), err.max())
+        # test_gpu_parity's shadowing tests) amplify fp32 rounding within one env-step: they are
+        # held to the oracle's own sensitivity there -- the same env-step from the state with qvel
+        # perturbed by one fp32 ulp (the shadowing envelope) -- and p99.9 to 5e-4.
+        pert = {k: v.copy() for k, v in st.items()}
+        pert["qvel"] = np.nextafter(pert["qvel"].astype(np.float32), np.float32(np.inf)).astype(np.float64)
+        env = np.abs(orc.step(pert, a.astype(np.float64), applied=app64) - oc).max(1)
+        assert np.median(err) < 1e-6 and np.percentile(err, 99.9) < 5e-4, (np.median(err), np.percentile(err, 99.9))
+        bad = err > 10 * env + 1e-5
+        assert bad.sum() == 0, (np.nonzero(bad)[0], err[bad], env[bad])
         S.reset(init_qpos=np.zeros((n, 5), np.float32))
         assert float(S.qfrc_applied.abs().max()) == 0.0
 

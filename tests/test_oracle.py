@@ -235,3 +235,52 @@ def test_golden_regression(arm_model_nocontact):
     for a in z["actions"]:
         obs.append(orc.step(st, a))
     np.testing.assert_allclose(np.stack(obs), z["obs"], atol=1e-9)
+
+
+def _world_hull(cm, xp, xm, g):
+    """World-frame vertices of geom g's convex shape (box corners or mesh hull)."""
+    d = cm.desc
+    if d.geom_type[g] == abi.GEOM_BOX:
+        h = np.array(d.geom_size[g])
+        loc = np.array([[sx * h[0], sy * h[1], sz * h[2]] for sx in (-1, 1) for sy in (-1, 1) for sz in (-1, 1)])
+    else:
+        a, nv = d.geom_hulladr[g], d.geom_hullnum[g]
+        loc = cm.hull_vert[a:a + nv].astype(np.float64)
+    return xp[g] + loc @ xm[g].T
+
+
+@pytest.mark.parametrize("xml", ["arm", "cube"])
+def test_native_ccd_is_minimum_penetration(xml):
+    """The oracle's native GJK/EPA (oracle_collision.c, MuJoCo's nativeccd restated) returns the
+    minimum penetration of each convex-convex contact: with h(d) = max_A x.d - min_B x.d the
+    Minkowski difference's support, its normal n has h(n) = depth within the EPA tolerance, and no
+    sampled direction d has h(d) < depth (the depth is the minimum over directions).  MPR, also
+    checked, satisfies h(n) >= depth only (it is not a minimum-depth method)."""
+    from test_gpu_parity import _contact_poses  # (the poses of the GPU contact test)
+    path = mjcf.SCENE_XML if xml == "arm" else mjcf.CUBE_SCENE_XML
+    rng = np.random.default_rng(5)
+    dirs = rng.normal(size=(6000, 3))
+    dirs /= np.linalg.norm(dirs, axis=1, keepdims=True)
+    for ccd in ("native", "mpr"):
+        cm = mjcf.compile_mjcf(path, ccd=ccd)
+        orc = Oracle(cm)
+        q = _contact_poses(cm, 48)
+        full = cube_qpos(cm, 48, np.random.default_rng(3), q) if cm.nq > 6 else q
+        n_conv = 0
+        for e in range(len(full)):
+            xp, xm = orc.geom_frames(full[e])
+            for r in orc.forward(full[e])["contacts"]:
+                g1, g2 = int(r[7]), int(r[8])
+                if not (cm.desc.geom_type[g1] in (abi.GEOM_BOX, abi.GEOM_MESH) and cm.desc.geom_type[g2] == abi.GEOM_MESH):
+                    continue
+                A, B = _world_hull(cm, xp, xm, g1), _world_hull(cm, xp, xm, g2)
+                n, depth = r[4:7], -r[0]
+                hn = (A @ n).max() - (B @ n).min()
+                if ccd == "native":
+                    assert abs(hn - depth) <= 2e-6, (e, g1, g2, hn, depth)
+                    hmin = ((A @ dirs.T).max(0) - (B @ dirs.T).min(0)).min()
+                    assert hmin >= depth - 1e-9, (e, g1, g2, hmin, depth)
+                else:
+                    assert hn >= depth - 2e-6, (e, g1, g2, hn, depth)
+                n_conv += 1
+        assert n_conv >= 20, (ccd, n_conv)
