@@ -111,11 +111,18 @@ struct NewtonRows {
   // Hessian terms added to H (packed lower over the subsystem's dofs; zero on entry), and sig, a
   // signature of this lane's rows' zones (quadratic / linear / inactive): Newton has converged
   // once a full step leaves every lane's unchanged (the cost is one quadratic there)
+  // The signature is exact (no two zone patterns collide): per lane at most ceil(LDS_CON / QL) LDS
+  // contacts x 4 edges (1 bit each), ceil(4 (SIM_MAXCON - LDS_CON) / QL) overflow edges (1 bit),
+  // NA frictionloss rows (3 zones: < 2 bits) and <= 2 NA limit rows (1 bit) -- 42 bits at QL 4,
+  // in a 64-bit word (a 32-bit shift signature dropped the oldest rows' zones).
+  static constexpr int SIG_BITS = 4 * ((LDS_CON + QL - 1) / QL) + (4 * (SIM_MAXCON - LDS_CON) + QL - 1) / QL +
+                                  2 * NA + 2 * NA;
+  static_assert(!CON || SIG_BITS <= 64, "zone signature must fit its 64-bit word");
   template <int LO, int HI, bool WANT_H>
-  DEVI float pass(const float a[NV], float jtf[NV], float H[], uint32_t& sig) const {
+  DEVI float pass(const float a[NV], float jtf[NV], float H[], uint64_t& sig) const {
     constexpr int NR = HI - LO, NH = NR * (NR + 1) / 2;
     float cost = 0.f;
-    sig = 0u;
+    sig = 0ull;
 #pragma unroll
     for (int i = LO; i < HI; i++) jtf[i] = 0.f;
     if constexpr (CON) {
@@ -141,7 +148,7 @@ struct NewtonRows {
           const int t = 1 + (ed >> 1);
           const float x = y[0] + s * y[t] - L.at(c, F_AREF + ed);
           const bool act = x < 0.f;
-          sig = sig * 2u + (act ? 1u : 0u);
+          sig = sig * 2ull + (act ? 1ull : 0ull);
           const float xa = act ? x : 0.f, Da = act ? D : 0.f;  // (branch-free)
           cost += 0.5f * xa * xa * D;
           const float f = -xa * D;
@@ -189,7 +196,7 @@ struct NewtonRows {
           float J[NV], x = -cr.S(r, 0);
 #pragma unroll
           for (int i = 0; i < NV; i++) J[i] = cr.J(r, i), x = fmaf(J[i], a[i], x);
-          sig = sig * 2u + (x < 0.f ? 1u : 0u);
+          sig = sig * 2ull + (x < 0.f ? 1ull : 0ull);
           if (x < 0.f) {
             const float D = cr.S(r, 2), f = -x * D;
             cost += 0.5f * x * x * D;
@@ -228,7 +235,7 @@ struct NewtonRows {
         const float flx = x < 0.f ? fl : -fl;
         jtf[i] += lin ? flx : -x * iR;
         cost += lin ? fmaf(fl, fabsf(x), -0.5f * Rfl * fl) : 0.5f * x * x * iR;
-        sig = sig * 3u + (q ? 1u : (x < 0.f ? 2u : 0u));
+        sig = sig * 3ull + (q ? 1ull : (x < 0.f ? 2ull : 0ull));
         if constexpr (WANT_H) H[hidx(i, i)] += q ? iR : 0.f;
       }
       // joint limits (J = sign e_dof)
@@ -239,7 +246,7 @@ struct NewtonRows {
 #pragma unroll
         for (int i = 0; i < NA; i++) ad = i == d ? a[i] : ad;
         const float x = sg * ad - L.lm(l, L_AREF);
-        sig = sig * 2u + (x < 0.f ? 1u : 0u);
+        sig = sig * 2ull + (x < 0.f ? 1ull : 0ull);
         if (x < 0.f) {
           cost += 0.5f * x * x * iR;
           const float f = -x * iR;
@@ -420,7 +427,7 @@ DEVI int newton_range(const Sim<NA, NF>& S, const NewtonRows<NA, NF, CON>& R, fl
     return c;
   };
   float H[NH], Ma[NV];
-  uint32_t sig = 0u;
+  uint64_t sig = 0ull;
   // warm start: qacc_warmstart unless qacc_smooth costs less (on this subsystem's cost); the
   // Hessian pass runs at the warm point, and again at qacc_smooth only in lanes where it wins
   float cost;
@@ -508,7 +515,7 @@ DEVI int newton_range(const Sim<NA, NF>& S, const NewtonRows<NA, NF, CON>& R, fl
     for (int i = 0; i < NV; i++) an_[i] = fmaf(al, p[i], a[i]);
 #pragma unroll
     for (int i = 0; i < NH; i++) H[i] = 0.f;
-    const uint32_t sig0 = sig;
+    const uint64_t sig0 = sig;
     const float cn = gauss(an_, Man) + R.template pass<LO, HI, true>(an_, jn, H, sig);
     NT_STAMP(3);
     if (!(cn <= cost + 1e-5f * fabsf(cost))) break;  // a real increase (numerical trouble): keep a

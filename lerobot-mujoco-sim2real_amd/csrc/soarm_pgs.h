@@ -2015,6 +2015,24 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
           qvarm(xq.eWp, D);
         }
       }
+      // verification: the retired frictionloss rows were never re-checked against the
+      // v_arm that E (and F) kept moving.  One full sweep with them; if it moves them by more than
+      // ARM_RETIRE on some lane, the full sweeps resume until the stopping test passes.
+      if (fret) {
+        float fa1 = 0.f, ff1 = 0.f;
+        sweep(std::true_type{}, std::true_type{}, fa1, ff1);
+        if (!__all(ff1 <= ARM_RETIRE)) {
+          done = false;
+          for (it++; it < m.iterations; it++) {
+            float fa2 = 0.f, ff2 = 0.f;
+            if (sweep(std::true_type{}, std::true_type{}, fa2, ff2) * scale < m.tolerance) {
+              done = true;
+              break;
+            }
+          }
+          done = true;  // (no block-only sweeps after these: the block took part in them)
+        }
+      }
     }
     if constexpr (RETIRE) {
       // the block-only sweeps hold far fewer values than the sweeps with the arm's rows:

@@ -11,3 +11,5 @@ for c in mpr native; do
   timeout -k 10 600 python bench.py --no-cpu-baseline --no-other-solver --ccd $c > gpurun_out/bench_$c.json 2> gpurun_out/bench_$c.err || exit $?
   python -c "import json; d=json.loads(open('gpurun_out/bench_$c.json').read().strip().split(chr(10))[-1]); print('$c', 'value', round(d['value']), 'steady', round(d['steady_state']['value']) if d['steady_state'] else None, {k: round(x,4) for k,x in d['roofline']['kernel_ms_per_step'].items()})"
 done
+timeout -k 10 600 python bench.py --no-cpu-baseline --config mpc_dbkn > gpurun_out/bench_mpc_dbkn.json 2> gpurun_out/bench_mpc_dbkn.err || exit $?
+python -c "import json; d=json.loads(open('gpurun_out/bench_mpc_dbkn.json').read().strip().split(chr(10))[-1]); print('mpc_dbkn', round(d['value']), d['ms_per_step'])"
