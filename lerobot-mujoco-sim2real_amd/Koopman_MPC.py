@@ -15,8 +15,12 @@ Per frame k of a T-frame reference ``state_all_ref = [cartesian xyz, joint angle
 feedforward terms once (the reference recomputes the same lifted rows every frame), then each
 frame is ``sim_bias`` + ``sim_koopman_mpc_step`` + ``sim_step``.  With a ``communicator``
 (``utility.ZMQ.ZMQCommunicator``) each frame also publishes env ``stream_env_id``'s joint angles
-as real-robot targets, as the reference does after its step (:186-190).  The viewer drawing
-and the return-to-home playback after the last frame (:137-175) are out of scope.
+as real-robot targets, as the reference does after its step (:186-190).  Past the last frame
+``runFunc`` plays the reference's return to the model's ``home`` keyframe (:62-81, :148-183): one
+frame builds the 20-point joint-space path from the last reference pose to home, the next 20 set
+``qpos`` along it and step with ``home_ctrl``, and every later frame holds ``qpos = home`` and
+steps (the last reference pose when the model has no ``home`` key).  The viewer drawing is out of
+scope.
 """
 from .sim import BatchSim
 from .utility.ZMQ import stream_env
@@ -57,6 +61,16 @@ class KoopmanMPCTracking:
         self.u_prev = torch.zeros((controller.u_dim, self.n), dtype=torch.float64, device=dev)
         self.action = torch.empty((self.n, controller.u_dim), dtype=torch.float32, device=dev)
         self.traj_index = 0
+        # the "home" keyframe (Koopman_MPC.py:62-76) and the return playback state (:78-81)
+        home = getattr(model, "keyframes", {}).get("home") if model is not None else None
+        self.home_qpos = None if home is None or home["qpos"] is None else \
+            torch.as_tensor(home["qpos"], dtype=torch.float32, device=dev)
+        nu = controller.u_dim
+        hc = home["ctrl"] if home is not None and home["ctrl"] is not None else [0.0] * nu
+        self.home_ctrl = torch.as_tensor(hc[:nu], dtype=torch.float32, device=dev).expand(self.n, nu).contiguous()
+        self.return_traj = None
+        self.return_index = 0
+        self.return_duration = 2.0
 
     def runBefore(self):
         """qpos[:num_joints] = joint_angle_traj[0] on a fresh MjData (qvel, ctrl, warm start 0),
@@ -71,10 +85,7 @@ class KoopmanMPCTracking:
         """One frame: gravity compensation, MPC, env.step (Koopman_MPC.py:110-136, 197-222)."""
         k = self.traj_index
         if k >= self.total_frames:
-            # the reference switches to its hold / return-home playback here (Koopman_MPC.py:148-183),
-            # which is out of scope (DESIGN.md section 9)
-            raise IndexError(f"runFunc: frame {k} is past the trajectory's {self.total_frames} frames "
-                             "(return-home playback is not built)")
+            return self._after_trajectory()
         self.sim.bias(out=self.sim.qfrc_applied)
         if self.ff is None:
             self.ctl.step_bilinear(self.state, self.zpad[k + 1:k + 1 + self.H], self.u_prev, self.action)
@@ -82,6 +93,33 @@ class KoopmanMPCTracking:
             self.ctl.step(self.state, self.ff[k], self.u_prev, self.action)
         self.state = self.sim.step(self.action)
         if self.communicator is not None:  # sim -> real (Koopman_MPC.py:186-190)
+            stream_env(self.sim, self.communicator, self.stream_env_id)
+        self.traj_index += 1
+        return self.state
+
+    def _after_trajectory(self):
+        """Koopman_MPC.py:148-183 for every env: build the return path (one frame, no step), play
+        it (qpos[:nj] = path point, mj_forward, step(home_ctrl)), then hold home; gravity
+        compensation and the sim -> real stream every frame as in the tracking frames."""
+        torch, nj = self.torch, self.num_joints
+        self.sim.bias(out=self.sim.qfrc_applied)  # qfrc_applied = qfrc_bias (:119)
+        if self.return_traj is None and self.home_qpos is not None:  # phase 2 (:150-165)
+            start = self.state_all_ref[-1, :, 3:3 + nj].T                  # joint_angle_traj[-1] [nj, n]
+            end = self.home_qpos[:nj, None].expand_as(start)
+            steps = int(self.return_duration / 0.1)
+            w = torch.linspace(0.0, 1.0, steps, device=start.device, dtype=torch.float64)[:, None, None]
+            self.return_traj = ((1 - w) * start.double() + w * end.double()).float()  # np.linspace rows
+            self.return_index = 0
+        else:
+            if self.return_traj is not None and self.return_index < len(self.return_traj):  # phase 3
+                self.sim.qpos[:nj] = self.return_traj[self.return_index]
+                self.return_index += 1
+            else:  # phase 4: hold home (or the last reference pose)
+                hold = self.home_qpos[:nj, None] if self.home_qpos is not None else \
+                    self.state_all_ref[-1, :, 3:3 + nj].T
+                self.sim.qpos[:nj] = hold
+            self.state = self.sim.step(self.home_ctrl)  # (mj_forward is inside the step)
+        if self.communicator is not None:
             stream_env(self.sim, self.communicator, self.stream_env_id)
         self.traj_index += 1
         return self.state

@@ -1842,16 +1842,42 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       }
     }
   };
-  // The wide kernel's hand-over round (see WideLds): every call of this solve on wave 0 runs
-  // exactly one round, WORK from the pure / uncoupled block-only sweeps below, else SKIP, so
-  // the helper waves' barriers pair with wave 0's.  WORK: each quad lane writes its block
-  // contact's 4 rows (scaled residuals, forces, ARdiag/2, its rows of C), the 4 waves sweep,
-  // and the quad reads the 16 forces back.
-  bool wide_done = false;
-  auto wide_round = [&](int it0, auto pk) {
+  // extras in row order: F = the first of two (arm-only), E = the last one
+  const int cE = npost >= 1 ? xidx(npost - 1) : LDS_CON, cF = npost == 2 ? xidx(0) : LDS_CON;
+  const bool hasE = npost >= 1, hasF = npost == 2;
+  // The wide kernel's hand-over round (see WideLds).  Wave 0 writes the rows, the 4 waves sweep,
+  // wave 0 reads the forces back; the helper waves wait at the workgroup barrier between rounds
+  // (a solve may run none).  Each quad lane writes its block contact's 4 rows (scaled residuals,
+  // forces, ARdiag/2, its rows of C); with NX extra rows (the extra-slot variants after the arm's
+  // frictionloss rows retire: E, or F then E), also their columns of C and, in the second slot of
+  // wide lanes 0..NX-1, the extra rows themselves (lane sub writes F's / E's edge sub):
+  //   C[block (k,e)][E d] = (X_kE folded, as qe01/qe23) . u^E_d,
+  //   C[E d'][block (j,e)] = -(1/ARd_E,d') w^E_d' . X_jE' u^j_e,   C[E d'][E d] = -(w^E_d' G_E u^E_d + R_E)/ARd_E,d',
+  //   C[F d'][F d] = -(w^F_d' G_F u^F_d + R_F)/ARd_F,d',  C[F d'][E d] / C[E d'][F d] through X_EF,
+  // with u^c_d = w^c_d = (1, +-mu_c on t(d)) the contact-space direction of edge d.
+  auto wide_round = [&](int it0, auto pk, auto nxc, auto cpl) {
+    constexpr int NX = decltype(nxc)::value;
     WideLds& W = *L.wide;
     if constexpr (decltype(pk)::value && QUAD) {
       const int col = L.col;
+      auto edir = [](int d, float mu, int q) {  // component q of (1, +-mu on t(d))
+        return q == 0 ? 1.f : (q == 1 + (d >> 1) ? ((d & 1) ? -mu : mu) : 0.f);
+      };
+      const float muE = NX ? xq.eMu : 0.f, muF = NX == 8 ? xq.fMu : 0.f;
+      float GE[3][3], GF[3][3], XEF[3][3];  // XEF[q][r] = J_E,arm[q] W_F[r]
+      {
+        float ge[6], gf[6];
+#pragma unroll
+        for (int i = 0; i < 6; i++) ge[i] = NX ? EX(E_G + i) : 0.f, gf[i] = NX == 8 ? L.at(cF, F_GRAM + i) : 0.f;
+        const int P[3][3] = {{0, 1, 2}, {1, 3, 4}, {2, 4, 5}};
+#pragma unroll
+        for (int q = 0; q < 3; q++)
+#pragma unroll
+          for (int r = 0; r < 3; r++) {
+            GE[q][r] = ge[P[q][r]], GF[q][r] = gf[P[q][r]];
+            XEF[q][r] = NX == 8 ? EX(F_XE + 3 * q + r) : 0.f;
+          }
+      }
 #pragma unroll
       for (int ed = 0; ed < 4; ed++) {
         const int row = 4 * sub + ed;
@@ -1865,26 +1891,111 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
             const f2 cc = ed < 2 ? C01[j][d] : C23[j][d];
             W.C[col][row][4 * j + d] = (ed & 1) ? cc.y : cc.x;
           }
+        if constexpr (NX > 0) {
+          float qe[3];  // this block edge's residual change per unit contact-space step of E
+#pragma unroll
+          for (int q = 0; q < 3; q++) {
+            const f2 p2 = ed < 2 ? xq.qe01[q] : xq.qe23[q];
+            qe[q] = (ed & 1) ? p2.y : p2.x;
+          }
+#pragma unroll
+          for (int d = 0; d < 4; d++) {
+            float cE = 0.f;
+#pragma unroll
+            for (int q = 0; q < 3; q++) cE = fmaf(qe[q], edir(d, muE, q), cE);
+            if (NX == 8) W.C[col][row][WIDE_R + d] = 0.f;  // F is arm-only
+            W.C[col][row][WIDE_R + NX - 4 + d] = decltype(cpl)::value ? cE : 0.f;
+          }
+        }
+      }
+      if constexpr (NX > 0) {
+        const int dp = sub;  // this lane writes edge dp of E (and of F)
+        {  // E row dp
+          const int x = NX - 4 + dp;
+          const float ia = EX(E_IA + dp), Rp = xq.eRp;
+          const float yt = dp < 2 ? yE[1] : yE[2];
+          const float se = (dp & 1) ? -muE : muE;
+          const float fEd = dp == 0 ? fE[0] : dp == 1 ? fE[1] : dp == 2 ? fE[2] : fE[3];
+          W.s1[col][x] = -(fmaf(Rp, fEd, fmaf(se, yt, yE[0]))) * ia;
+          W.f1[col][x] = fEd;
+          W.hd1[col][x] = EX(E_HD + dp);
+#pragma unroll
+          for (int j = 0; j < FC; j++)
+#pragma unroll
+            for (int e2 = 0; e2 < 4; e2++) {
+              float v = 0.f;  // w^E_dp . X_jE' u^j_e2
+#pragma unroll
+              for (int q = 0; q < 3; q++)
+#pragma unroll
+                for (int rr = 0; rr < 3; rr++)
+                  v = fmaf(edir(dp, muE, q) * EX(E_X + 9 * j + 3 * rr + q), edir(e2, ymu[j], rr), v);
+              W.C1[col][x][4 * j + e2] = decltype(cpl)::value ? -ia * v : 0.f;
+            }
+#pragma unroll
+          for (int d = 0; d < 4; d++) {
+            float vE = 0.f, vF = 0.f;
+#pragma unroll
+            for (int q = 0; q < 3; q++)
+#pragma unroll
+              for (int r = 0; r < 3; r++) {
+                vE = fmaf(edir(dp, muE, q) * GE[q][r], edir(d, muE, r), vE);
+                vF = fmaf(edir(dp, muE, q) * XEF[q][r], edir(d, muF, r), vF);
+              }
+            W.C1[col][x][WIDE_R + NX - 4 + d] = -ia * (vE + (d == dp ? Rp : 0.f));
+            if (NX == 8) W.C1[col][x][WIDE_R + d] = -ia * vF;
+          }
+        }
+        if constexpr (NX == 8) {  // F row dp
+          const int x = dp;
+          const float ia = EX(F_IA + dp), Rp = xq.fRp;
+          float yF[3];
+#pragma unroll
+          for (int q = 0; q < 3; q++) {
+            float t = -EX(F_SH + q);
+#pragma unroll
+            for (int i = 0; i < NA; i++) t = fmaf(EX(F_J + 6 * q + i), v[i], t);
+            yF[q] = t;
+          }
+          const float se = (dp & 1) ? -muF : muF;
+          const float fFd = dp == 0 ? fF[0] : dp == 1 ? fF[1] : dp == 2 ? fF[2] : fF[3];
+          W.s1[col][x] = -(fmaf(Rp, fFd, fmaf(se, dp < 2 ? yF[1] : yF[2], yF[0]))) * ia;
+          W.f1[col][x] = fFd;
+          W.hd1[col][x] = EX(F_HD + dp);
+#pragma unroll
+          for (int q = 0; q < WIDE_R; q++) W.C1[col][x][q] = 0.f;
+#pragma unroll
+          for (int d = 0; d < 4; d++) {
+            float vF = 0.f, vE = 0.f;
+#pragma unroll
+            for (int q = 0; q < 3; q++)
+#pragma unroll
+              for (int r = 0; r < 3; r++) {
+                vF = fmaf(edir(dp, muF, q) * GF[q][r], edir(d, muF, r), vF);
+                vE = fmaf(edir(dp, muF, r) * XEF[q][r], edir(d, muE, q), vE);  // w^F . X_EF' u^E
+              }
+            W.C1[col][x][WIDE_R + d] = -ia * (vF + (d == dp ? Rp : 0.f));
+            W.C1[col][x][WIDE_R + 4 + d] = -ia * vE;
+          }
+        }
       }
       if (sub == 0) W.it[col] = it0;
-      W.flag = WIDE_WORK;
+      W.flag = NX == 0 ? WIDE_WORK : NX == 4 ? WIDE_WORK4 : WIDE_WORK8;
       __syncthreads();
-      wide_sweeps<0>(m, W, L.lane);
+      wide_sweeps<NX>(m, W, L.lane);
       __syncthreads();
 #pragma unroll
       for (int k = 0; k < FC; k++)
 #pragma unroll
         for (int ed = 0; ed < 4; ed++) cfo[k][ed] = W.f[col][4 * k + ed];
-    } else {
-      W.flag = WIDE_SKIP;
-      __syncthreads();
-      __syncthreads();
+      if constexpr (NX > 0) {
+#pragma unroll
+        for (int ed = 0; ed < 4; ed++) {
+          fE[ed] = W.f1[col][NX - 4 + ed];
+          if (NX == 8) fF[ed] = W.f1[col][ed];
+        }
+      }
     }
-    wide_done = true;
   };
-  // extras in row order: F = the first of two (arm-only), E = the last one
-  const int cE = npost >= 1 ? xidx(npost - 1) : LDS_CON, cF = npost == 2 ? xidx(0) : LDS_CON;
-  const bool hasE = npost >= 1, hasF = npost == 2;
   auto ysweeps = [&](auto ext, auto coupled, auto ext2) {
     yblock_setup();
     using PK = std::integral_constant<bool, QUAD>;
@@ -1988,7 +2099,27 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       float fE0[4];
 #pragma unroll
       for (int ed = 0; ed < 4; ed++) fE0[ed] = fE[ed];
-      if (fret && !done)
+      if (fret && !done && L.wide) {
+        // the wide kernel: block + E (+ F) one lane per edge until the stopping test passes;
+        // v_arm takes E's (and F's) total force change afterwards (nothing reads it meanwhile)
+        float fF0[4];
+#pragma unroll
+        for (int ed = 0; ed < 4; ed++) fF0[ed] = fF[ed];
+        wide_round(it, PK{}, std::integral_constant<int, decltype(ext2)::value ? 8 : 4>{}, coupled);
+        done = true;
+#ifdef SOARM_PHASE_PROF
+        it = L.wide->it[L.col] - 1;
+#endif
+        if constexpr (decltype(ext2)::value) {
+          float dE[4], dF[4];
+#pragma unroll
+          for (int ed = 0; ed < 4; ed++) dE[ed] = fE[ed] - fE0[ed], dF[ed] = fF[ed] - fF0[ed];
+          const float DE[3] = {(dE[0] + dE[1]) + (dE[2] + dE[3]), xq.eMu * (dE[0] - dE[1]), xq.eMu * (dE[2] - dE[3])};
+          const float DF[3] = {(dF[0] + dF[1]) + (dF[2] + dF[3]), xq.fMu * (dF[0] - dF[1]), xq.fMu * (dF[2] - dF[3])};
+          qvarm(xq.eWp, DE);
+          qvarm(xq.fWp, DF);
+        }
+      } else if (fret && !done)
         for (; it < m.iterations; it++) {
           float famax = 0.f, ffmax = 0.f;
           if (sweep(std::true_type{}, std::false_type{}, famax, ffmax) * scale < m.tolerance) {
@@ -2049,11 +2180,13 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
         vpin(ro01), vpin(ro23);
       }
       if (L.wide) {  // wave-uniform: the 4-wave kernel sweeps the block one lane per edge
-        wide_round(done ? m.iterations : it, std::bool_constant<PK::value>{});
+        if (!done) {
+          wide_round(it, std::bool_constant<PK::value>{}, std::integral_constant<int, 0>{}, std::false_type{});
 #ifdef SOARM_PHASE_PROF
-        it = L.wide->it[L.col] - 1;
-        done = it + 1 < m.iterations || done;
+          it = L.wide->it[L.col] - 1;
+          done = it + 1 < m.iterations;
 #endif
+        }
       } else if (!done)
         for (; it < m.iterations; it++) {
           float unused = 0.f, unused2 = 0.f;
@@ -2119,7 +2252,6 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   } else {
     sweeps(std::false_type{});
   }
-  if (L.wide && !wide_done) wide_round(0, std::false_type{});  // (SKIP: see wide_round)
   if constexpr (NF == 1 && CON) {  // the block's forces back to their records (for J' f)
 #pragma unroll
     for (int k = 0; k < FC; k++)

@@ -410,9 +410,26 @@ def test_tracking_loop_matches_oracle(gpu_lib, arm_model):
         q = run.sim.qpos[:6, 3].double().cpu().numpy()
         assert json.loads(sent.msgs[-1]) == real_targets(q) and len(sent.msgs) == k + 1
     assert int(run.sim.status.abs().sum()) == 0
-    # past the last frame the reference plays back its return-home path (out of scope): a clear error
-    with pytest.raises(IndexError, match="past the trajectory"):
-        run.runFunc()
+    # past the last frame: the reference's return to the "home" keyframe (Koopman_MPC.py:148-183).
+    # Frame T builds the 20-point path (no step); frames T+1..T+20 set qpos[:nj] along it and step
+    # with home_ctrl; later frames hold home.  Each checked against the oracle doing the same.
+    home = np.asarray(arm_model.keyframes["home"]["qpos"], np.float64)
+    hctrl = np.asarray(arm_model.keyframes["home"]["ctrl"], np.float64)[:5]
+    before = run.sim.qpos.cpu().numpy().copy()
+    run.runFunc()
+    np.testing.assert_array_equal(run.sim.qpos.cpu().numpy(), before)  # path built, no step
+    path = np.linspace(jq[-1].astype(np.float32).astype(np.float64), np.broadcast_to(home[:5], (n, 5)), 20)
+    for i in range(24):
+        c64 = lambda t: np.ascontiguousarray(t.cpu().numpy().T, dtype=np.float64)  # noqa: E731
+        st = {"qpos": c64(run.sim.qpos), "qvel": c64(run.sim.qvel), "warm": c64(run.sim.qacc_warmstart),
+              "ctrl": c64(run.sim.ctrl), "status": run.sim.status.cpu().numpy().copy(), "ncon": np.zeros(n)}
+        applied = orc.bias(st)  # qfrc_applied = qfrc_bias before qpos is overwritten (:119)
+        st["qpos"][:, :5] = (path[i] if i < 20 else np.broadcast_to(home[:5], (n, 5))).astype(np.float32)
+        obs = run.runFunc().cpu().numpy()
+        oc = orc.step(st, np.broadcast_to(hctrl, (n, 5)).copy(), applied=applied)
+        err = np.abs(obs - oc)
+        assert np.median(err) < 2e-6 and err.max() < 1e-3, (i, np.median(err), err.max())
+    assert len(sent.msgs) == T + 25
 
 
 @pytest.mark.gpu
