@@ -234,8 +234,8 @@ DEVI void wide_sweeps(const DModel& m, WideLds& W, int t) {
       break;
     }
   }
-  W.f[c][r] = f0;
-  if (x) W.f1[c][r & (WIDE_X - 1)] = f1;
+  W.f[c][r] = f0, W.s[c][r] = s0;  // (the residuals too: a quad sweep may follow, see wide_round)
+  if (x) W.f1[c][r & (WIDE_X - 1)] = f1, W.s1[c][r & (WIDE_X - 1)] = s1;
   if (r == 0) W.it[c] = it;
 }
 DEVI void wide_dispatch(const DModel& m, WideLds& W, int t, int flag) {
@@ -1987,11 +1987,23 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       for (int k = 0; k < FC; k++)
 #pragma unroll
         for (int ed = 0; ed < 4; ed++) cfo[k][ed] = W.f[col][4 * k + ed];
+      // the quad's sweep state back from the rows (the verification sweep after frictionloss
+      // retirement continues from it): this lane's block residuals, and E's contact-space y from
+      // its edge residuals, r_d = -s_d ARdiag_d = y0 +- mu y_t(d) + R f_d
+      ro01 = f2{W.s[col][4 * sub], W.s[col][4 * sub + 1]}, ro23 = f2{W.s[col][4 * sub + 2], W.s[col][4 * sub + 3]};
       if constexpr (NX > 0) {
+        float rr[4];
 #pragma unroll
         for (int ed = 0; ed < 4; ed++) {
           fE[ed] = W.f1[col][NX - 4 + ed];
           if (NX == 8) fF[ed] = W.f1[col][ed];
+          const float ia = EX(E_IA + ed);
+          rr[ed] = (ia > 0.f ? -W.s1[col][NX - 4 + ed] / ia : 0.f) - xq.eRp * fE[ed];
+        }
+        if (muE > 0.f) {
+          yE[0] = 0.25f * ((rr[0] + rr[1]) + (rr[2] + rr[3]));
+          yE[1] = 0.5f * (rr[0] - rr[1]) / muE;
+          yE[2] = 0.5f * (rr[2] - rr[3]) / muE;
         }
       }
     }
