@@ -647,17 +647,19 @@ DEVI int epa(const MPair& P, const MSup p[4], float& depth, float dir[3], float 
     P.sup(F[best].n, w);
     upper = fminf(upper, dot3(F[best].n, w.v));
     if (upper - F[best].d < MPR_TOLF || nv == EPA_KV) break;
-    // faces seen from w go; the edges they do not share bound the hole (the horizon)
-    int ne = 0, m = 0;
+    // faces seen from w go; the edges they do not share bound the hole (the horizon).  The
+    // polytope is left untouched until the expansion is known to fit (a budget exit keeps it and
+    // its closest face intact).
+    uint64_t vis = 0ull;
+    int ne = 0, nvis = 0;
     bool full = false;
     for (int i = 0; i < nf; i++) {
       const int a = F[i].abc & 255, b = (F[i].abc >> 8) & 255, c = (F[i].abc >> 16) & 255;
       float aw[3];
       sub(aw, w.v, V[a]);
-      if (dot3(F[i].n, aw) <= 0.f) {
-        F[m++] = F[i];
-        continue;
-      }
+      if (dot3(F[i].n, aw) <= 0.f) continue;
+      vis |= 1ull << i;
+      nvis++;
       const int ed[3][2] = {{a, b}, {b, c}, {c, a}};
 #pragma unroll
       for (int q = 0; q < 3; q++) {
@@ -675,10 +677,10 @@ DEVI int epa(const MPair& P, const MSup p[4], float& depth, float dir[3], float 
         }
       }
     }
-    if (ne == 0 || full || m + ne > EPA_KF) {  // (budget exhausted: keep the best face so far)
-      nf = m > 0 ? nf : nf;
-      break;
-    }
+    if (ne == 0 || full || nf - nvis + ne > EPA_KF) break;  // (budget exhausted: the best face so far)
+    int m = 0;
+    for (int i = 0; i < nf; i++)
+      if (!((vis >> i) & 1ull)) F[m++] = F[i];
     nf = m;
     copy3(V[nv], w.v), copy3(V[nv] + 3, w.v1);
     for (int r = 0; r < ne; r++) epa_face(F[nf++], V, E[r][0], E[r][1], nv);

@@ -630,14 +630,18 @@ static int epa(const mpair* P, msup* V, double* depth, double dir[3], double pos
     double dw = dot3(F[best].n, w.v);
     if (dw < upper) upper = dw;
     if (upper - F[best].d < CCD_TOL || nv == EPA_MAXV) break;
-    /* faces seen from w go; their boundary (edges not shared by two of them) is the horizon */
-    int E[3 * EPA_MAXF][2], ne = 0;
+    /* faces seen from w go; their boundary (edges not shared by two of them) is the horizon.
+       The polytope is untouched until the expansion is known to fit. */
+    int E[3 * EPA_MAXF][2], ne = 0, nvis = 0;
+    unsigned char vis[EPA_MAXF];
     for (int i = 0; i < nf; i++) {
+      vis[i] = 0;
       if (!F[i].live) continue;
       double aw[3];
       sub3(aw, w.v, V[F[i].a].v);
       if (dot3(F[i].n, aw) <= 0) continue;
-      F[i].live = 0;
+      vis[i] = 1;
+      nvis++;
       const int ed[3][2] = {{F[i].a, F[i].b}, {F[i].b, F[i].c}, {F[i].c, F[i].a}};
       for (int q = 0; q < 3; q++) {
         int dup = -1;
@@ -652,16 +656,20 @@ static int epa(const mpair* P, msup* V, double* depth, double dir[3], double pos
         }
       }
     }
-    if (ne == 0) break;
-    /* compact the face list, then add one face per horizon edge */
+    if (ne == 0 || nf - nvis + ne > EPA_MAXF) break; /* (budget: keep the best face so far) */
     int m = 0;
     for (int i = 0; i < nf; i++)
-      if (F[i].live) F[m++] = F[i];
+      if (F[i].live && !vis[i]) F[m++] = F[i];
     nf = m;
-    if (nf + ne > EPA_MAXF) break;
     V[nv] = w;
     for (int r = 0; r < ne; r++) epa_face_set(&F[nf++], V, E[r][0], E[r][1], nv);
     nv++;
+    best = -1;
+  }
+  if (best < 0) {
+    best = 0;
+    for (int i = 1; i < nf; i++)
+      if (F[i].d < F[best].d) best = i;
   }
   /* witness points of the closest face */
   const epa_face* f = &F[best];
