@@ -160,8 +160,9 @@ constexpr int WIDE_COLS = 16;    // envs per workgroup
 // order block, F, E).  WIDE_WORK + NX selects the sweep with NX = 0, 4 (E) or 8 (F, E) extra rows.
 constexpr int WIDE_X = 8;
 constexpr int WIDE_S = WIDE_R + WIDE_X;  // steps of the longest sweep
-enum { WIDE_SKIP = 0, WIDE_WORK = 1, WIDE_EXIT = 2, WIDE_WORK4 = 3, WIDE_WORK8 = 4 };
+enum { WIDE_SKIP = 0, WIDE_WORK = 1, WIDE_EXIT = 2, WIDE_WORK4 = 3, WIDE_WORK8 = 4, WIDE_GEOM = 5 };
 struct WideLds {
+  float qpos[WIDE_COLS][SIM_MAXQ];      // WIDE_GEOM: the new positions whose geom poses the helpers write
   float C[WIDE_COLS][WIDE_R][WIDE_S];   // [env][row][step]: the block's rows
   float C1[WIDE_COLS][WIDE_X][WIDE_S];  // the extra rows (slot 1 of lanes 0..NX-1)
   float s[WIDE_COLS][WIDE_R], f[WIDE_COLS][WIDE_R], hd[WIDE_COLS][WIDE_R];

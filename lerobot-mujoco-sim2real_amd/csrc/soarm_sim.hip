@@ -421,6 +421,19 @@ __global__ __launch_bounds__(WIDE ? 256 : 64) void k_substep(const DModel* __res
         __syncthreads();
         const int fl = s_wide.flag;
         if (fl == WIDE_EXIT) return;
+        if (fl == WIDE_GEOM) {
+          // the next substep's geom poses, while wave 0 stores the state and the obs: 12 lanes
+          // per env (the FK chain on each, every 12th geom of a body); no closing barrier -- the
+          // next round is wave 0's EXIT
+          const int h = (int)threadIdx.x - 64, c = h / 12, k = h - 12 * c;
+          const int eg = blockIdx.x * WIDE_COLS + c;
+          Sim<NA, NF> G(dm, 1.f, -1.f, 1.f);
+#pragma unroll
+          for (int i = 0; i < Sim<NA, NF>::NQ; i++) G.qpos[i] = s_wide.qpos[c][i];
+          G.kinematics();
+          write_geom_poses(G, gpose, n, eg, k, 12);
+          continue;
+        }
         wide_dispatch(*dm, s_wide, (int)threadIdx.x, fl);
         __syncthreads();
       }
@@ -501,6 +514,15 @@ __global__ __launch_bounds__(WIDE ? 256 : 64) void k_substep(const DModel* __res
   PSTAMP(11);
   S.integrate();
   PSTAMP(12);
+  if constexpr (WIDE) {
+    if (gpose) {  // hand the new positions to the helper waves for the next substep's geom poses
+      if ((threadIdx.x & 3) == 0)
+#pragma unroll
+        for (int i = 0; i < Sim<NA, NF>::NQ; i++) s_wide.qpos[L.col][i] = S.qpos[i];
+      s_wide.flag = WIDE_GEOM;
+      __syncthreads();
+    }
+  }
   store_state(S, st, n, e);
   if (st.ncon) st.ncon[e] = ncon_prev + (float)ncon;
   if (obs) {
@@ -508,7 +530,7 @@ __global__ __launch_bounds__(WIDE ? 256 : 64) void k_substep(const DModel* __res
     write_obs(S, obs, e);
   }
   PSTAMP(13);
-  if (gpose) {
+  if (!WIDE && gpose) {
     S.kinematics();
     PSTAMP(14);
     write_geom_poses(S, gpose, n, e, (int)threadIdx.x % lpe<NF>(), lpe<NF>());
