@@ -366,6 +366,30 @@ def test_one_substep_domain_randomised(gpu_lib):
     assert to_np(S.ncon).sum() == st["ncon"].sum()
 
 
+def test_dr_env_step_full_size(gpu_lib):
+    """BASELINE config 4 at its per-GPU size: 8192 envs (65536 over 8 GPUs) of the pick scene with
+    per-env mass / friction / damping DR, one graph-captured 10-substep env-step (the one-wave
+    kernel: 8192 envs fill the SIMDs without the wide workgroup) from t = 40 bench states against
+    one oracle env-step with the same parameters; the bars of the headline's full-size test."""
+    from lerobot_mujoco_sim2real_amd import workloads as W
+    n = 8192
+    cm, orc, st, prm = _bench_states("dr", n, 40, nthreads=16)
+    p = W.dr_params(np.arange(n))
+    S = make_sim(cm, n)
+    S.set_params(**p)
+    a = W.chirp_action(W.chirp_tables(np.arange(n)), 40).astype(np.float32)
+    st["ncon"][:] = 0
+    load_state(S, st)
+    og = to_np(S.step(a))
+    oc = orc.step(st, a.astype(np.float64), params=prm, nthreads=16)
+    assert_pct(np.abs(og - oc).max(1), 1e-6, 2e-6, 2e-4, what="obs")
+    dv = np.abs(to_np(S.qvel).T - st["qvel"])
+    assert_pct(dv[:, 6:].max(1), 5e-6, 5e-4, 2e-2, what="cube qvel")
+    assert_pct(dv[:, :6].max(1), 5e-6, 5e-4, 0.1, what="arm qvel")
+    np.testing.assert_allclose(to_np(S.qpos).T[:, 6:9], st["qpos"][:, 6:9], atol=5e-6)
+    assert int((to_np(S.status) != 0).sum()) == int((st["status"] != 0).sum())
+
+
 @pytest.mark.parametrize("n", [1, 100])
 def test_odd_batch_sizes(gpu_lib, cube_model, n):
     """Batches that are not a multiple of the 64-lane wave (tail lanes masked)."""
