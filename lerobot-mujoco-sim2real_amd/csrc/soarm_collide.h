@@ -50,12 +50,21 @@ struct GeomPose {
   float p[3], R[9];
 };
 
-// geom world poses in global memory, SoA [geom*12 + k][env]
+// geom world records in global memory, SoA [geom*GREC + k][env]: position (3), rotation (9), then
+// what the midphase reads -- the world centre of the geom's collision box (3) and that box's
+// world-axis half-extents |R| h (3) -- so a pair the midphase rejects (~80 of the 86 candidate pairs
+// of an env) costs 12 loads instead of the 24 of two full poses; the values are the ones the
+// midphase computed from the poses before (same expressions), so its decisions are unchanged
+constexpr int GREC = 18;
 DEVI void load_pose(const float* __restrict__ gpose, int n, int e, int g, GeomPose& o) {
 #pragma unroll
-  for (int k = 0; k < 3; k++) o.p[k] = soa(gpose, g * 12 + k, n, e);
+  for (int k = 0; k < 3; k++) o.p[k] = soa(gpose, g * GREC + k, n, e);
 #pragma unroll
-  for (int k = 0; k < 9; k++) o.R[k] = soa(gpose, g * 12 + 3 + k, n, e);
+  for (int k = 0; k < 9; k++) o.R[k] = soa(gpose, g * GREC + 3 + k, n, e);
+}
+DEVI void load_bound(const float* __restrict__ gpose, int n, int e, int g, float c[3], float h[3]) {
+#pragma unroll
+  for (int k = 0; k < 3; k++) c[k] = soa(gpose, g * GREC + 12 + k, n, e), h[k] = soa(gpose, g * GREC + 15 + k, n, e);
 }
 
 // contacts of one candidate pair (<= 4: box-box / plane-box corners; 1 otherwise), written
@@ -1007,7 +1016,7 @@ DEVI void box_box(const DModel& m, int g1, int g2, const GeomPose& P1, const Geo
   emit(o, -best / 1.05f, pos, bn);
 }
 
-// world poses of every collidable geom of this env -> global SoA [geom*12+k][env]
+// world records (pose + midphase bound, GREC floats) of every collidable geom of this env
 template <int NA, int NF>
 // geoms g0, g0 + gstep, ... of each body (quad mode: lane k of the quad writes every 4th)
 DEVI void write_geom_poses(const Sim<NA, NF>& S, float* __restrict__ gpose, int n, int e, int g0 = 0,
@@ -1033,44 +1042,50 @@ DEVI void write_geom_poses(const Sim<NA, NF>& S, float* __restrict__ gpose, int 
       float w[3], R[9];
       mv(w, bR, gp);
       mm(R, bR, m.geom_mat[g]);
+      GeomPose P;
 #pragma unroll
-      for (int c = 0; c < 3; c++) soa(gpose, g * 12 + c, n, e) = bp[c] + w[c];
+      for (int c = 0; c < 3; c++) P.p[c] = bp[c] + w[c], soa(gpose, g * GREC + c, n, e) = P.p[c];
 #pragma unroll
-      for (int c = 0; c < 9; c++) soa(gpose, g * 12 + 3 + c, n, e) = R[c];
+      for (int c = 0; c < 9; c++) P.R[c] = R[c], soa(gpose, g * GREC + 3 + c, n, e) = R[c];
+      float cc[3];
+      geom_center(m, g, P, cc);
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        soa(gpose, g * GREC + 12 + k, n, e) = cc[k];
+        soa(gpose, g * GREC + 15 + k, n, e) = fabsf(R[3 * k]) * m.geom_half[g][0] + fabsf(R[3 * k + 1]) * m.geom_half[g][1] +
+                                              fabsf(R[3 * k + 2]) * m.geom_half[g][2];
+      }
     }
   }
 }
 
-// midphase of candidate pair p: bounding spheres and world-aligned boxes, and for a plane the
-// other geom's bounding sphere above it.  false: no contact is possible.
-DEVI bool midphase(const DModel& m, int p, const GeomPose& P1, const GeomPose& P2) {
+// midphase of candidate pair p from the geoms' records: bounding spheres and world-aligned boxes
+// (before the poses are loaded), and for a plane the other geom's bounding sphere above it.
+// false: no contact is possible.  P1 / P2 are loaded here when the pair survives.
+DEVI bool midphase(const DModel& m, int p, const float* __restrict__ gpose, int n, int e, GeomPose& P1,
+                   GeomPose& P2) {
   const int g1 = m.pair_geom1[p], g2 = m.pair_geom2[p];
+  float c2[3], h2[3];
+  if (m.geom_rbound[g2] > 0.f) load_bound(gpose, n, e, g2, c2, h2);
   if (m.geom_rbound[g1] > 0.f && m.geom_rbound[g2] > 0.f) {
-    float c1[3], c2[3], r[3];
-    geom_center(m, g1, P1, c1);
-    geom_center(m, g2, P2, c2);
+    float c1[3], h1[3], r[3];
+    load_bound(gpose, n, e, g1, c1, h1);
     sub(r, c1, c2);
     const float mg = m.pair_margin[p];
     const float rr = m.geom_rbound[g1] + m.geom_rbound[g2] + mg;
     if (dot3(r, r) > rr * rr) return false;
     bool sep = false;
 #pragma unroll
-    for (int k = 0; k < 3; k++) {
-      const float e1 = fabsf(P1.R[3 * k]) * m.geom_half[g1][0] + fabsf(P1.R[3 * k + 1]) * m.geom_half[g1][1] +
-                       fabsf(P1.R[3 * k + 2]) * m.geom_half[g1][2];
-      const float e2 = fabsf(P2.R[3 * k]) * m.geom_half[g2][0] + fabsf(P2.R[3 * k + 1]) * m.geom_half[g2][1] +
-                       fabsf(P2.R[3 * k + 2]) * m.geom_half[g2][2];
-      sep |= fabsf(r[k]) > e1 + e2 + mg;
-    }
+    for (int k = 0; k < 3; k++) sep |= fabsf(r[k]) > h1[k] + h2[k] + mg;
     if (sep) return false;
   }
+  load_pose(gpose, n, e, g1, P1);
   if (m.geom_type[g1] == SIM_GEOM_PLANE && m.geom_rbound[g2] > 0.f) {
     // bounding sphere of geom2 entirely above the plane (beyond the margin): no contact
-    float c2[3];
-    geom_center(m, g2, P2, c2);
     const float h = (c2[0] - P1.p[0]) * P1.R[2] + (c2[1] - P1.p[1]) * P1.R[5] + (c2[2] - P1.p[2]) * P1.R[8];
     if (h > m.geom_rbound[g2] + m.pair_margin[p]) return false;
   }
+  load_pose(gpose, n, e, g2, P2);
   return true;
 }
 
@@ -1209,10 +1224,11 @@ DEVI void narrowphase(const DModel& m, int p, const GeomPose& P1, const GeomPose
 }  // namespace soarm
 
 namespace soarm {
-// midphase + narrowphase of candidate pair p
-DEVI void collide_pair(const DModel& m, int p, const GeomPose& P1, const GeomPose& P2, PairOut& o,
-                         const SepCache& sc = SepCache{nullptr, 0, 0}) {
+// midphase + narrowphase of candidate pair p of env e (geom records in gpose)
+DEVI void collide_pair(const DModel& m, int p, const float* __restrict__ gpose, int n, int e, PairOut& o,
+                       const SepCache& sc = SepCache{nullptr, 0, 0}) {
   o.n = 0;
-  if (midphase(m, p, P1, P2)) narrowphase(m, p, P1, P2, o, sc);
+  GeomPose P1, P2;
+  if (midphase(m, p, gpose, n, e, P1, P2)) narrowphase(m, p, P1, P2, o, sc);
 }
 }  // namespace soarm

@@ -127,7 +127,7 @@ struct sim_batch {
   DModel* d_model = nullptr;   // shared per (model, device): DevModel
   float* d_scratch = nullptr;  // contact rows, [slot][env]
   size_t scratch_floats = 0;
-  float* d_gpose = nullptr;    // geom world poses [geom*12+k][env]
+  float* d_gpose = nullptr;    // geom world records [geom*GREC+k][env] (pose + midphase bound)
   float* d_cbuf = nullptr;     // collide output [slot*7+f][env]
   int* d_ccount = nullptr;     // contacts per pair [pair][env]
   uint32_t* d_pmask = nullptr; // pairs with contacts, bit p%32 of word p/32: [word][env]
@@ -340,11 +340,8 @@ __global__ __launch_bounds__(256, SOARM_COLLIDE_WAVES) void k_collide(const DMod
   if (e >= n) return;
   const long long t0 = pcyc ? clock64() : 0;
   const DModel& m = *dm;
-  GeomPose P1, P2;
-  load_pose(gpose, n, e, m.pair_geom1[p], P1);
-  load_pose(gpose, n, e, m.pair_geom2[p], P2);
   PairOut o{cbuf, n, e, m.pair_slot[p], m.pair_cap[p], 0};
-  collide_pair(m, p, P1, P2, o, SepCache{sepax, n, e});
+  collide_pair(m, p, gpose, n, e, o, SepCache{sepax, n, e});
   // (no per-pair count is stored: the pair mask bit and, for multi-contact pairs, its 2-bit
   // count word carry it -- an empty pair costs no store)
   (void)ccount;
@@ -1405,7 +1402,7 @@ int sim_batch_create(const sim_model* m, int n_envs, int device, sim_batch** out
     const int nv = m->desc.nv;
     B->scratch_floats = (size_t)4 * SIM_MAXCON * (2 * nv + 4) * n_envs;
     HIPCHECK(hipMalloc(&B->d_scratch, B->scratch_floats * sizeof(float)));
-    HIPCHECK(hipMalloc(&B->d_gpose, (size_t)m->desc.ngeom * 12 * n_envs * sizeof(float)));
+    HIPCHECK(hipMalloc(&B->d_gpose, (size_t)m->desc.ngeom * GREC * n_envs * sizeof(float)));
     HIPCHECK(hipMalloc(&B->d_cbuf, (size_t)(m->dm.nslot > 0 ? m->dm.nslot : 1) * 7 * n_envs * sizeof(float)));
     HIPCHECK(hipMalloc(&B->d_ccount, (size_t)(m->desc.npair > 0 ? m->desc.npair : 1) * n_envs * sizeof(int)));
     const size_t nw = (size_t)std::max(pmask_words(m->dm), 1);
