@@ -254,7 +254,13 @@ int sim_model_load(const char* path, sim_model** out);
 
 /* replaces MjData(model) for n_envs envs on `device` (HIP ordinal).  The model's
    read-only device data (constants, hull records, support LUT) is uploaded by the
-   first batch on a device and shared by the model's later batches there. */
+   first batch on a device and shared by the model's later batches there.
+   device = -1: the CPU backend -- the same per-env physics compiled
+   for the host, envs split over SOARM_CPU_THREADS (else OMP_NUM_THREADS, else all
+   cores) threads.  Every call then takes HOST pointers in the same layouts, ignores
+   `stream` and returns when done; sim_profile_* / sim_collide_profile need a GPU batch.
+   The constraint solve is a dense scalar restatement of mj_solPGS / mj_solNewton in
+   MuJoCo's row order (the kernels' lane-cooperative sweeps do not exist on the host). */
 int sim_batch_create(const sim_model* m, int n_envs, int device, sim_batch** out);
 void sim_batch_free(sim_batch* b);
 int sim_batch_set_params(sim_batch* b, const sim_params* p);

@@ -14,8 +14,11 @@ import time
 from .abi import LIB_PATH, PKG_DIR
 
 SRC_DIR = os.path.join(PKG_DIR, "csrc")
-SOURCES = ["soarm_sim.hip", "koopman_mpc.hip"]
-HEADERS = ["dmodel.h", "soarm_kernels.h", "soarm_step.h", "soarm_collide.h", "soarm_pgs.h", "soarm_newton.h"]
+SOURCES = ["soarm_sim.hip", "koopman_mpc.hip", "soarm_cpu.hip"]
+# translation units compiled for the host only (the CPU backend: no kernels)
+HOST_ONLY = {"soarm_cpu.hip"}
+HEADERS = ["dmodel.h", "soarm_kernels.h", "soarm_step.h", "soarm_collide.h", "soarm_pgs.h", "soarm_newton.h",
+           "soarm_env.h", "sim_internal.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # -fno-slp-vectorize: the per-lane algebra gains nothing from v_pk_* packing; the
 # packing's operand shuffles (v_mov) and the extra register pressure (AGPR
@@ -54,10 +57,29 @@ def build(force=False, verbose=False):
         return LIB_PATH
     want = source_hash()
     tmp = f"{LIB_PATH}.{os.getpid()}.tmp"
-    cmd = [HIPCC] + FLAGS + ["-o", tmp] + [os.path.join(SRC_DIR, s) for s in SOURCES]
-    if verbose:
-        print(" ".join(cmd))
-    subprocess.check_call(cmd, cwd=SRC_DIR)
+    # one object per translation unit, compiled concurrently, then one link
+    cflags = [f for f in FLAGS if f != "-shared"]
+    objs, procs = [], []
+    for src in SOURCES:
+        obj = f"{tmp}.{os.path.splitext(src)[0]}.o"
+        extra = ["-x", "hip", "--offload-host-only"] if src in HOST_ONLY else []
+        cmd = [HIPCC] + cflags + extra + ["-c", os.path.join(SRC_DIR, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd))
+        objs.append(obj)
+        procs.append(subprocess.Popen(cmd, cwd=SRC_DIR))
+    try:
+        rcs = [p.wait() for p in procs]
+        if any(rcs):
+            raise subprocess.CalledProcessError(max(rcs, key=abs), "hipcc")
+        cmd = [HIPCC] + FLAGS + ["-o", tmp] + objs + ["-lpthread"]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.check_call(cmd, cwd=SRC_DIR)
+    finally:
+        for o in objs:
+            if os.path.exists(o):
+                os.remove(o)
     os.replace(tmp, LIB_PATH)  # atomic: concurrent loaders never see a partial file
     with open(STAMP + f".{os.getpid()}.tmp", "w") as f:
         f.write(want + "\n")

@@ -39,9 +39,9 @@ constexpr float SEP_MARGIN = 1e-6f;
 struct ConLds {
   float (*a)[64];  // [SIM_MAXCON * 8][64]: dist, pos(3), n(3), pair
   int lane;
-  DEVI float& dist(int c) const { return a[c * 8][lane]; }
-  DEVI float& pos(int c, int k) const { return a[c * 8 + 1 + k][lane]; }
-  DEVI float& n(int c, int k) const { return a[c * 8 + 4 + k][lane]; }
+  HDI float& dist(int c) const { return a[c * 8][lane]; }
+  HDI float& pos(int c, int k) const { return a[c * 8 + 1 + k][lane]; }
+  HDI float& n(int c, int k) const { return a[c * 8 + 4 + k][lane]; }
   DEVI int pair(int c) const { return __float_as_int(a[c * 8 + 7][lane]); }
   DEVI void set_pair(int c, int p) const { a[c * 8 + 7][lane] = __int_as_float(p); }
 };
@@ -56,13 +56,13 @@ struct GeomPose {
 // of an env) costs 12 loads instead of the 24 of two full poses; the values are the ones the
 // midphase computed from the poses before (same expressions), so its decisions are unchanged
 constexpr int GREC = 18;
-DEVI void load_pose(const float* __restrict__ gpose, int n, int e, int g, GeomPose& o) {
+HDI void load_pose(const float* __restrict__ gpose, int n, int e, int g, GeomPose& o) {
 #pragma unroll
   for (int k = 0; k < 3; k++) o.p[k] = soa(gpose, g * GREC + k, n, e);
 #pragma unroll
   for (int k = 0; k < 9; k++) o.R[k] = soa(gpose, g * GREC + 3 + k, n, e);
 }
-DEVI void load_bound(const float* __restrict__ gpose, int n, int e, int g, float c[3], float h[3]) {
+HDI void load_bound(const float* __restrict__ gpose, int n, int e, int g, float c[3], float h[3]) {
 #pragma unroll
   for (int k = 0; k < 3; k++) c[k] = soa(gpose, g * GREC + 12 + k, n, e), h[k] = soa(gpose, g * GREC + 15 + k, n, e);
 }
@@ -86,13 +86,18 @@ struct PairOut {
 // dependent round trip.  Same comparisons, order and result as a CSR walk.
 // (the hull tables are read through global-address-space pointers: the DModel holds them as
 // plain pointers, which would otherwise compile to flat loads)
+#if SOARM_DEVICE_PASS
 template <class T>
 using gptr = const __attribute__((address_space(1))) T*;
-DEVI uint4 ldg(gptr<uint4> p, int i) {  // (dword loads, merged into one 16-B load)
+#else
+template <class T>
+using gptr = const T*;
+#endif
+HDI uint4 ldg(gptr<uint4> p, int i) {  // (dword loads, merged into one 16-B load)
   const gptr<uint32_t> q = (gptr<uint32_t>)(p + i);
   return make_uint4(q[0], q[1], q[2], q[3]);
 }
-DEVI float3 hull_support(const DModel& m, int g, const float l[3]) {
+HDI float3 hull_support(const DModel& m, int g, const float l[3]) {
   const gptr<uint4> rec = (gptr<uint4>)m.hull_rec + 2 * m.geom_hulladr[g];
   const gptr<uint4> lr = (gptr<uint4>)m.hull_lutrec + HULL_LUTREC * (m.geom_lutadr[g] + lut_cell(l[0], l[1], l[2]));
   uint4 r0 = ldg(lr, 0), r1 = ldg(lr, 1), nb[8];
@@ -100,7 +105,7 @@ DEVI float3 hull_support(const DModel& m, int g, const float l[3]) {
   for (int k = 0; k < 8; k++) nb[k] = ldg(lr, 2 + k);
   const int nvert = m.geom_hullnum[g];
   auto dotr = [&](const uint4& r) {
-    return l[0] * __uint_as_float(r.x) + l[1] * __uint_as_float(r.y) + l[2] * __uint_as_float(r.z);
+    return l[0] * fbits(r.x) + l[1] * fbits(r.y) + l[2] * fbits(r.z);
   };
   float cd = dotr(r0);
   if ((r0.w & 255u) <= 8) {  // first step from the cell's copy of the start's neighbours
@@ -111,7 +116,7 @@ DEVI float3 hull_support(const DModel& m, int g, const float l[3]) {
       const float s = dotr(nb[k]);
       if (s > nd) nd = s, best = k;
     }
-    if (best < 0) return make_float3(__uint_as_float(r0.x), __uint_as_float(r0.y), __uint_as_float(r0.z));
+    if (best < 0) return make_float3(fbits(r0.x), fbits(r0.y), fbits(r0.z));
     uint32_t u = 0;
 #pragma unroll
     for (int k = 0; k < 8; k++)
@@ -156,13 +161,13 @@ DEVI float3 hull_support(const DModel& m, int g, const float l[3]) {
     if (best < 0) break;
     r0 = b0, r1 = b1, cd = nd;
   }
-  return make_float3(__uint_as_float(r0.x), __uint_as_float(r0.y), __uint_as_float(r0.z));
+  return make_float3(fbits(r0.x), fbits(r0.y), fbits(r0.z));
 }
 
 // world support point of geom g (type uniform across the wave)
 // upper bound on a mesh hull's support value along a (not necessarily unit) local direction l
 // from the support-bound table (dmodel.h HULL_SB_K): 3 table loads, no hull data
-DEVI float support_ub(const DModel& m, int g, const float l[3]) {
+HDI float support_ub(const DModel& m, int g, const float l[3]) {
   const float a0 = fabsf(l[0]), a1 = fabsf(l[1]), a2 = fabsf(l[2]);
   int face;
   float u, v, mx;
@@ -184,7 +189,7 @@ DEVI float support_ub(const DModel& m, int g, const float l[3]) {
   return mx * q;
 }
 
-DEVI void support(const DModel& m, int g, const GeomPose& P, const float d[3], float out[3]) {
+HDI void support(const DModel& m, int g, const GeomPose& P, const float d[3], float out[3]) {
   float l[3];
   mtv(l, P.R, d);
   float p[3] = {0, 0, 0};
@@ -201,7 +206,7 @@ DEVI void support(const DModel& m, int g, const GeomPose& P, const float d[3], f
   out[0] = P.p[0] + w[0], out[1] = P.p[1] + w[1], out[2] = P.p[2] + w[2];
 }
 
-DEVI void geom_center(const DModel& m, int g, const GeomPose& P, float c[3]) {
+HDI void geom_center(const DModel& m, int g, const GeomPose& P, float c[3]) {
   const float lc[3] = {m.geom_center[g][0], m.geom_center[g][1], m.geom_center[g][2]};
   float w[3];
   mv(w, P.R, lc);
@@ -216,32 +221,32 @@ struct MPair {
   const DModel& m;
   int g1, g2;
   const GeomPose &P1, &P2;
-  DEVI void sup(const float d[3], MSup& s) const {
+  HDI void sup(const float d[3], MSup& s) const {
     const float nd[3] = {-d[0], -d[1], -d[2]};
     support(m, g1, P1, d, s.v1);
     support(m, g2, P2, nd, s.v2);
     s.v[0] = s.v1[0] - s.v2[0], s.v[1] = s.v1[1] - s.v2[1], s.v[2] = s.v1[2] - s.v2[2];
   }
 };
-DEVI bool fz(float x) { return fabsf(x) < FEPS; }
-DEVI void nrm(float a[3]) {
+HDI bool fz(float x) { return fabsf(x) < FEPS; }
+HDI void nrm(float a[3]) {
   const float n2 = dot3(a, a);
   if (n2 > 0.f) {
-    const float s = rsqrtf(n2);
+    const float s = frsqrt(n2);
     a[0] *= s, a[1] *= s, a[2] *= s;
   }
 }
-DEVI void sub(float r[3], const float a[3], const float b[3]) {
+HDI void sub(float r[3], const float a[3], const float b[3]) {
   r[0] = a[0] - b[0], r[1] = a[1] - b[1], r[2] = a[2] - b[2];
 }
-DEVI void portal_dir(const MSup p[4], float d[3]) {
+HDI void portal_dir(const MSup p[4], float d[3]) {
   float a[3], b[3];
   sub(a, p[2].v, p[1].v);
   sub(b, p[3].v, p[1].v);
   cross(d, a, b);
   nrm(d);
 }
-DEVI bool reach_tol(const MSup p[4], const MSup& v4, const float d[3]) {
+HDI bool reach_tol(const MSup p[4], const MSup& v4, const float d[3]) {
   const float d4 = dot3(v4.v, d);
   const float mn = fminf(fminf(d4 - dot3(p[1].v, d), d4 - dot3(p[2].v, d)), d4 - dot3(p[3].v, d));
   return mn <= MPR_TOLF;
@@ -249,7 +254,7 @@ DEVI bool reach_tol(const MSup p[4], const MSup& v4, const float d[3]) {
 // dst = c ? src : dst, element by element (v_cndmask): a branchy `p[i] = v4` lets the
 // compiler sink the stores into one store through a computed index, which puts the whole
 // portal in scratch memory
-DEVI void sel(MSup& dst, bool c, const MSup& src) {
+HDI void sel(MSup& dst, bool c, const MSup& src) {
 #pragma unroll
   for (int k = 0; k < 3; k++) {
     dst.v[k] = c ? src.v[k] : dst.v[k];
@@ -257,7 +262,7 @@ DEVI void sel(MSup& dst, bool c, const MSup& src) {
     dst.v2[k] = c ? src.v2[k] : dst.v2[k];
   }
 }
-DEVI void expand(MSup p[4], const MSup& v4) {
+HDI void expand(MSup p[4], const MSup& v4) {
   float x[3];
   cross(x, v4.v, p[0].v);
   const bool c1 = dot3(p[1].v, x) > 0.f, c2 = dot3(p[2].v, x) > 0.f, c3 = dot3(p[3].v, x) > 0.f;
@@ -269,8 +274,8 @@ DEVI void expand(MSup p[4], const MSup& v4) {
 // -1 separated, 0 portal, 1 origin on v1, 2 origin on segment v0-v1.  On a separated exit
 // found by a support query, sep = that query's direction (the Minkowski difference lies
 // on its negative side: a separating axis); otherwise sep is left as it was.
-DEVI void setsep(float sep[3], const float d[3]) { sep[0] = d[0], sep[1] = d[1], sep[2] = d[2]; }
-DEVI int discover(const MPair& P, MSup p[4], float sep[3]) {
+HDI void setsep(float sep[3], const float d[3]) { sep[0] = d[0], sep[1] = d[1], sep[2] = d[2]; }
+HDI int discover(const MPair& P, MSup p[4], float sep[3]) {
   float c1[3], c2[3], d[3], va[3], vb[3];
   geom_center(P.m, P.g1, P.P1, c1);
   geom_center(P.m, P.g2, P.P2, c2);
@@ -330,7 +335,7 @@ DEVI int discover(const MPair& P, MSup p[4], float sep[3]) {
   }
   return -1;
 }
-DEVI void closest_tri(const float a[3], const float b[3], const float c[3], float o[3]) {
+HDI void closest_tri(const float a[3], const float b[3], const float c[3], float o[3]) {
   float ab[3], ac[3];
   sub(ab, b, a);
   sub(ac, c, a);
@@ -378,7 +383,7 @@ DEVI void closest_tri(const float a[3], const float b[3], const float c[3], floa
 #pragma unroll
   for (int k = 0; k < 3; k++) o[k] = a[k] + ab[k] * v + ac[k] * w;
 }
-DEVI void portal_pos(const MSup p[4], float pos[3]) {
+HDI void portal_pos(const MSup p[4], float pos[3]) {
   float d[3], x[3], b[4];
   portal_dir(p, d);
   cross(x, p[1].v, p[2].v);
@@ -411,7 +416,7 @@ DEVI void portal_pos(const MSup p[4], float pos[3]) {
 }
 // returns 1 with depth/dir(geom1->geom2)/pos when penetrating; sep = a separating axis
 // when it proved the pair apart by a support query (else unchanged)
-DEVI int mpr(const MPair& P, float& depth, float dir[3], float pos[3], float sep[3]) {
+HDI int mpr(const MPair& P, float& depth, float dir[3], float pos[3], float sep[3]) {
   MSup p[4];
   const int res = discover(P, p, sep);
   if (res < 0 || res == 1) return 0;
@@ -472,9 +477,9 @@ DEVI int mpr(const MPair& P, float& depth, float dir[3], float pos[3], float sep
 // arrays: EPA_KV vertices (v and the geom1 support point; geom2's is v1 - v), EPA_KF faces.
 constexpr int CCD_ITERS = 50;
 constexpr int EPA_KV = 32, EPA_KF = 64, EPA_KE = 48;
-DEVI void copy3(float d[3], const float s[3]) { d[0] = s[0], d[1] = s[1], d[2] = s[2]; }
+HDI void copy3(float d[3], const float s[3]) { d[0] = s[0], d[1] = s[1], d[2] = s[2]; }
 // closest point of simplex p[0..n) (n <= 3) to the origin; the carrying sub-simplex moves to the front
-DEVI int gjk_reduce(MSup p[4], int n, float x[3]) {
+HDI int gjk_reduce(MSup p[4], int n, float x[3]) {
   if (n == 1) {
     copy3(x, p[0].v);
     return 1;
@@ -550,10 +555,13 @@ DEVI int gjk_reduce(MSup p[4], int n, float x[3]) {
   return 3;
 }
 // tetrahedron faces: face k = the vertices other than k
-__device__ constexpr int TETF[4][3] = {{1, 2, 3}, {0, 3, 2}, {0, 1, 3}, {0, 2, 1}};
+#if SOARM_DEVICE_PASS
+__device__
+#endif
+constexpr int TETF[4][3] = {{1, 2, 3}, {0, 3, 2}, {0, 1, 3}, {0, 2, 1}};
 // 1: origin inside tetrahedron p; 0: reduced to the face the origin lies beyond (n, x set);
 // -1: flat tetrahedron
-DEVI int tet_contains(MSup p[4], float x[3], int& n) {
+HDI int tet_contains(MSup p[4], float x[3], int& n) {
   float best = 0.f;
   int bk = -1;
 #pragma unroll
@@ -584,7 +592,7 @@ DEVI int tet_contains(MSup p[4], float x[3], int& n) {
 }
 // GJK: true with p a tetrahedron enclosing the origin; false apart (sep = a separating axis when
 // a support plane proved it) or touching
-DEVI bool gjk_enclose(const MPair& P, MSup p[4], float sep[3]) {
+HDI bool gjk_enclose(const MPair& P, MSup p[4], float sep[3]) {
   float c1[3], c2[3], x[3];
   geom_center(P.m, P.g1, P.P1, c1);
   geom_center(P.m, P.g2, P.P2, c2);
@@ -621,7 +629,7 @@ struct EpaFace {
   uint32_t abc;  // vertex ids, 8 bits each
   float n[3], d;
 };
-DEVI void epa_face(EpaFace& f, const float (*V)[6], int a, int b, int c) {
+HDI void epa_face(EpaFace& f, const float (*V)[6], int a, int b, int c) {
   float ab[3], ac[3];
   sub(ab, V[b], V[a]);
   sub(ac, V[c], V[a]);
@@ -631,7 +639,7 @@ DEVI void epa_face(EpaFace& f, const float (*V)[6], int a, int b, int c) {
   f.d = dot3(f.n, V[a]);
 }
 // EPA from the enclosing tetrahedron p: 1 with depth / dir / pos
-DEVI int epa(const MPair& P, const MSup p[4], float& depth, float dir[3], float pos[3]) {
+HDI int epa(const MPair& P, const MSup p[4], float& depth, float dir[3], float pos[3]) {
   float V[EPA_KV][6];  // v (3), geom1 support point (3)
   EpaFace F[EPA_KF];
   uint8_t E[EPA_KE][2];
@@ -721,7 +729,7 @@ DEVI int epa(const MPair& P, const MSup p[4], float& depth, float dir[3], float 
   depth = f.d;
   return f.d > 0.f;
 }
-DEVI int ccd_native(const MPair& P, float& depth, float dir[3], float pos[3], float sep[3]) {
+HDI int ccd_native(const MPair& P, float& depth, float dir[3], float pos[3], float sep[3]) {
   MSup p[4];
   if (!gjk_enclose(P, p, sep)) return 0;
   return epa(P, p, depth, dir, pos);
@@ -729,7 +737,7 @@ DEVI int ccd_native(const MPair& P, float& depth, float dir[3], float pos[3], fl
 
 // ------------------------------------------------------------- primitives
 // append one contact (dropped past the pair's slot count)
-DEVI void emit(PairOut& o, float dist, const float pos[3], const float n[3]) {
+HDI void emit(PairOut& o, float dist, const float pos[3], const float n[3]) {
   if (o.n >= o.cap) return;
   const int r = (o.s0 + o.n) * 7;
   soa(o.cbuf, r, o.nenv, o.e) = dist;
@@ -738,7 +746,7 @@ DEVI void emit(PairOut& o, float dist, const float pos[3], const float n[3]) {
   o.n++;
 }
 
-DEVI void plane_box(const DModel& m, int gp, int gb, const GeomPose& Pp, const GeomPose& Pb, PairOut& o) {
+HDI void plane_box(const DModel& m, int gp, int gb, const GeomPose& Pp, const GeomPose& Pb, PairOut& o) {
   const float n[3] = {Pp.R[2], Pp.R[5], Pp.R[8]};
   int cnt = 0;
   for (int i = 0; i < 8 && cnt < 4; i++) {
@@ -757,7 +765,7 @@ DEVI void plane_box(const DModel& m, int gp, int gb, const GeomPose& Pp, const G
   }
 }
 
-DEVI void plane_convex(const DModel& m, int gp, int g, const GeomPose& Pp, const GeomPose& Pg, PairOut& o) {
+HDI void plane_convex(const DModel& m, int gp, int g, const GeomPose& Pp, const GeomPose& Pg, PairOut& o) {
   const float n[3] = {Pp.R[2], Pp.R[5], Pp.R[8]};
   const float nn[3] = {-n[0], -n[1], -n[2]};
   float p[3], rel[3];
@@ -776,14 +784,14 @@ DEVI void plane_convex(const DModel& m, int gp, int g, const GeomPose& Pp, const
 // live in scratch memory (k_collide had 656 B of scratch per lane).
 // (value selects, v_cndmask: a conditional store `if (j == k) out[j] = x` is merged by the
 // optimizer into one store through a computed index, which sends the array to scratch)
-DEVI void put8(float out[8][3], int k, const float x[3]) {
+HDI void put8(float out[8][3], int k, const float x[3]) {
 #pragma unroll
   for (int j = 0; j < 8; j++)
 #pragma unroll
     for (int c = 0; c < 3; c++) out[j][c] = j == k ? x[c] : out[j][c];
 }
 template <int R>
-DEVI void row3(const float M[R][3], int i, float out[3]) {
+HDI void row3(const float M[R][3], int i, float out[3]) {
 #pragma unroll
   for (int c = 0; c < 3; c++) out[c] = M[0][c];
 #pragma unroll
@@ -791,10 +799,10 @@ DEVI void row3(const float M[R][3], int i, float out[3]) {
 #pragma unroll
     for (int c = 0; c < 3; c++) out[c] = j == i ? M[j][c] : out[c];
 }
-DEVI float pick3(const float* h, int i) { return i == 0 ? h[0] : (i == 1 ? h[1] : h[2]); }
+HDI float pick3(const float* h, int i) { return i == 0 ? h[0] : (i == 1 ? h[1] : h[2]); }
 
 // one Sutherland-Hodgman step: keep the part of polygon in[0..n) with (x - o).a <= lim
-DEVI int clip_poly8(const float in[8][3], int n, float out[8][3], const float o[3], const float a[3], float lim) {
+HDI int clip_poly8(const float in[8][3], int n, float out[8][3], const float o[3], const float a[3], float lim) {
   float sd[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) {
@@ -826,7 +834,7 @@ DEVI int clip_poly8(const float in[8][3], int n, float out[8][3], const float o[
   return k < 8 ? k : 8;
 }
 
-DEVI void box_box(const DModel& m, int g1, int g2, const GeomPose& P1, const GeomPose& P2, PairOut& o) {
+HDI void box_box(const DModel& m, int g1, int g2, const GeomPose& P1, const GeomPose& P2, PairOut& o) {
   const float *h1 = m.geom_size[g1], *h2 = m.geom_size[g2];
   float A[3][3], B[3][3], t[3];
 #pragma unroll
@@ -1019,7 +1027,7 @@ DEVI void box_box(const DModel& m, int g1, int g2, const GeomPose& P1, const Geo
 // world records (pose + midphase bound, GREC floats) of every collidable geom of this env
 template <int NA, int NF>
 // geoms g0, g0 + gstep, ... of each body (quad mode: lane k of the quad writes every 4th)
-DEVI void write_geom_poses(const Sim<NA, NF>& S, float* __restrict__ gpose, int n, int e, int g0 = 0,
+HDI void write_geom_poses(const Sim<NA, NF>& S, float* __restrict__ gpose, int n, int e, int g0 = 0,
                            int gstep = 1) {
   // bodies in compile-time order, each body's geoms from a wave-uniform list: the body frame
   // is read with constant indices (a per-lane body id would select it with 12 v_cndmask per
@@ -1062,7 +1070,7 @@ DEVI void write_geom_poses(const Sim<NA, NF>& S, float* __restrict__ gpose, int 
 // midphase of candidate pair p from the geoms' records: bounding spheres and world-aligned boxes
 // (before the poses are loaded), and for a plane the other geom's bounding sphere above it.
 // false: no contact is possible.  P1 / P2 are loaded here when the pair survives.
-DEVI bool midphase(const DModel& m, int p, const float* __restrict__ gpose, int n, int e, GeomPose& P1,
+HDI bool midphase(const DModel& m, int p, const float* __restrict__ gpose, int n, int e, GeomPose& P1,
                    GeomPose& P2) {
   const int g1 = m.pair_geom1[p], g2 = m.pair_geom2[p];
   float c2[3], h2[3];
@@ -1098,24 +1106,24 @@ DEVI bool midphase(const DModel& m, int p, const float* __restrict__ gpose, int 
 struct SepCache {
   float* a;  // null: no cache (the fused-collide build)
   int n, e;
-  DEVI void load(int p, float d[3]) const {
+  HDI void load(int p, float d[3]) const {
 #pragma unroll
     for (int k = 0; k < 3; k++) d[k] = a ? soa(a, 3 * p + k, n, e) : 0.f;
   }
-  DEVI void store(int p, const float d[3]) const {
+  HDI void store(int p, const float d[3]) const {
     if (!a) return;
 #pragma unroll
     for (int k = 0; k < 3; k++) soa(a, 3 * p + k, n, e) = d[k];
   }
 };
 // upper bound on geom g's support value along the local direction l (box: exact)
-DEVI float support_ub_any(const DModel& m, int g, const float l[3]) {
+HDI float support_ub_any(const DModel& m, int g, const float l[3]) {
   if (m.geom_type[g] == SIM_GEOM_BOX)
     return fabsf(l[0]) * m.geom_size[g][0] + fabsf(l[1]) * m.geom_size[g][1] + fabsf(l[2]) * m.geom_size[g][2];
   return support_ub(m, g, l);
 }
 // upper bound on max over (geom1 - geom2) of x.d: below zero proves the pair apart along d
-DEVI float minkowski_ub(const DModel& m, int g1, int g2, const GeomPose& P1, const GeomPose& P2, const float d[3]) {
+HDI float minkowski_ub(const DModel& m, int g1, int g2, const GeomPose& P1, const GeomPose& P2, const float d[3]) {
   float l1[3], l2[3];
   mtv(l1, P1.R, d);
   mtv(l2, P2.R, d);
@@ -1124,7 +1132,7 @@ DEVI float minkowski_ub(const DModel& m, int g1, int g2, const GeomPose& P1, con
          support_ub_any(m, g1, l1) + support_ub_any(m, g2, l2);
 }
 // the cached axis of pair p still separates it
-DEVI bool cached_apart(const DModel& m, int p, int g1, int g2, const GeomPose& P1, const GeomPose& P2,
+HDI bool cached_apart(const DModel& m, int p, int g1, int g2, const GeomPose& P1, const GeomPose& P2,
                        const SepCache& sc) {
   float d[3];
   sc.load(p, d);
@@ -1133,7 +1141,7 @@ DEVI bool cached_apart(const DModel& m, int p, int g1, int g2, const GeomPose& P
 }
 
 // narrowphase of a pair that passed the midphase (geom types are uniform over a pair)
-DEVI void narrowphase(const DModel& m, int p, const GeomPose& P1, const GeomPose& P2, PairOut& o,
+HDI void narrowphase(const DModel& m, int p, const GeomPose& P1, const GeomPose& P2, PairOut& o,
                       const SepCache& sc) {
   o.n = 0;
   o.xc = 6;
@@ -1196,7 +1204,7 @@ DEVI void narrowphase(const DModel& m, int p, const GeomPose& P1, const GeomPose
     float d[3] = {c2[0] - c1[0], c2[1] - c1[1], c2[2] - c1[2]};
     const float n2 = dot3(d, d);
     if (n2 > 1e-20f) {
-      const float inv = rsqrtf(n2);
+      const float inv = frsqrt(n2);
       d[0] *= inv, d[1] *= inv, d[2] *= inv;
       const float l1[3] = {P1.R[0] * d[0] + P1.R[3] * d[1] + P1.R[6] * d[2],
                            P1.R[1] * d[0] + P1.R[4] * d[1] + P1.R[7] * d[2],
@@ -1225,7 +1233,7 @@ DEVI void narrowphase(const DModel& m, int p, const GeomPose& P1, const GeomPose
 
 namespace soarm {
 // midphase + narrowphase of candidate pair p of env e (geom records in gpose)
-DEVI void collide_pair(const DModel& m, int p, const float* __restrict__ gpose, int n, int e, PairOut& o,
+HDI void collide_pair(const DModel& m, int p, const float* __restrict__ gpose, int n, int e, PairOut& o,
                        const SepCache& sc = SepCache{nullptr, 0, 0}) {
   o.n = 0;
   GeomPose P1, P2;

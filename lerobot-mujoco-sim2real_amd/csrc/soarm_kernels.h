@@ -19,9 +19,20 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cstring>
+
 #include "dmodel.h"
 
 #define DEVI __device__ __forceinline__
+// the per-env physics (this header, soarm_step.h, soarm_collide.h) also builds for the host:
+// the CPU backend (device = -1, soarm_cpu.hip) runs the same code on an env per thread.
+// Device intrinsics go through the f* helpers below (host: their libm equivalents).
+#define HDI __host__ __device__ __forceinline__
+#if defined(__HIP_DEVICE_COMPILE__)
+#define SOARM_DEVICE_PASS 1
+#else
+#define SOARM_DEVICE_PASS 0
+#endif
 
 // element e of row r of a [row][env] array (4-byte T): the row pointer is wave-uniform
 // (SGPRs) and the lane's byte offset e*4 a 32-bit VGPR shared by every row, so the access
@@ -30,62 +41,97 @@
 // an opaque copy of a (wave-uniform) pointer: addresses derived from it are not CSE'd with
 // those of an earlier access, so no per-lane address stays live between the two
 template <class T>
-DEVI T* launder(T* p) {
+HDI T* launder(T* p) {
   // laundered as a global-address-space pointer, so address-space inference still emits
   // global (not flat) accesses through the result: a flat store counts against lgkmcnt as
   // well, and every later LDS / scalar-load wait would then also wait for it to land
+#if SOARM_DEVICE_PASS
   auto g = (__attribute__((address_space(1))) T*)p;
   asm volatile("" : "+s"(g));
   return (T*)g;
+#else
+  return p;
+#endif
 }
 template <class T>
-DEVI T& soa(T* p, int r, int n, int e) {
+HDI T& soa(T* p, int r, int n, int e) {
   static_assert(sizeof(T) == 4, "4-byte elements");
   return *(T*)((const char*)(p + (size_t)r * n) + ((uint32_t)e << 2));
 }
 
 namespace soarm {
 
+HDI float frsqrt(float x) {
+#if SOARM_DEVICE_PASS
+  return rsqrtf(x);
+#else
+  return 1.f / sqrtf(x);
+#endif
+}
+HDI void fsincos(float x, float* s, float* c) {
+#if SOARM_DEVICE_PASS
+  __sincosf(x, s, c);
+#else
+  *s = sinf(x), *c = cosf(x);
+#endif
+}
+HDI float fpow(float x, float y) {
+#if SOARM_DEVICE_PASS
+  return fpow(x, y);
+#else
+  return powf(x, y);
+#endif
+}
+HDI float fbits(uint32_t u) {
+#if SOARM_DEVICE_PASS
+  return __uint_as_float(u);
+#else
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
+#endif
+}
+
 constexpr float MINVALF = 1e-15f;
 constexpr float MAXVALF = 1e10f;
 constexpr float MINIMPF = 0.0001f, MAXIMPF = 0.9999f;
 
 // ------------------------------------------------------------------ algebra
-DEVI void qmul(float r[4], const float a[4], const float b[4]) {
+HDI void qmul(float r[4], const float a[4], const float b[4]) {
   float t0 = a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3];
   float t1 = a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2];
   float t2 = a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1];
   float t3 = a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0];
   r[0] = t0, r[1] = t1, r[2] = t2, r[3] = t3;
 }
-DEVI void qnormalize(float q[4]) {
+HDI void qnormalize(float q[4]) {
   float n2 = q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3];
   if (n2 < 1e-30f) {
     q[0] = 1, q[1] = q[2] = q[3] = 0;
     return;
   }
-  float s = rsqrtf(n2);
+  float s = frsqrt(n2);
   q[0] *= s, q[1] *= s, q[2] *= s, q[3] *= s;
 }
-DEVI void q2m(float R[9], const float q[4]) {
+HDI void q2m(float R[9], const float q[4]) {
   float w = q[0], x = q[1], y = q[2], z = q[3];
   R[0] = 1 - 2 * (y * y + z * z), R[1] = 2 * (x * y - w * z), R[2] = 2 * (x * z + w * y);
   R[3] = 2 * (x * y + w * z), R[4] = 1 - 2 * (x * x + z * z), R[5] = 2 * (y * z - w * x);
   R[6] = 2 * (x * z - w * y), R[7] = 2 * (y * z + w * x), R[8] = 1 - 2 * (x * x + y * y);
 }
-DEVI void mv(float r[3], const float R[9], const float v[3]) {
+HDI void mv(float r[3], const float R[9], const float v[3]) {
   float a = R[0] * v[0] + R[1] * v[1] + R[2] * v[2];
   float b = R[3] * v[0] + R[4] * v[1] + R[5] * v[2];
   float c = R[6] * v[0] + R[7] * v[1] + R[8] * v[2];
   r[0] = a, r[1] = b, r[2] = c;
 }
-DEVI void mtv(float r[3], const float R[9], const float v[3]) {
+HDI void mtv(float r[3], const float R[9], const float v[3]) {
   float a = R[0] * v[0] + R[3] * v[1] + R[6] * v[2];
   float b = R[1] * v[0] + R[4] * v[1] + R[7] * v[2];
   float c = R[2] * v[0] + R[5] * v[1] + R[8] * v[2];
   r[0] = a, r[1] = b, r[2] = c;
 }
-DEVI void mm(float r[9], const float A[9], const float B[9]) {
+HDI void mm(float r[9], const float A[9], const float B[9]) {
   float t[9];
 #pragma unroll
   for (int i = 0; i < 3; i++)
@@ -95,16 +141,16 @@ DEVI void mm(float r[9], const float A[9], const float B[9]) {
 #pragma unroll
   for (int i = 0; i < 9; i++) r[i] = t[i];
 }
-DEVI void cross(float r[3], const float a[3], const float b[3]) {
+HDI void cross(float r[3], const float a[3], const float b[3]) {
   float x = a[1] * b[2] - a[2] * b[1], y = a[2] * b[0] - a[0] * b[2], z = a[0] * b[1] - a[1] * b[0];
   r[0] = x, r[1] = y, r[2] = z;
 }
-DEVI float dot3(const float a[3], const float b[3]) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
-DEVI float dot6(const float a[6], const float b[6]) {
+HDI float dot3(const float a[3], const float b[3]) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+HDI float dot6(const float a[6], const float b[6]) {
   return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3] + a[4] * b[4] + a[5] * b[5];
 }
 // spatial motion cross product  v x m  (MuJoCo mju_crossMotion)
-DEVI void cross_motion(float r[6], const float v[6], const float m[6]) {
+HDI void cross_motion(float r[6], const float v[6], const float m[6]) {
   float t0 = -v[2] * m[1] + v[1] * m[2];
   float t1 = v[2] * m[0] - v[0] * m[2];
   float t2 = -v[1] * m[0] + v[0] * m[1];
@@ -114,7 +160,7 @@ DEVI void cross_motion(float r[6], const float v[6], const float m[6]) {
   r[0] = t0, r[1] = t1, r[2] = t2, r[3] = t3, r[4] = t4, r[5] = t5;
 }
 // spatial force cross product  v x* f  (MuJoCo mju_crossForce)
-DEVI void cross_force(float r[6], const float v[6], const float f[6]) {
+HDI void cross_force(float r[6], const float v[6], const float f[6]) {
   float t0 = -v[2] * f[1] + v[1] * f[2] - v[5] * f[4] + v[4] * f[5];
   float t1 = v[2] * f[0] - v[0] * f[2] + v[5] * f[3] - v[3] * f[5];
   float t2 = -v[1] * f[0] + v[0] * f[1] - v[4] * f[3] + v[3] * f[4];
@@ -124,7 +170,7 @@ DEVI void cross_force(float r[6], const float v[6], const float f[6]) {
   r[0] = t0, r[1] = t1, r[2] = t2, r[3] = t3, r[4] = t4, r[5] = t5;
 }
 // 10-vector inertia [Ixx Iyy Izz Ixy Ixz Iyz, m c, m] times motion
-DEVI void inert_mul(float r[6], const float i[10], const float v[6]) {
+HDI void inert_mul(float r[6], const float i[10], const float v[6]) {
   float a = i[0] * v[0] + i[3] * v[1] + i[4] * v[2] - i[8] * v[4] + i[7] * v[5];
   float b = i[3] * v[0] + i[1] * v[1] + i[5] * v[2] + i[8] * v[3] - i[6] * v[5];
   float c = i[4] * v[0] + i[5] * v[1] + i[2] * v[2] - i[7] * v[3] + i[6] * v[4];
@@ -136,7 +182,7 @@ DEVI void inert_mul(float r[6], const float i[10], const float v[6]) {
 
 // dense LDL' in place on a packed lower triangle (row-major, n(n+1)/2), D inverted
 template <int N>
-DEVI void ldl_factor(float L[N * (N + 1) / 2], float Dinv[N]) {
+HDI void ldl_factor(float L[N * (N + 1) / 2], float Dinv[N]) {
   float D[N];
 #pragma unroll
   for (int i = 0; i < N; i++) {
@@ -155,7 +201,7 @@ DEVI void ldl_factor(float L[N * (N + 1) / 2], float Dinv[N]) {
   }
 }
 template <int N>
-DEVI void ldl_solve(const float L[N * (N + 1) / 2], const float Dinv[N], float x[N], const float b[N]) {
+HDI void ldl_solve(const float L[N * (N + 1) / 2], const float Dinv[N], float x[N], const float b[N]) {
   float y[N];
 #pragma unroll
   for (int i = 0; i < N; i++) {
@@ -176,7 +222,7 @@ DEVI void ldl_solve(const float L[N * (N + 1) / 2], const float Dinv[N], float x
 }
 
 // MuJoCo getimpedance (solimp: dmin, dmax, width, midpoint, power)
-DEVI float impedance(const float* si, float pos, float margin) {
+HDI float impedance(const float* si, float pos, float margin) {
   float dmin = fminf(fmaxf(si[0], MINIMPF), MAXIMPF);
   float dmax = fminf(fmaxf(si[1], MINIMPF), MAXIMPF);
   if (dmin == dmax || si[2] <= MINVALF) return 0.5f * (dmin + dmax);
@@ -187,12 +233,12 @@ DEVI float impedance(const float* si, float pos, float margin) {
   if (p == 1.f)
     y = x;
   else if (x <= mid)
-    y = __powf(x, p) / __powf(mid, p - 1.f);
+    y = fpow(x, p) / fpow(mid, p - 1.f);
   else
-    y = 1.f - __powf(1.f - x, p) / __powf(1.f - mid, p - 1.f);
+    y = 1.f - fpow(1.f - x, p) / fpow(1.f - mid, p - 1.f);
   return dmin + y * (dmax - dmin);
 }
 
-DEVI bool bad(float x) { return !(fabsf(x) <= MAXVALF); }
+HDI bool bad(float x) { return !(fabsf(x) <= MAXVALF); }
 
 }  // namespace soarm

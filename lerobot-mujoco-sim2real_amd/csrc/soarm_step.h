@@ -34,15 +34,17 @@ struct Sim {
   float cdofdot[NV][6];
   float fsmooth[NV], qacc_s[NV], qacc[NV], fcon[NV];
 
-  DEVI Sim(const DModel* m_, float ms, float fr, float ds) : mp(m_), mscale(ms), fric(fr), dscale(ds) {}
-  DEVI void relaunder() {  // (through the constant address space: the model stays scalar-loaded)
+  HDI Sim(const DModel* m_, float ms, float fr, float ds) : mp(m_), mscale(ms), fric(fr), dscale(ds) {}
+  HDI void relaunder() {  // (through the constant address space: the model stays scalar-loaded)
+#if SOARM_DEVICE_PASS
     auto c = (__attribute__((address_space(4))) const DModel*)mp;
     asm volatile("" : "+s"(c));
     mp = (const DModel*)c;
+#endif
   }
 
   // ---------------------------------------------------------------- mj_kinematics
-  DEVI void kinematics() {
+  HDI void kinematics() {
     const DModel& m = *mp;
     xpos[0][0] = xpos[0][1] = xpos[0][2] = 0.f;
     xquat[0][0] = 1.f, xquat[0][1] = xquat[0][2] = xquat[0][3] = 0.f;
@@ -70,7 +72,7 @@ struct Sim {
         anchor[j][0] = pos[0] + t[0], anchor[j][1] = pos[1] + t[1], anchor[j][2] = pos[2] + t[2];
         mv(axis[j], R, ja);
         float s, c;
-        __sincosf(0.5f * (qpos[j] - m.qpos0[j]), &s, &c);
+        fsincos(0.5f * (qpos[j] - m.qpos0[j]), &s, &c);
         const float ql[4] = {c, ja[0] * s, ja[1] * s, ja[2] * s};
         qmul(q, q, ql);
         q2m(R, q);
@@ -108,7 +110,7 @@ struct Sim {
   }
 
   // ---------------------------------------------------- mj_comPos + mj_crb/makeM
-  DEVI void com_crb() {
+  HDI void com_crb() {
     const DModel& m = *mp;
 #pragma unroll
     for (int b = 1; b < NB; b++) {
@@ -195,7 +197,7 @@ struct Sim {
     }
   }
 
-  DEVI void factor() {
+  HDI void factor() {
     const DModel& m = *mp;
 #pragma unroll
     for (int k = 0; k < NLA; k++) LA[k] = MA[k];
@@ -209,7 +211,7 @@ struct Sim {
   }
 
   // x = M^-1 b (block diagonal)
-  DEVI void solve_m(float x[NV], const float b[NV]) const {
+  HDI void solve_m(float x[NV], const float b[NV]) const {
     const DModel& m = *mp;
     ldl_solve<NA>(LA, DAi, x, b);
 #pragma unroll
@@ -219,7 +221,7 @@ struct Sim {
   // ------------------------------- mj_comVel + mj_rne(flg_acc=0) + passive + actuation
   // RNE_ONLY: fsmooth = -qfrc_bias (gravity + Coriolis/centrifugal), no passive/actuation
   template <bool RNE_ONLY = false>
-  DEVI void smooth_forces() {
+  HDI void smooth_forces() {
     const DModel& m = *mp;
     // arm chain
     float cv[6] = {0, 0, 0, 0, 0, 0};
@@ -295,13 +297,13 @@ struct Sim {
   }
 
   // qfrc_smooth += qfrc_applied ([nv][N] SoA, caller-owned)
-  DEVI void add_applied(const float* applied, int n, int e) {
+  HDI void add_applied(const float* applied, int n, int e) {
 #pragma unroll
     for (int i = 0; i < NV; i++) fsmooth[i] += soa(applied, i, n, e);
   }
 
   // ---------------------------------------------------------- Euler integration
-  DEVI void integrate() {
+  HDI void integrate() {
     const DModel& m = *mp;
     const float h = m.timestep;
     float qa[NV];
@@ -348,7 +350,7 @@ struct Sim {
       if (n2 > 1e-30f) {
         const float n = sqrtf(n2), inv = 1.f / n;
         float s, c;
-        __sincosf(0.5f * n * h, &s, &c);
+        fsincos(0.5f * n * h, &s, &c);
         const float qr[4] = {c, w[0] * inv * s, w[1] * inv * s, w[2] * inv * s};
         qmul(q, q, qr);
       }
@@ -360,7 +362,7 @@ struct Sim {
   }
 
   // mj_resetData for this env (MuJoCo's auto-reset on a bad state)
-  DEVI void soft_reset(int bit) {
+  HDI void soft_reset(int bit) {
     const DModel& m = *mp;
     status |= bit;
 #pragma unroll
@@ -370,7 +372,7 @@ struct Sim {
 #pragma unroll
     for (int i = 0; i < NA; i++) ctrl[i] = 0.f;
   }
-  DEVI void check_state() {
+  HDI void check_state() {
     const DModel& m = *mp;
     bool bq = false, bv = false;
 #pragma unroll
@@ -380,7 +382,7 @@ struct Sim {
     for (int i = 0; i < NV; i++) bv |= bad(qvel[i]);
     if (bv) soft_reset(SIM_ST_BADQVEL);
   }
-  DEVI bool acc_bad() const {
+  HDI bool acc_bad() const {
     const DModel& m = *mp;
     bool b = false;
 #pragma unroll

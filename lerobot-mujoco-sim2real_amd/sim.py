@@ -7,6 +7,10 @@ object the reference-shaped APIs (``SOARM101Env``, ``SOARM101VecEnv``,
 ``SOARM101DataGenerator``, ``CartesianTrajectoryGenerator``) drive.  Every call
 is asynchronous on torch's current stream; nothing here falls back to a CPU
 path — if the HIP library or the GPU is missing, construction raises.
+
+``device=-1`` selects the library's CPU backend explicitly (``sim_batch_create(...,
+-1, ...)``): the same per-env physics compiled for the host, with the
+state as CPU torch tensors and synchronous calls.  It is never chosen implicitly.
 """
 import ctypes as C
 import os
@@ -100,21 +104,24 @@ class SimModel:
 
 
 class BatchSim:
-    """`n_envs` SO-ARM101 environments stepped in lockstep on one GPU."""
+    """`n_envs` SO-ARM101 environments stepped in lockstep on one GPU (device = HIP ordinal), or
+    on the host threads (device = -1: the CPU backend)."""
 
     def __init__(self, model=None, n_envs=1, device=0, model_handle=None, **compile_kw):
         """model: a CompiledModel (sizes, names); model_handle: a SimModel to run instead of the
         model's own (e.g. SimModel.from_file of the same model's saved file)."""
         import torch
 
-        if not torch.cuda.is_available():
-            raise RuntimeError("BatchSim needs a ROCm GPU (torch.cuda.is_available() is False)")
+        self.cpu = device == -1
+        if not self.cpu and not torch.cuda.is_available():
+            raise RuntimeError("BatchSim needs a ROCm GPU (torch.cuda.is_available() is False); "
+                               "device=-1 selects the CPU backend explicitly")
         self.torch = torch
         self.cm = model if model is not None else compile_mjcf(SCENE_XML, **compile_kw)
         self.lib = abi.load_lib()
         d = self.cm.desc
         self.n = int(n_envs)
-        self.device = torch.device("cuda", device)
+        self.device = torch.device("cpu") if self.cpu else torch.device("cuda", device)
         self.nq, self.nv, self.nu = d.nq, d.nv, d.nu
         self.nact, self.obs_dim = d.nact, 3 + d.obs_nq
         self.frame_skip = max(1, int(round(0.02 / d.timestep)))
@@ -151,6 +158,8 @@ class BatchSim:
 
     # ------------------------------------------------------------------ utils
     def _stream(self):
+        if self.cpu:
+            return None  # (the CPU backend's calls are synchronous)
         return C.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
 
     def _dev(self, x, shape=None):

@@ -13,6 +13,7 @@ import pytest
 
 from conftest import cube_qpos
 from oracle import Oracle
+from test_cpu_backend import contact_point_split
 
 pytestmark = pytest.mark.gpu
 
@@ -186,7 +187,7 @@ def test_contacts_match_oracle(gpu_lib, arm_model, cube_model, ccd):
         out, nc = to_np(out), to_np(nc).astype(int)
         pair_ids = out.astype(np.float32).view(np.int32)[..., 7]
         d = cm.desc
-        checked = total = deep = deep_bad = shallow = nrm_bad = geo_bad = 0
+        checked = total = deep = deep_bad = shallow = nrm_bad = geo_bad = slide = 0
         skipped_grazing = skipped_count = 0
         for e in range(n):
             ref = orc.forward(full[e])
@@ -212,7 +213,11 @@ def test_contacts_match_oracle(gpu_lib, arm_model, cube_model, ccd):
                 if abs(rc[k, 0]) < 5e-3:
                     shallow += 1
                     ok_d = abs(out[e, k, 0] - rc[k, 0]) <= 5e-5 + 2e-2 * abs(rc[k, 0])
-                    ok_p = np.abs(out[e, k, 1:4] - rc[k, 1:4]).max() <= 2e-3
+                    if ccd == "native":  # EPA's witness point may slide within a face contact's patch
+                        ok_p, tang = contact_point_split(out[e, k, 1:4] - rc[k, 1:4], rc[k, 4:7])
+                        slide += tang > 2e-3
+                    else:
+                        ok_p = np.abs(out[e, k, 1:4] - rc[k, 1:4]).max() <= 2e-3
                     geo_bad += not (ok_d and ok_p)
                     assert out[e, k, 0] < 0
                     nrm_bad += np.abs(out[e, k, 4:7] - rc[k, 4:7]).max() > 2e-2
@@ -234,6 +239,7 @@ def test_contacts_match_oracle(gpu_lib, arm_model, cube_model, ccd):
         # depth / point: MPR is not a minimum-depth method; its portal refinement can end on
         # a different face in fp32 than in fp64 for a few edge contacts
         assert geo_bad <= max(2, 0.06 * shallow), ("depth/point", geo_bad, shallow)
+        assert slide <= 0.15 * shallow, ("EPA point slides", slide, shallow)
         print(f"contacts: {total} checked, shallow {shallow} (geometry off {geo_bad}, normal off {nrm_bad}), "
               f"deep {deep} (off {deep_bad}); envs skipped: grazing {skipped_grazing}, count {skipped_count}")
 

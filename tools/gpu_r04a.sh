@@ -13,3 +13,5 @@ for c in mpr native; do
 done
 timeout -k 10 600 python bench.py --no-cpu-baseline --config mpc_dbkn > gpurun_out/bench_mpc_dbkn.json 2> gpurun_out/bench_mpc_dbkn.err || exit $?
 python -c "import json; d=json.loads(open('gpurun_out/bench_mpc_dbkn.json').read().strip().split(chr(10))[-1]); print('mpc_dbkn', round(d['value']), d['ms_per_step'])"
+timeout -k 10 180 python tools/collide_prof.py 120 > gpurun_out/collide_prof.log 2>&1 || exit $?
+tail -2 gpurun_out/collide_prof.log
