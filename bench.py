@@ -95,6 +95,43 @@ def launch_ranks(args):
     return bad[0] if bad else 0
 
 
+def cpu_backend_leg(cm, cfg, seed, n, T, threads):
+    """The library's own CPU backend (sim_batch_create(..., -1, ...): the kernels' per-env code
+    compiled for the host, fp32) on `threads` host threads: n envs x T env-steps of the workload
+    (after 2 untimed env-steps).  A measured side line, not the bench's cpu_baseline (the oracle)."""
+    import numpy as np
+    from lerobot_mujoco_sim2real_amd import workloads as W
+    from lerobot_mujoco_sim2real_amd.sim import BatchSim
+    old = os.environ.get("SOARM_CPU_THREADS")
+    os.environ["SOARM_CPU_THREADS"] = str(threads)
+    try:
+        ids = np.arange(n)
+        S = BatchSim(cm, n, -1)
+        q = W.initial_qpos(cm, ids, seed)
+        S.reset(init_qpos=q[:, :5], extra_qpos=q, seed=seed)
+        tab = W.chirp_tables(ids, seed)
+        if cfg["dr"]:
+            S.set_params(**W.dr_params(ids, seed))
+        rng = np.random.default_rng(seed)
+        acts = [np.zeros((n, 5), np.float32) if cfg["action"] == "zero" else
+                W.chirp_action(tab, t).astype(np.float32) if cfg["action"] == "chirp" else
+                rng.uniform(-0.5, 0.5, (n, 5)).astype(np.float32) for t in range(T + 2)]
+        for t in range(2):
+            S.step(acts[t])
+        t0 = time.perf_counter()
+        for t in range(2, T + 2):
+            S.step(acts[t])
+        dt = time.perf_counter() - t0
+        S.close()
+    finally:
+        if old is None:
+            os.environ.pop("SOARM_CPU_THREADS", None)
+        else:
+            os.environ["SOARM_CPU_THREADS"] = old
+    return {"value": n * T / dt, "unit": "env-steps/s", "threads": threads, "dtype": "f32",
+            "sample": f"{n} envs x {T} env-steps of the library's CPU backend (device = -1), {dt:.2f} s"}
+
+
 def cpu_baseline(cfg_name, seconds, seed, solver="pgs", ccd="mpr"):
     """The float64 oracle (C restatement of mj_step; for `mpc` plus the numpy MPC restatement)
     on the host cores, a bounded sample of the same workload: chunks of envs x T env-steps."""
@@ -167,7 +204,7 @@ def cpu_baseline(cfg_name, seconds, seed, solver="pgs", ccd="mpr"):
         dt = time.perf_counter() - t0
         return {"value": 1000 / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
                 "sample": f"1 env x 1000 env-steps (zero action) of the float64 C oracle on 1 thread, {dt:.2f} s",
-                "nproc": os.cpu_count()}
+                "nproc": os.cpu_count(), "fp32_cpu_backend": cpu_backend_leg(cm, cfg, seed, 1, 1000, 1)}
     n = 256
     done, chunk, t0 = 0, 0, time.perf_counter()
     while time.perf_counter() - t0 < seconds:
@@ -189,7 +226,12 @@ def cpu_baseline(cfg_name, seconds, seed, solver="pgs", ccd="mpr"):
     import importlib.util
     mj = "available (not used)" if importlib.util.find_spec("mujoco") else "MuJoCo unavailable"
     what = "float64 C oracle" + (" + numpy MPC restatement" if mpc else "")
+    fp32 = None
+    if cfg["action"] in ("chirp", "random"):  # the library's CPU backend on the same workload
+        fp32 = cpu_backend_leg(cm, cfg, seed, 256, T, cores)
+        fp32["single_core"] = cpu_backend_leg(cm, cfg, seed, 64, T, 1)
     return {"value": done / dt, "unit": "env-steps/s", "cores": cores, "kind": "port",
+            "fp32_cpu_backend": fp32,
             "sample": f"{done} env-steps ({chunk} chunks of {n} envs x {T} steps, {cfg_name} workload) "
                       f"of the {what}, OpenMP over envs, {dt:.1f} s",
             "single_core": {"value": d1 / t1, "sample": f"{d1} env-steps ({c1} chunks of 64 envs x {T} steps) "
