@@ -77,7 +77,7 @@ HDI void fsincos(float x, float* s, float* c) {
 }
 HDI float fpow(float x, float y) {
 #if SOARM_DEVICE_PASS
-  return fpow(x, y);
+  return __powf(x, y);
 #else
   return powf(x, y);
 #endif
