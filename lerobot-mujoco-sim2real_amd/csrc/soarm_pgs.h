@@ -222,7 +222,7 @@ DEVI void wide_sweeps(const DModel& m, WideLds& W, int t) {
   float s1 = x ? W.s1[c][r & (WIDE_X - 1)] : 0.f, f1 = x ? W.f1[c][r & (WIDE_X - 1)] : 0.f;
   const float hd0 = W.hd[c][r], hd1 = x ? W.hd1[c][r & (WIDE_X - 1)] : 0.f;
   const float scale = m.pgs_scale, tol = m.tolerance;
-  int it = W.it[c];
+  int it = min(max(W.it[c], 0), m.iterations);  // (bounded whatever the LDS holds: the loop always ends)
   const int iters = m.iterations;
   for (; it < iters; it++) {
     const float s00 = s0, f00 = f0, s10 = s1, f10 = f1;
@@ -1856,7 +1856,11 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   //   C[E d'][block (j,e)] = -(1/ARd_E,d') w^E_d' . X_jE' u^j_e,   C[E d'][E d] = -(w^E_d' G_E u^E_d + R_E)/ARd_E,d',
   //   C[F d'][F d] = -(w^F_d' G_F u^F_d + R_F)/ARd_F,d',  C[F d'][E d] / C[E d'][F d] through X_EF,
   // with u^c_d = w^c_d = (1, +-mu_c on t(d)) the contact-space direction of edge d.
-  auto wide_round = [&](int it0, auto pk, auto nxc, auto cpl) {
+  // Called with every lane of wave 0 active (a wave-uniform call site): the round's barriers
+  // and wave 0's own share of the sweeps (threads 0-63 = edges of envs 0-3, whose lanes belong
+  // to quads 0-15) need all 64 lanes.  part: this env takes part; the others hand over their
+  // state with a first sweep index of `iterations` (nothing to do) and read nothing back.
+  auto wide_round = [&](int it0, auto pk, auto nxc, auto cpl, bool part) {
     constexpr int NX = decltype(nxc)::value;
     WideLds& W = *L.wide;
     if constexpr (decltype(pk)::value && QUAD) {
@@ -1979,11 +1983,12 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
           }
         }
       }
-      if (sub == 0) W.it[col] = it0;
+      if (sub == 0) W.it[col] = part ? it0 : m.iterations;
       W.flag = NX == 0 ? WIDE_WORK : NX == 4 ? WIDE_WORK4 : WIDE_WORK8;
       __syncthreads();
       wide_sweeps<NX>(m, W, L.lane);
       __syncthreads();
+      if (!part) return;
 #pragma unroll
       for (int k = 0; k < FC; k++)
 #pragma unroll
@@ -2112,16 +2117,19 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       float fE0[4];
 #pragma unroll
       for (int ed = 0; ed < 4; ed++) fE0[ed] = fE[ed];
-      if (fret && !done && L.wide) {
+      const bool wpart = fret && !done;
+      if (L.wide) {
         // the wide kernel: block + E (+ F) one lane per edge until the stopping test passes;
-        // v_arm takes E's (and F's) total force change afterwards (nothing reads it meanwhile)
+        // v_arm takes E's (and F's) total force change afterwards (nothing reads it meanwhile).
+        // (wave-uniform entry: see wide_round)
         float fF0[4];
 #pragma unroll
         for (int ed = 0; ed < 4; ed++) fF0[ed] = fF[ed];
-        wide_round(it, PK{}, std::integral_constant<int, decltype(ext2)::value ? 8 : 4>{}, coupled);
-        done = true;
+        if (__any(wpart))
+          wide_round(it, PK{}, std::integral_constant<int, decltype(ext2)::value ? 8 : 4>{}, coupled, wpart);
+        if (wpart) done = true;
 #ifdef SOARM_PHASE_PROF
-        it = L.wide->it[L.col] - 1;
+        if (wpart) it = L.wide->it[L.col] - 1;
 #endif
         if constexpr (decltype(ext2)::value) {
           float dE[4], dF[4];
@@ -2129,7 +2137,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
           for (int ed = 0; ed < 4; ed++) dE[ed] = fE[ed] - fE0[ed], dF[ed] = fF[ed] - fF0[ed];
           const float DE[3] = {(dE[0] + dE[1]) + (dE[2] + dE[3]), xq.eMu * (dE[0] - dE[1]), xq.eMu * (dE[2] - dE[3])};
           const float DF[3] = {(dF[0] + dF[1]) + (dF[2] + dF[3]), xq.fMu * (dF[0] - dF[1]), xq.fMu * (dF[2] - dF[3])};
-          qvarm(xq.eWp, DE);
+          qvarm(xq.eWp, DE);  // (zero change where the env sat the round out)
           qvarm(xq.fWp, DF);
         }
       } else if (fret && !done)
@@ -2193,11 +2201,11 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
         vpin(ro01), vpin(ro23);
       }
       if (L.wide) {  // wave-uniform: the 4-wave kernel sweeps the block one lane per edge
-        if (!done) {
-          wide_round(it, std::bool_constant<PK::value>{}, std::integral_constant<int, 0>{}, std::false_type{});
+        if (__any(!done)) {
+          const bool part = !done;
+          wide_round(it, std::bool_constant<PK::value>{}, std::integral_constant<int, 0>{}, std::false_type{}, part);
 #ifdef SOARM_PHASE_PROF
-          it = L.wide->it[L.col] - 1;
-          done = it + 1 < m.iterations;
+          if (part) it = L.wide->it[L.col] - 1, done = it + 1 < m.iterations;
 #endif
         }
       } else if (!done)
