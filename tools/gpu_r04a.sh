@@ -2,7 +2,7 @@
 # r04: wide-step microbenchmark, GPU tests (incl. native CCD contacts), contact bench MPR vs native
 mkdir -p gpurun_out
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -o gpurun_out/mb_wide tools/mb_wide.hip 2>/dev/null && timeout -k 5 60 gpurun_out/mb_wide > gpurun_out/mb_wide.log 2>&1; rm -f gpurun_out/mb_wide; cat gpurun_out/mb_wide.log
-timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 150 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
 rc=$?
 echo "pytest rc=$rc" >> gpurun_out/pytest_gpu.log
 grep -E "passed|failed|FAILED|Error|assert" gpurun_out/pytest_gpu.log | tail -25
