@@ -155,19 +155,12 @@ enum { L_DOF = 0, L_SGN = 1, L_AREF = 2, L_R = 3, L_ARD = 4, L_IARD = 5, L_FRC =
 // cost(f0) - cost(f1) = sum_r ARdiag_r / 2 (f1 - f0)_r (s0 + s1)_r, summed over the row.
 constexpr int WIDE_R = 16;       // block edges = lanes per env in the wide sweep
 constexpr int WIDE_COLS = 16;    // envs per workgroup
-// Extra rows (the extra-slot variants, after the arm's frictionloss rows retire): F's and E's
-// 4 edges ride in a second register slot of lanes 0-7 (rows 16-19 F, 20-23 E: the quad sweep's
-// order block, F, E).  WIDE_WORK + NX selects the sweep with NX = 0, 4 (E) or 8 (F, E) extra rows.
-constexpr int WIDE_X = 8;
-constexpr int WIDE_S = WIDE_R + WIDE_X;  // steps of the longest sweep
-enum { WIDE_SKIP = 0, WIDE_WORK = 1, WIDE_EXIT = 2, WIDE_WORK4 = 3, WIDE_WORK8 = 4, WIDE_GEOM = 5 };
+enum { WIDE_WORK = 1, WIDE_EXIT = 2, WIDE_GEOM = 3 };
 struct WideLds {
-  float qpos[WIDE_COLS][SIM_MAXQ];      // WIDE_GEOM: the new positions whose geom poses the helpers write
-  float C[WIDE_COLS][WIDE_R][WIDE_S];   // [env][row][step]: the block's rows
-  float C1[WIDE_COLS][WIDE_X][WIDE_S];  // the extra rows (slot 1 of lanes 0..NX-1)
+  float qpos[WIDE_COLS][SIM_MAXQ];     // WIDE_GEOM: the new positions whose geom poses the helpers write
+  float C[WIDE_COLS][WIDE_R][WIDE_R];  // [env][row][step]
   float s[WIDE_COLS][WIDE_R], f[WIDE_COLS][WIDE_R], hd[WIDE_COLS][WIDE_R];
-  float s1[WIDE_COLS][WIDE_X], f1[WIDE_COLS][WIDE_X], hd1[WIDE_COLS][WIDE_X];
-  int it[WIDE_COLS];                    // first sweep index (>= iterations: nothing to do)
+  int it[WIDE_COLS];                   // first sweep index (>= iterations: nothing to do)
   int flag;
 };
 template <int Q>
@@ -182,70 +175,42 @@ DEVI float rowsum16(float x) {
   x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x128, 0xF, 0xF, false));  // row_ror:8
   return rowbcast<0>(x);
 }
-// one row step: the stepping slot's projected step max(s, -f) is broadcast from lane Q % 16,
-// every row moves by its C entry, the stepping row's force takes the step (oh: one-hot of the
-// lane's row, so only lane Q % 16 changes)
-template <int Q, int NX>
-DEVI void wide_step(const float (&C0)[WIDE_S], const float (&C1)[WIDE_S], const float (&oh)[WIDE_R], float& s0,
-                    float& f0, float& s1, float& f1) {
-  constexpr bool X = Q >= WIDE_R;
+// one row step: the projected step max(s, -f) is broadcast from lane Q, every row moves by its
+// C entry, lane Q's force takes the step (oh: one-hot of the lane's row)
+template <int Q>
+DEVI void wide_step(const float (&Cr)[WIDE_R], const float (&oh)[WIDE_R], float& s, float& f) {
   float cand;
-  asm("v_max_f32_e64 %0, %1, -%2" : "=v"(cand) : "v"(X ? s1 : s0), "v"(X ? f1 : f0));  // max(s, -f), see max_neg
-  const float d = rowbcast<Q % WIDE_R>(cand);
-  s0 = fmaf(C0[Q], d, s0);
-  if constexpr (NX > 0) s1 = fmaf(C1[Q], d, s1);
-  if constexpr (X)
-    f1 = fmaf(oh[Q % WIDE_R], cand, f1);
-  else
-    f0 = fmaf(oh[Q], cand, f0);
+  asm("v_max_f32_e64 %0, %1, -%2" : "=v"(cand) : "v"(s), "v"(f));  // max(s, -f), see max_neg
+  s = fmaf(Cr[Q], rowbcast<Q>(cand), s);
+  f = fmaf(oh[Q], cand, f);
 }
-template <int NX, int... Qs>
-DEVI void wide_sweep(const float (&C0)[WIDE_S], const float (&C1)[WIDE_S], const float (&oh)[WIDE_R], float& s0,
-                     float& f0, float& s1, float& f1, std::integer_sequence<int, Qs...>) {
-  (wide_step<Qs, NX>(C0, C1, oh, s0, f0, s1, f1), ...);
+template <int... Qs>
+DEVI void wide_sweep(const float (&Cr)[WIDE_R], const float (&oh)[WIDE_R], float& s, float& f,
+                     std::integer_sequence<int, Qs...>) {
+  (wide_step<Qs>(Cr, oh, s, f), ...);
 }
 // The wide sweeps of the envs handed over in W, by every thread t of the workgroup (env t / 16,
 // edge t % 16); each env continues from its own sweep index until its stopping test passes.
-template <int NX>
 DEVI void wide_sweeps(const DModel& m, WideLds& W, int t) {
   const int c = t >> 4, r = t & 15;
-  const bool x = NX > 0 && r < NX;  // this lane holds an extra row in slot 1
-  float C0[WIDE_S], C1[WIDE_S], oh[WIDE_R];
+  float Cr[WIDE_R], oh[WIDE_R];
 #pragma unroll
-  for (int q = 0; q < WIDE_S; q++) {
-    C0[q] = q < WIDE_R + NX ? W.C[c][r][q] : 0.f;
-    C1[q] = (q < WIDE_R + NX && x) ? W.C1[c][r & (WIDE_X - 1)][q] : 0.f;
-  }
-#pragma unroll
-  for (int q = 0; q < WIDE_R; q++) oh[q] = q == r ? 1.f : 0.f;
-  float s0 = W.s[c][r], f0 = W.f[c][r];
-  float s1 = x ? W.s1[c][r & (WIDE_X - 1)] : 0.f, f1 = x ? W.f1[c][r & (WIDE_X - 1)] : 0.f;
-  const float hd0 = W.hd[c][r], hd1 = x ? W.hd1[c][r & (WIDE_X - 1)] : 0.f;
-  const float scale = m.pgs_scale, tol = m.tolerance;
+  for (int q = 0; q < WIDE_R; q++) Cr[q] = W.C[c][r][q], oh[q] = q == r ? 1.f : 0.f;
+  float s = W.s[c][r], f = W.f[c][r];
+  const float hd = W.hd[c][r], scale = m.pgs_scale, tol = m.tolerance;
   int it = min(max(W.it[c], 0), m.iterations);  // (bounded whatever the LDS holds: the loop always ends)
   const int iters = m.iterations;
   for (; it < iters; it++) {
-    const float s00 = s0, f00 = f0, s10 = s1, f10 = f1;
-    wide_sweep<NX>(C0, C1, oh, s0, f0, s1, f1, std::make_integer_sequence<int, WIDE_R + NX>{});
-    float im = hd0 * (f0 - f00) * (s00 + s0);
-    if constexpr (NX > 0) im = fmaf(hd1 * (f1 - f10), s10 + s1, im);
-    const float imp = rowsum16(im);
+    const float s0 = s, f0 = f;
+    wide_sweep(Cr, oh, s, f, std::make_integer_sequence<int, WIDE_R>{});
+    const float imp = rowsum16(hd * (f - f0) * (s0 + s));
     if (imp * scale < tol) {
       it++;
       break;
     }
   }
-  W.f[c][r] = f0, W.s[c][r] = s0;  // (the residuals too: a quad sweep may follow, see wide_round)
-  if (x) W.f1[c][r & (WIDE_X - 1)] = f1, W.s1[c][r & (WIDE_X - 1)] = s1;
+  W.f[c][r] = f;
   if (r == 0) W.it[c] = it;
-}
-DEVI void wide_dispatch(const DModel& m, WideLds& W, int t, int flag) {
-  if (flag == WIDE_WORK)
-    wide_sweeps<0>(m, W, t);
-  else if (flag == WIDE_WORK4)
-    wide_sweeps<4>(m, W, t);
-  else if (flag == WIDE_WORK8)
-    wide_sweeps<8>(m, W, t);
 }
 
 // Per-env LDS state, [field][column]: one column per env of the workgroup (64 / lanes per
@@ -458,7 +423,7 @@ namespace soarm {
 // soarm_newton.h), sets S.qacc / S.fcon.
 // Contacts are read straight from the collide output (pair mask + cbuf, pair
 // order).  Returns the number of contacts used.
-template <int NA, int NF, bool CON, int SOL = SIM_SOL_PGS>
+template <int NA, int NF, bool CON, int SOL = SIM_SOL_PGS, bool WIDE = false>
 DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const int* __restrict__ ccount,
                            const uint32_t* __restrict__ pmask, int n, int e, const RowLds& L,
                            const ContactRows<NA, NF>& cr, const PairMask& pm) {
@@ -1849,40 +1814,15 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   // The wide kernel's hand-over round (see WideLds).  Wave 0 writes the rows, the 4 waves sweep,
   // wave 0 reads the forces back; the helper waves wait at the workgroup barrier between rounds
   // (a solve may run none).  Each quad lane writes its block contact's 4 rows (scaled residuals,
-  // forces, ARdiag/2, its rows of C); with NX extra rows (the extra-slot variants after the arm's
-  // frictionloss rows retire: E, or F then E), also their columns of C and, in the second slot of
-  // wide lanes 0..NX-1, the extra rows themselves (lane sub writes F's / E's edge sub):
-  //   C[block (k,e)][E d] = (X_kE folded, as qe01/qe23) . u^E_d,
-  //   C[E d'][block (j,e)] = -(1/ARd_E,d') w^E_d' . X_jE' u^j_e,   C[E d'][E d] = -(w^E_d' G_E u^E_d + R_E)/ARd_E,d',
-  //   C[F d'][F d] = -(w^F_d' G_F u^F_d + R_F)/ARd_F,d',  C[F d'][E d] / C[E d'][F d] through X_EF,
-  // with u^c_d = w^c_d = (1, +-mu_c on t(d)) the contact-space direction of edge d.
-  // Called with every lane of wave 0 active (a wave-uniform call site): the round's barriers
-  // and wave 0's own share of the sweeps (threads 0-63 = edges of envs 0-3, whose lanes belong
-  // to quads 0-15) need all 64 lanes.  part: this env takes part; the others hand over their
-  // state with a first sweep index of `iterations` (nothing to do) and read nothing back.
-  auto wide_round = [&](int it0, auto pk, auto nxc, auto cpl, bool part) {
-    constexpr int NX = decltype(nxc)::value;
+  // forces, ARdiag/2, its rows of C).  Called with every lane of wave 0 active (a wave-uniform
+  // call site): the round's barriers and wave 0's own share of the sweeps (threads 0-63 = the
+  // edges of envs 0-3, whose lanes belong to quads 0-15) need all 64 lanes.  part: this env
+  // takes part; the others hand over their state with a first sweep index of `iterations`
+  // (nothing to do) and read nothing back.
+  auto wide_round = [&](int it0, auto pk, bool part) {
     WideLds& W = *L.wide;
     if constexpr (decltype(pk)::value && QUAD) {
       const int col = L.col;
-      auto edir = [](int d, float mu, int q) {  // component q of (1, +-mu on t(d))
-        return q == 0 ? 1.f : (q == 1 + (d >> 1) ? ((d & 1) ? -mu : mu) : 0.f);
-      };
-      const float muE = NX ? xq.eMu : 0.f, muF = NX == 8 ? xq.fMu : 0.f;
-      float GE[3][3], GF[3][3], XEF[3][3];  // XEF[q][r] = J_E,arm[q] W_F[r]
-      {
-        float ge[6], gf[6];
-#pragma unroll
-        for (int i = 0; i < 6; i++) ge[i] = NX ? EX(E_G + i) : 0.f, gf[i] = NX == 8 ? L.at(cF, F_GRAM + i) : 0.f;
-        const int P[3][3] = {{0, 1, 2}, {1, 3, 4}, {2, 4, 5}};
-#pragma unroll
-        for (int q = 0; q < 3; q++)
-#pragma unroll
-          for (int r = 0; r < 3; r++) {
-            GE[q][r] = ge[P[q][r]], GF[q][r] = gf[P[q][r]];
-            XEF[q][r] = NX == 8 ? EX(F_XE + 3 * q + r) : 0.f;
-          }
-      }
 #pragma unroll
       for (int ed = 0; ed < 4; ed++) {
         const int row = 4 * sub + ed;
@@ -1896,122 +1836,17 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
             const f2 cc = ed < 2 ? C01[j][d] : C23[j][d];
             W.C[col][row][4 * j + d] = (ed & 1) ? cc.y : cc.x;
           }
-        if constexpr (NX > 0) {
-          float qe[3];  // this block edge's residual change per unit contact-space step of E
-#pragma unroll
-          for (int q = 0; q < 3; q++) {
-            const f2 p2 = ed < 2 ? xq.qe01[q] : xq.qe23[q];
-            qe[q] = (ed & 1) ? p2.y : p2.x;
-          }
-#pragma unroll
-          for (int d = 0; d < 4; d++) {
-            float cE = 0.f;
-#pragma unroll
-            for (int q = 0; q < 3; q++) cE = fmaf(qe[q], edir(d, muE, q), cE);
-            if (NX == 8) W.C[col][row][WIDE_R + d] = 0.f;  // F is arm-only
-            W.C[col][row][WIDE_R + NX - 4 + d] = decltype(cpl)::value ? cE : 0.f;
-          }
-        }
-      }
-      if constexpr (NX > 0) {
-        const int dp = sub;  // this lane writes edge dp of E (and of F)
-        {  // E row dp
-          const int x = NX - 4 + dp;
-          const float ia = EX(E_IA + dp), Rp = xq.eRp;
-          const float yt = dp < 2 ? yE[1] : yE[2];
-          const float se = (dp & 1) ? -muE : muE;
-          const float fEd = dp == 0 ? fE[0] : dp == 1 ? fE[1] : dp == 2 ? fE[2] : fE[3];
-          W.s1[col][x] = -(fmaf(Rp, fEd, fmaf(se, yt, yE[0]))) * ia;
-          W.f1[col][x] = fEd;
-          W.hd1[col][x] = EX(E_HD + dp);
-#pragma unroll
-          for (int j = 0; j < FC; j++)
-#pragma unroll
-            for (int e2 = 0; e2 < 4; e2++) {
-              float v = 0.f;  // w^E_dp . X_jE' u^j_e2
-#pragma unroll
-              for (int q = 0; q < 3; q++)
-#pragma unroll
-                for (int rr = 0; rr < 3; rr++)
-                  v = fmaf(edir(dp, muE, q) * EX(E_X + 9 * j + 3 * rr + q), edir(e2, ymu[j], rr), v);
-              W.C1[col][x][4 * j + e2] = decltype(cpl)::value ? -ia * v : 0.f;
-            }
-#pragma unroll
-          for (int d = 0; d < 4; d++) {
-            float vE = 0.f, vF = 0.f;
-#pragma unroll
-            for (int q = 0; q < 3; q++)
-#pragma unroll
-              for (int r = 0; r < 3; r++) {
-                vE = fmaf(edir(dp, muE, q) * GE[q][r], edir(d, muE, r), vE);
-                vF = fmaf(edir(dp, muE, q) * XEF[q][r], edir(d, muF, r), vF);
-              }
-            W.C1[col][x][WIDE_R + NX - 4 + d] = -ia * (vE + (d == dp ? Rp : 0.f));
-            if (NX == 8) W.C1[col][x][WIDE_R + d] = -ia * vF;
-          }
-        }
-        if constexpr (NX == 8) {  // F row dp
-          const int x = dp;
-          const float ia = EX(F_IA + dp), Rp = xq.fRp;
-          float yF[3];
-#pragma unroll
-          for (int q = 0; q < 3; q++) {
-            float t = -EX(F_SH + q);
-#pragma unroll
-            for (int i = 0; i < NA; i++) t = fmaf(EX(F_J + 6 * q + i), v[i], t);
-            yF[q] = t;
-          }
-          const float se = (dp & 1) ? -muF : muF;
-          const float fFd = dp == 0 ? fF[0] : dp == 1 ? fF[1] : dp == 2 ? fF[2] : fF[3];
-          W.s1[col][x] = -(fmaf(Rp, fFd, fmaf(se, dp < 2 ? yF[1] : yF[2], yF[0]))) * ia;
-          W.f1[col][x] = fFd;
-          W.hd1[col][x] = EX(F_HD + dp);
-#pragma unroll
-          for (int q = 0; q < WIDE_R; q++) W.C1[col][x][q] = 0.f;
-#pragma unroll
-          for (int d = 0; d < 4; d++) {
-            float vF = 0.f, vE = 0.f;
-#pragma unroll
-            for (int q = 0; q < 3; q++)
-#pragma unroll
-              for (int r = 0; r < 3; r++) {
-                vF = fmaf(edir(dp, muF, q) * GF[q][r], edir(d, muF, r), vF);
-                vE = fmaf(edir(dp, muF, r) * XEF[q][r], edir(d, muE, q), vE);  // w^F . X_EF' u^E
-              }
-            W.C1[col][x][WIDE_R + d] = -ia * (vF + (d == dp ? Rp : 0.f));
-            W.C1[col][x][WIDE_R + 4 + d] = -ia * vE;
-          }
-        }
       }
       if (sub == 0) W.it[col] = part ? it0 : m.iterations;
-      W.flag = NX == 0 ? WIDE_WORK : NX == 4 ? WIDE_WORK4 : WIDE_WORK8;
+      W.flag = WIDE_WORK;
       __syncthreads();
-      wide_sweeps<NX>(m, W, L.lane);
+      wide_sweeps(m, W, L.lane);
       __syncthreads();
       if (!part) return;
 #pragma unroll
       for (int k = 0; k < FC; k++)
 #pragma unroll
         for (int ed = 0; ed < 4; ed++) cfo[k][ed] = W.f[col][4 * k + ed];
-      // the quad's sweep state back from the rows (the verification sweep after frictionloss
-      // retirement continues from it): this lane's block residuals, and E's contact-space y from
-      // its edge residuals, r_d = -s_d ARdiag_d = y0 +- mu y_t(d) + R f_d
-      ro01 = f2{W.s[col][4 * sub], W.s[col][4 * sub + 1]}, ro23 = f2{W.s[col][4 * sub + 2], W.s[col][4 * sub + 3]};
-      if constexpr (NX > 0) {
-        float rr[4];
-#pragma unroll
-        for (int ed = 0; ed < 4; ed++) {
-          fE[ed] = W.f1[col][NX - 4 + ed];
-          if (NX == 8) fF[ed] = W.f1[col][ed];
-          const float ia = EX(E_IA + ed);
-          rr[ed] = (ia > 0.f ? -W.s1[col][NX - 4 + ed] / ia : 0.f) - xq.eRp * fE[ed];
-        }
-        if (muE > 0.f) {
-          yE[0] = 0.25f * ((rr[0] + rr[1]) + (rr[2] + rr[3]));
-          yE[1] = 0.5f * (rr[0] - rr[1]) / muE;
-          yE[2] = 0.5f * (rr[2] - rr[3]) / muE;
-        }
-      }
     }
   };
   auto ysweeps = [&](auto ext, auto coupled, auto ext2) {
@@ -2117,30 +1952,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       float fE0[4];
 #pragma unroll
       for (int ed = 0; ed < 4; ed++) fE0[ed] = fE[ed];
-      const bool wpart = fret && !done;
-      if (L.wide) {
-        // the wide kernel: block + E (+ F) one lane per edge until the stopping test passes;
-        // v_arm takes E's (and F's) total force change afterwards (nothing reads it meanwhile).
-        // (wave-uniform entry: see wide_round)
-        float fF0[4];
-#pragma unroll
-        for (int ed = 0; ed < 4; ed++) fF0[ed] = fF[ed];
-        if (__any(wpart))
-          wide_round(it, PK{}, std::integral_constant<int, decltype(ext2)::value ? 8 : 4>{}, coupled, wpart);
-        if (wpart) done = true;
-#ifdef SOARM_PHASE_PROF
-        if (wpart) it = L.wide->it[L.col] - 1;
-#endif
-        if constexpr (decltype(ext2)::value) {
-          float dE[4], dF[4];
-#pragma unroll
-          for (int ed = 0; ed < 4; ed++) dE[ed] = fE[ed] - fE0[ed], dF[ed] = fF[ed] - fF0[ed];
-          const float DE[3] = {(dE[0] + dE[1]) + (dE[2] + dE[3]), xq.eMu * (dE[0] - dE[1]), xq.eMu * (dE[2] - dE[3])};
-          const float DF[3] = {(dF[0] + dF[1]) + (dF[2] + dF[3]), xq.fMu * (dF[0] - dF[1]), xq.fMu * (dF[2] - dF[3])};
-          qvarm(xq.eWp, DE);  // (zero change where the env sat the round out)
-          qvarm(xq.fWp, DF);
-        }
-      } else if (fret && !done)
+      if (fret && !done)
         for (; it < m.iterations; it++) {
           float famax = 0.f, ffmax = 0.f;
           if (sweep(std::true_type{}, std::false_type{}, famax, ffmax) * scale < m.tolerance) {
@@ -2168,19 +1980,24 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
         }
       }
       // verification: the retired frictionloss rows were never re-checked against the
-      // v_arm that E (and F) kept moving.  One full sweep with them; if it moves them by more than
-      // ARM_RETIRE on some lane, the full sweeps resume until the stopping test passes.
-      if (fret) {
-        float fa1 = 0.f, ff1 = 0.f;
-        sweep(std::true_type{}, std::true_type{}, fa1, ff1);
-        if (!__all(ff1 <= ARM_RETIRE)) {
+      // v_arm that E (and F) kept moving.  Their would-be steps at the final v_arm, without
+      // applying them: where some env's exceed ARM_RETIRE in total, the full sweeps resume until
+      // the stopping test passes; otherwise the forces stand as they are (an applied extra sweep
+      // would take the result one sweep past the stopping point mj_solPGS reaches)
+      bool fok = true;
+#pragma unroll
+      for (int i = 0; i < NA; i++) {
+        const float fl = m.dof_frictionloss[i];
+        const float res = fmaf(fR[i], ff[i], v[i] - fa[i]);
+        const float fn = fminf(fmaxf(fmaf(res, -fiD[i], ff[i]), -fl), fl);
+        fok = fok && fabsf(fn - ff[i]) <= ARM_RETIRE;  // (a NaN step fails)
+      }
+      if (!__all(!fret || fok)) {
+        if (fret) {
           done = false;
-          for (it++; it < m.iterations; it++) {
+          for (; it < m.iterations; it++) {
             float fa2 = 0.f, ff2 = 0.f;
-            if (sweep(std::true_type{}, std::true_type{}, fa2, ff2) * scale < m.tolerance) {
-              done = true;
-              break;
-            }
+            if (sweep(std::true_type{}, std::true_type{}, fa2, ff2) * scale < m.tolerance) break;
           }
           done = true;  // (no block-only sweeps after these: the block took part in them)
         }
@@ -2200,10 +2017,10 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
         }
         vpin(ro01), vpin(ro23);
       }
-      if (L.wide) {  // wave-uniform: the 4-wave kernel sweeps the block one lane per edge
-        if (__any(!done)) {
+      if constexpr (WIDE) {  // the 4-wave kernel sweeps the block one lane per edge
+        if (__any(!done)) {  // (wave-uniform)
           const bool part = !done;
-          wide_round(it, std::bool_constant<PK::value>{}, std::integral_constant<int, 0>{}, std::false_type{}, part);
+          wide_round(it, std::bool_constant<PK::value>{}, part);
 #ifdef SOARM_PHASE_PROF
           if (part) it = L.wide->it[L.col] - 1, done = it + 1 < m.iterations;
 #endif

@@ -173,7 +173,7 @@ __device__ unsigned long long g_phase[77];  // [53..56] contact-row build split 
 
 // one mj_forward (position + velocity + acceleration stages); the contacts
 // (cbuf/ccount, may be null) were produced by k_collide from this substep's positions
-template <int NA, int NF, bool CON, int SOL>
+template <int NA, int NF, bool CON, int SOL, bool WIDE = false>
 DEVI int forward(Sim<NA, NF>& S, const float* cbuf, const int* ccount, const uint32_t* pmask, int n, int e,
                  const RowLds& L, const ContactRows<NA, NF>& cr, const float* applied = nullptr,
                  PairMask pm = PairMask{}) {
@@ -183,7 +183,7 @@ DEVI int forward(Sim<NA, NF>& S, const float* cbuf, const int* ccount, const uin
   S.smooth_forces();
   pm.hold();
   if (applied) S.add_applied(applied, n, e);
-  return solve_constraints<NA, NF, CON, SOL>(S, cbuf, ccount, pmask, n, e, L, cr, pm);
+  return solve_constraints<NA, NF, CON, SOL, WIDE>(S, cbuf, ccount, pmask, n, e, L, cr, pm);
 }
 
 // contact-free scenes (mjDSBL_CONTACT): all frame_skip substeps fused in one launch.
@@ -345,7 +345,7 @@ __global__ __launch_bounds__(WIDE ? 256 : 64) void k_substep(const DModel* __res
           write_geom_poses(G, gpose, n, eg, k, 12);
           continue;
         }
-        wide_dispatch(*dm, s_wide, (int)threadIdx.x, fl);
+        wide_sweeps(*dm, s_wide, (int)threadIdx.x);  // (WIDE_WORK)
         __syncthreads();
       }
     }
@@ -399,9 +399,9 @@ __global__ __launch_bounds__(WIDE ? 256 : 64) void k_substep(const DModel* __res
   PSTAMP(5);
   pm.hold();
   if (AP) S.add_applied(st.qfrc_applied, n, e);
-  int ncon = solve_constraints<NA, NF, true, SOL>(S, use ? cbuf : nullptr, use ? ccount : nullptr, pmask, n, e, L, cr, pm);
+  int ncon = solve_constraints<NA, NF, true, SOL, WIDE>(S, use ? cbuf : nullptr, use ? ccount : nullptr, pmask, n, e, L, cr, pm);
 #else
-  int ncon = forward<NA, NF, true, SOL>(S, use ? cbuf : nullptr, use ? ccount : nullptr, pmask, n, e, L, cr,
+  int ncon = forward<NA, NF, true, SOL, WIDE>(S, use ? cbuf : nullptr, use ? ccount : nullptr, pmask, n, e, L, cr,
                                         AP ? st.qfrc_applied : nullptr, pm);
 #endif
   if (S.acc_bad()) {
