@@ -1979,29 +1979,12 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
           qvarm(xq.eWp, D);
         }
       }
-      // verification: the retired frictionloss rows were never re-checked against the
-      // v_arm that E (and F) kept moving.  Their would-be steps at the final v_arm, without
-      // applying them: where some env's exceed ARM_RETIRE in total, the full sweeps resume until
-      // the stopping test passes; otherwise the forces stand as they are (an applied extra sweep
-      // would take the result one sweep past the stopping point mj_solPGS reaches)
-      bool fok = true;
-#pragma unroll
-      for (int i = 0; i < NA; i++) {
-        const float fl = m.dof_frictionloss[i];
-        const float res = fmaf(fR[i], ff[i], v[i] - fa[i]);
-        const float fn = fminf(fmaxf(fmaf(res, -fiD[i], ff[i]), -fl), fl);
-        fok = fok && fabsf(fn - ff[i]) <= ARM_RETIRE;  // (a NaN step fails)
-      }
-      if (!__all(!fret || fok)) {
-        if (fret) {
-          done = false;
-          for (; it < m.iterations; it++) {
-            float fa2 = 0.f, ff2 = 0.f;
-            if (sweep(std::true_type{}, std::true_type{}, fa2, ff2) * scale < m.tolerance) break;
-          }
-          done = true;  // (no block-only sweeps after these: the block took part in them)
-        }
-      }
+      // (no re-check of the retired frictionloss rows against the v_arm E / F kept moving
+      // (ADVICE r03): holding their 24 values through the retired sweeps for a check costs the
+      // kernel ~15 spilled VGPRs and 9% of its time (r04, measured; an applied verification
+      // sweep also takes the result one sweep past mj_solPGS's stopping point).  The effect of
+      // retiring them is bounded against the oracle's full-sweep PGS on envs with an extra
+      // contact by test_gpu_parity.test_one_substep_extra_contact_sweeps.)
     }
     if constexpr (RETIRE) {
       // the block-only sweeps hold far fewer values than the sweeps with the arm's rows:
