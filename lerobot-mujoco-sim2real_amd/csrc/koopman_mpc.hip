@@ -19,6 +19,7 @@
 // conflict-free, lane-contiguous ds_read_b64.  4096 envs = 256 waves = 64 workgroups of 4 waves.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -267,8 +268,16 @@ __global__ __launch_bounds__(256) void k_feedforward(KDev K, const double* __res
 // y / e [nz] each (35 KB at nz 32, nu 5, H 10); BL_EPW envs (waves) per workgroup.
 struct BDev {
   int nz, nu, H, N, delta, per_env;  // per_env: doubles of LDS per env
+  int xreg;                          // doubles of the X / packed-Hessian region
   double q, r, uclip;
 };
+// a double of lane l (l wave-uniform) in every lane: two v_readlane
+DEVI double rdlane(double x, int l) {
+  const long long b = __double_as_longlong(x);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(b & 0xffffffff), l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
 // LDS written by other lanes of this wave is read after this (the wave's LDS operations complete
 // in order once issued; the fence keeps the compiler from moving them across)
 DEVI void wsync() {
@@ -287,10 +296,10 @@ __global__ __launch_bounds__(64 * BL_EPW) void k_bilinear(BDev K, const double* 
   const int e = blockIdx.x * BL_EPW + w;
   if (e >= n) return;  // (whole waves: no workgroup barrier below)
   const int nz = K.nz, nu = K.nu, H = K.H, N = K.N, zu = nz * nu;
-  double* X = lds + (size_t)w * K.per_env;  // [H][zu]
-  double* M = X + H * zu;                   // [zu]
-  double* Hs = M + zu;                      // [N][N]
-  double* zb = Hs + N * N;                  // [nz]: z0, then A^t z0
+  double* X = lds + (size_t)w * K.per_env;  // [H][zu]; later the packed Hessian (N (N + 1) / 2)
+  double* M = X + K.xreg;                   // [zu]
+  double* G = M + zu;                       // [N][N] Gram of the stacked X_k (lower tiles)
+  double* zb = G + N * N;                   // [nz]: z0, then A^t z0
   double* eb = zb + nz;                     // [nz]: e_t
   for (int i = lane; i < nz; i += 64) zb[i] = z0g[(size_t)i * n + e];
   double up[8];
@@ -331,24 +340,8 @@ __global__ __launch_bounds__(64 * BL_EPW) void k_bilinear(BDev K, const double* 
     }
     wsync();
   }
-  // Hessian: lane per (d, c1, c2); Hs[s1][s1 + d](c1, c2) = q S_d(H - 1 - s1 - d),
-  // S_d(m) = sum_{b <= m} W[b + d][b](c1, c2)
-  for (int tr = lane; tr < H * nu * nu; tr += 64) {
-    const int d = tr / (nu * nu), c1 = (tr / nu) % nu, c2 = tr % nu;
-    double S = 0.0;
-    for (int b = 0; b + d < H; b++) {
-      const double* xa = X + (b + d) * zu + c1;  // X_{b+d}[:, c1]
-      const double* xb = X + b * zu + c2;        // X_b[:, c2]
-      double wv = 0.0;
-      for (int i = 0; i < nz; i++) wv = fma(xa[i * nu], xb[i * nu], wv);
-      S += wv;
-      const int s1 = H - 1 - b - d, s2 = s1 + d;  // the block whose sum ends at b
-      const double hv = K.q * S + ((d == 0 && c1 == c2) ? K.r : 0.0);
-      Hs[(s1 * nu + c1) * N + s2 * nu + c2] = hv;
-      Hs[(s2 * nu + c2) * N + s1 * nu + c1] = hv;
-    }
-  }
   // rhs (lane l = s nu + c): e_t = ref_t - A^{t+1} z0 - [delta] C_t u_prev, rhs[s] += q X_{t-s}' e_t
+  // (before the Hessian: the packed Hessian overwrites X's storage)
   double rhs = 0.0;
   const int ls = lane / nu, lc = lane - ls * nu;
   for (int t = 0; t < H; t++) {
@@ -377,41 +370,100 @@ __global__ __launch_bounds__(64 * BL_EPW) void k_bilinear(BDev K, const double* 
     }
     wsync();
   }
-  // Cholesky Hs = L L' in place (lower triangle); the trailing update over (i, k) pairs
+  // Gram G[a][b] = sum_i X[i][a] X[i][b] over the N = H nu columns a = k nu + c of the stacked X_k
+  // (rows i < nz), on the f64 MFMA: the A fragment of (tile t, k-step ks) -- lane l holds
+  // X[4 ks + (l >> 4)][16 t + (l & 15)] -- is also the B fragment of (t, ks), so 4 fragment loads
+  // per k-step feed the <= 10 lower tiles (ta >= tb); C: lane l, register r = row (l >> 4) + 4 r,
+  // column l & 15 of the tile.  Stored to G (its lower tiles: every (max, min) index lives there).
+  {
+    const int NT = (N + 15) >> 4, KS = (nz + 3) >> 2;
+    d4 acc[10];
+#pragma unroll
+    for (int q = 0; q < 10; q++) acc[q] = d4{0.0, 0.0, 0.0, 0.0};
+    const int fr = lane >> 4, fc = lane & 15;
+    for (int ks = 0; ks < KS; ks++) {
+      double fg[4];
+      const int i = 4 * ks + fr;
+#pragma unroll
+      for (int t = 0; t < 4; t++) {
+        const int a = 16 * t + fc, k = a / nu;
+        fg[t] = (t < NT && a < N && i < nz) ? X[k * zu + i * nu + (a - k * nu)] : 0.0;
+      }
+#pragma unroll
+      for (int ta = 0, q = 0; ta < 4; ta++)
+#pragma unroll
+        for (int tb = 0; tb <= ta; tb++, q++)
+          if (ta < NT) acc[q] = mfma(fg[ta], fg[tb], acc[q]);
+    }
+#pragma unroll
+    for (int ta = 0, q = 0; ta < 4; ta++)
+#pragma unroll
+      for (int tb = 0; tb <= ta; tb++, q++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int row = 16 * ta + fr + 4 * r, col = 16 * tb + fc;
+          if (ta < NT && row < N && col < N) G[row * N + col] = acc[q][r];
+        }
+  }
+  wsync();
+  // Hessian, packed lower into X's storage (P[R (R + 1) / 2 + C], R >= C): one lane per block
+  // diagonal d and (c1, c2); Hess[(s1, c1)][(s1 + d, c2)] = q sum_{b <= H-1-s1-d} W[b + d][b](c1, c2)
+  // + r [d = 0, c1 = c2], W[k1][k2](c1, c2) = G[k1 nu + c1][k2 nu + c2], a running sum over b
+  double* P = X;
+  for (int tr = lane; tr < H * nu * nu; tr += 64) {
+    const int d = tr / (nu * nu), c1 = (tr / nu) % nu, c2 = tr % nu;
+    if (d == 0 && c1 < c2) continue;  // (its symmetric twin writes the element)
+    double S = 0.0;
+    for (int b = 0; b + d < H; b++) {
+      const int a1 = (b + d) * nu + c1, a2 = b * nu + c2;
+      S += a1 >= a2 ? G[a1 * N + a2] : G[a2 * N + a1];
+      const int s1 = H - 1 - b - d, s2 = s1 + d;
+      const int R = s2 * nu + c2, Cc = s1 * nu + c1;  // (d = 0: c1 >= c2, so R <= Cc there)
+      const double hv = K.q * S + ((d == 0 && c1 == c2) ? K.r : 0.0);
+      if (R >= Cc)
+        P[R * (R + 1) / 2 + Cc] = hv;
+      else
+        P[Cc * (Cc + 1) / 2 + R] = hv;
+    }
+  }
+  wsync();
+  // Cholesky P = L L' in place (packed lower, right-looking).  Lane l keeps 1 / L[l][l].  The
+  // trailing update is spread over the lanes by packed pair index p = (ii, kk), ii >= kk: lane l
+  // walks p = l, l + 64, ... from its own start (ii0, kk0), advanced incrementally (no sqrt)
+  int ii0 = 0, kk0 = lane;
+  while (kk0 > ii0) kk0 -= ii0 + 1, ii0++;
+  double idg = 0.0;
   for (int j = 0; j < N; j++) {
-    const double dj = sqrt(Hs[j * N + j]);
+    const int jj = j * (j + 1) / 2;
+    const double dj = sqrt(P[jj + j]), id = 1.0 / dj;
     wsync();
-    for (int i = j + 1 + lane; i < N; i += 64) Hs[i * N + j] /= dj;
-    if (lane == 0) Hs[j * N + j] = dj;
+    if (lane == j) idg = id;
+    const int i1 = j + 1 + lane;
+    if (i1 < N) P[i1 * (i1 + 1) / 2 + j] *= id;
+    if (lane == 0) P[jj + j] = dj;
     wsync();
-    const int m = N - j - 1;  // trailing size; pairs (i >= k) in [j+1, N)
-    for (int p = lane; p < m * (m + 1) / 2; p += 64) {
-      int ii = (int)((sqrt(8.0 * p + 1.0) - 1.0) * 0.5);  // row of pair p in the packed triangle
-      while ((ii + 1) * (ii + 2) / 2 <= p) ii++;
-      while (ii * (ii + 1) / 2 > p) ii--;
-      const int kk = p - ii * (ii + 1) / 2;
+    const int m = N - j - 1, np = m * (m + 1) / 2;
+    int ii = ii0, kk = kk0;
+    for (int p = lane; p < np; p += 64) {
       const int i = j + 1 + ii, k2 = j + 1 + kk;
-      Hs[i * N + k2] = fma(-Hs[i * N + j], Hs[k2 * N + j], Hs[i * N + k2]);
+      const int ri = i * (i + 1) / 2;
+      P[ri + k2] = fma(-P[ri + j], P[k2 * (k2 + 1) / 2 + j], P[ri + k2]);
+      kk += 64;
+      while (kk > ii) kk -= ii + 1, ii++;
     }
     wsync();
   }
-  // L y = rhs, L' v = y: lane i holds row i's value
+  // L y = rhs, L' v = y: lane i holds row i's value; the pivot's comes by readlane
   double y = rhs;
   for (int j = 0; j < N; j++) {
-    if (lane == j) eb[0] = y / Hs[j * N + j];
-    wsync();
-    const double yj = eb[0];
+    const double yj = rdlane(y, j) * rdlane(idg, j);
     if (lane == j) y = yj;
-    if (lane > j && lane < N) y = fma(-Hs[lane * N + j], yj, y);
-    wsync();
+    if (lane > j && lane < N) y = fma(-P[lane * (lane + 1) / 2 + j], yj, y);
   }
   for (int j = N - 1; j >= 0; j--) {
-    if (lane == j) eb[0] = y / Hs[j * N + j];
-    wsync();
-    const double vj = eb[0];
+    const double vj = rdlane(y, j) * rdlane(idg, j);
     if (lane == j) y = vj;
-    if (lane < j) y = fma(-Hs[j * N + lane], vj, y);
-    wsync();
+    if (lane < j) y = fma(-P[j * (j + 1) / 2 + lane], vj, y);
   }
   if (lane < nu) {  // u0 = v_0 + u_prev (get_control, MPC_Controler.py:147-149)
     double upl = 0.0;
@@ -560,7 +612,8 @@ int sim_koopman_set_bilinear(sim_koopman* k, const double* A, const double* B, c
   if (!(q > 0.0) || !(r > 0.0)) return soarm_set_error(SIM_E_ARG, "bilinear MPC: q and r must be positive");
   BDev b{};
   b.nz = nz, b.nu = nu, b.H = H, b.N = N, b.delta = delta ? 1 : 0, b.q = q, b.r = r, b.uclip = k->kd.uclip;
-  b.per_env = (H * nz * nu + nz * nu + N * N + 2 * nz + 1) & ~1;
+  b.xreg = std::max(H * nz * nu, N * (N + 1) / 2);
+  b.per_env = (b.xreg + nz * nu + N * N + 2 * nz + 1) & ~1;
   if ((size_t)b.per_env * BL_EPW * 8 > 160 * 1024) return soarm_set_error(SIM_E_MODEL, "bilinear MPC does not fit in LDS");
   std::vector<double> hht((size_t)nz * nu * nz);
   for (int j = 0; j < nz; j++)

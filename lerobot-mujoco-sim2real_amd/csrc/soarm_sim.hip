@@ -1220,15 +1220,13 @@ int sim_reset(sim_batch* b, const sim_state* s, const float* init_qpos, const fl
 }
 
 // the 4-wave wide PGS substep (k_substep<..., WIDE>): whole 16-env workgroups, and at most one
-// wave per SIMD in total (its waves hold 512 registers: 4096 envs = 1024 waves); larger batches
-// keep the one-wave kernel, whose 64-lane workgroups already fill the SIMDs.  SOARM_WIDE=0
-// disables it (A/B).
+// wave per SIMD in total (its waves hold 512 registers: 4096 envs = 1024 waves).  Opt-in
+// (SOARM_WIDE=1, read when the env-step is enqueued): measured at the headline's 4096 envs it
+// runs 2% slower than the one-wave quad kernel (DESIGN.md §4 "Wide PGS sweep"), whose launch
+// time is set by the extra-contact waves the wide rounds do not cover.
 static bool wide_ok(const sim_batch* b) {
-  static const bool on = [] {
-    const char* v = getenv("SOARM_WIDE");
-    return !(v && v[0] == '0');
-  }();
-  return on && b->n % WIDE_COLS == 0 && b->n <= 4096;
+  const char* v = getenv("SOARM_WIDE");
+  return v && v[0] == '1' && b->n % WIDE_COLS == 0 && b->n <= 4096;
 }
 
 int sim_step(sim_batch* b, const sim_state* s, const float* action, int frame_skip, float* obs,
