@@ -285,6 +285,21 @@ DEVI void wsync() {
   __builtin_amdgcn_wave_barrier();
 }
 constexpr int BL_EPW = 4;
+// sum_j x[j * sx] y[j], j < len: four independent FMA chains (the loads of a step do not wait for
+// the previous step's FMA)
+DEVI double dotn(const double* x, int sx, const double* y, int len) {
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  int j = 0;
+#pragma unroll 2
+  for (; j + 4 <= len; j += 4) {
+    s0 = fma(x[j * sx], y[j], s0);
+    s1 = fma(x[(j + 1) * sx], y[j + 1], s1);
+    s2 = fma(x[(j + 2) * sx], y[j + 2], s2);
+    s3 = fma(x[(j + 3) * sx], y[j + 3], s3);
+  }
+  for (; j < len; j++) s0 = fma(x[j * sx], y[j], s0);
+  return (s0 + s1) + (s2 + s3);
+}
 __global__ __launch_bounds__(64 * BL_EPW) void k_bilinear(BDev K, const double* __restrict__ A,
                                                           const double* __restrict__ Bm,
                                                           const double* __restrict__ HhT, int n,
@@ -294,8 +309,13 @@ __global__ __launch_bounds__(64 * BL_EPW) void k_bilinear(BDev K, const double* 
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int e = blockIdx.x * BL_EPW + w;
-  if (e >= n) return;  // (whole waves: no workgroup barrier below)
   const int nz = K.nz, nu = K.nu, H = K.H, N = K.N, zu = nz * nu;
+  // A, shared by the workgroup's envs: every product with A reads it from LDS (a global read in
+  // each step of a dependent FMA chain costs the latency of the cache hierarchy per step)
+  double* As = lds + (size_t)BL_EPW * K.per_env;
+  for (int i = threadIdx.x; i < nz * nz; i += blockDim.x) As[i] = A[i];
+  __syncthreads();
+  if (e >= n) return;  // (whole waves: no workgroup barrier below)
   double* X = lds + (size_t)w * K.per_env;  // [H][zu]; later the packed Hessian (N (N + 1) / 2)
   double* M = X + K.xreg;                   // [zu]
   double* G = M + zu;                       // [N][N] Gram of the stacked X_k (lower tiles)
@@ -308,9 +328,7 @@ __global__ __launch_bounds__(64 * BL_EPW) void k_bilinear(BDev K, const double* 
   wsync();
   // B_total = B + sum_j z0_j Hhat_j  (HhT [(i nu + c)][j])
   for (int o = lane; o < zu; o += 64) {
-    double s = Bm[o];
-    const double* h = HhT + (size_t)o * nz;
-    for (int j = 0; j < nz; j++) s = fma(h[j], zb[j], s);
+    const double s = Bm[o] + dotn(HhT + (size_t)o * nz, 1, zb, nz);
     M[o] = s, X[o] = s;
   }
   wsync();
@@ -323,10 +341,7 @@ __global__ __launch_bounds__(64 * BL_EPW) void k_bilinear(BDev K, const double* 
       nm[q] = 0.0;
       if (o < zu) {
         const int i = o / nu, c = o - i * nu;
-        double s = 0.0;
-        const double* a = A + (size_t)i * nz;
-        for (int j = 0; j < nz; j++) s = fma(a[j], M[j * nu + c], s);
-        nm[q] = s;
+        nm[q] = dotn(M + c, nu, As + i * nz, nz);
       }
     }
     wsync();  // (every lane has read M_{k-1})
@@ -346,10 +361,7 @@ __global__ __launch_bounds__(64 * BL_EPW) void k_bilinear(BDev K, const double* 
   const int ls = lane / nu, lc = lane - ls * nu;
   for (int t = 0; t < H; t++) {
     double yn = 0.0;
-    if (lane < nz) {
-      const double* a = A + (size_t)lane * nz;
-      for (int j = 0; j < nz; j++) yn = fma(a[j], zb[j], yn);
-    }
+    if (lane < nz) yn = dotn(zb, 1, As + lane * nz, nz);
     wsync();
     if (lane < nz) {
       zb[lane] = yn;
@@ -363,10 +375,7 @@ __global__ __launch_bounds__(64 * BL_EPW) void k_bilinear(BDev K, const double* 
     }
     wsync();
     if (lane < N && ls <= t) {
-      const double* xk = X + (t - ls) * zu + lc;
-      double s = 0.0;
-      for (int i = 0; i < nz; i++) s = fma(xk[i * nu], eb[i], s);
-      rhs = fma(K.q, s, rhs);
+      rhs = fma(K.q, dotn(X + (t - ls) * zu + lc, nu, eb, nz), rhs);
     }
     wsync();
   }
@@ -614,7 +623,8 @@ int sim_koopman_set_bilinear(sim_koopman* k, const double* A, const double* B, c
   b.nz = nz, b.nu = nu, b.H = H, b.N = N, b.delta = delta ? 1 : 0, b.q = q, b.r = r, b.uclip = k->kd.uclip;
   b.xreg = std::max(H * nz * nu, N * (N + 1) / 2);
   b.per_env = (b.xreg + nz * nu + N * N + 2 * nz + 1) & ~1;
-  if ((size_t)b.per_env * BL_EPW * 8 > 160 * 1024) return soarm_set_error(SIM_E_MODEL, "bilinear MPC does not fit in LDS");
+  if (((size_t)b.per_env * BL_EPW + (size_t)nz * nz) * 8 > 160 * 1024)
+    return soarm_set_error(SIM_E_MODEL, "bilinear MPC does not fit in LDS");
   std::vector<double> hht((size_t)nz * nu * nz);
   for (int j = 0; j < nz; j++)
     for (int i = 0; i < nz; i++)
@@ -639,7 +649,8 @@ int sim_koopman_bilinear_step(sim_koopman* k, int n, const double* z0, const dou
   if (!k->d_A) return soarm_set_error(SIM_E_ARG, "sim_koopman_set_bilinear was not called");
   if (n == 0) return SIM_OK;
   hipLaunchKernelGGL(k_bilinear, dim3((n + BL_EPW - 1) / BL_EPW), dim3(64 * BL_EPW),
-                     (size_t)k->bd.per_env * BL_EPW * sizeof(double), (hipStream_t)stream, k->bd, k->d_A, k->d_B,
+                     ((size_t)k->bd.per_env * BL_EPW + (size_t)k->bd.nz * k->bd.nz) * sizeof(double), (hipStream_t)stream,
+                     k->bd, k->d_A, k->d_B,
                      k->d_HhT, n, z0, window, u_prev, action);
   KCHECK(hipGetLastError());
   return SIM_OK;
