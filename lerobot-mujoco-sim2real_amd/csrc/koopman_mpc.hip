@@ -258,16 +258,21 @@ __global__ __launch_bounds__(256) void k_feedforward(KDev K, const double* __res
 // The bilinear model's input matrix depends on the lifted state: B_total = B + sum_j z0_j Hhat_j
 // (linearize_B, MPC_Controler.py:46-63), so the condensed QP (MPC_Controler.py:100-141, state_full:
 // Q = q I, R = r I) differs per env and frame.  One wave per env, float64, everything in LDS:
-//   M_0 = B_total, M_k = A M_{k-1}; X_k = M_k ('mpc') or C_k = sum_{i<=k} M_i ('delta_mpc');
-//   Hess[s1][s2] = q sum_{t >= max(s1,s2)} X_{t-s1}' X_{t-s2} + r I -- along each block diagonal
-//     d = s2 - s1 a running sum of W[b+d][b] = X_{b+d}' X_b (one lane per (d, c1, c2));
+//   M_0 = B_total, M_k = A M_{k-1}; X_k = M_k ('mpc') or C_k = sum_{i<=k} M_i ('delta_mpc')
+//     (A staged in LDS once per workgroup);
 //   rhs[s] = q sum_{t >= s} X_{t-s}' e_t, e_t = ref_t - A^{t+1} z0 - [delta] C_t u_prev;
+//   G = Xs' Xs, the Gram of the stacked X_k (N = H nu columns, nz rows) on the f64 MFMA;
+//   Hess[s1][s2] = q sum_{t >= max(s1,s2)} X_{t-s1}' X_{t-s2} + r I -- along each block diagonal
+//     d = s2 - s1 a running sum of G's blocks W[b+d][b] (one lane per (d, c1, c2)), packed lower;
 //   v = Hess^-1 rhs by an in-LDS Cholesky (right-looking; the trailing update spread over the
-//   wave's lanes) and two triangular solves; u0 = v_0 + u_prev, action = clip(u0).
-// Shapes: nz <= 64, nu <= 8, N = H nu <= 64.  Per env LDS: X [H][nz*nu], M [nz*nu], Hess [N][N],
-// y / e [nz] each (35 KB at nz 32, nu 5, H 10); BL_EPW envs (waves) per workgroup.
+//   wave's lanes by packed pair index) and two triangular solves (pivots by readlane);
+//   u0 = v_0 + u_prev, action = clip(u0).
+// Shapes: nz <= 64, nu <= 8, N = H nu <= 64.  Per env LDS: the X region (X [H][nz*nu], later the
+// packed Hessian), M [nz*nu], G packed, y / e [nz] each (24.8 KB at nz 32, nu 5, H 10); up to
+// 6 envs (waves) per workgroup, or as many as the LDS holds with A [nz][nz].
 struct BDev {
   int nz, nu, H, N, delta, per_env;  // per_env: doubles of LDS per env
+  int epw;                           // envs (waves) per workgroup
   int xreg;                          // doubles of the X / packed-Hessian region
   double q, r, uclip;
 };
@@ -284,7 +289,6 @@ DEVI void wsync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
 }
-constexpr int BL_EPW = 4;
 // sum_j x[j * sx] y[j], j < len: four independent FMA chains (the loads of a step do not wait for
 // the previous step's FMA)
 DEVI double dotn(const double* x, int sx, const double* y, int len) {
@@ -300,7 +304,8 @@ DEVI double dotn(const double* x, int sx, const double* y, int len) {
   for (; j < len; j++) s0 = fma(x[j * sx], y[j], s0);
   return (s0 + s1) + (s2 + s3);
 }
-__global__ __launch_bounds__(64 * BL_EPW) void k_bilinear(BDev K, const double* __restrict__ A,
+template <int EPW>
+__global__ __launch_bounds__(64 * EPW) void k_bilinear(BDev K, const double* __restrict__ A,
                                                           const double* __restrict__ Bm,
                                                           const double* __restrict__ HhT, int n,
                                                           const double* __restrict__ z0g,
@@ -308,18 +313,18 @@ __global__ __launch_bounds__(64 * BL_EPW) void k_bilinear(BDev K, const double* 
                                                           double* __restrict__ uprev, float* __restrict__ action) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int e = blockIdx.x * BL_EPW + w;
+  const int e = blockIdx.x * EPW + w;
   const int nz = K.nz, nu = K.nu, H = K.H, N = K.N, zu = nz * nu;
   // A, shared by the workgroup's envs: every product with A reads it from LDS (a global read in
   // each step of a dependent FMA chain costs the latency of the cache hierarchy per step)
-  double* As = lds + (size_t)BL_EPW * K.per_env;
+  double* As = lds + (size_t)EPW * K.per_env;
   for (int i = threadIdx.x; i < nz * nz; i += blockDim.x) As[i] = A[i];
   __syncthreads();
   if (e >= n) return;  // (whole waves: no workgroup barrier below)
   double* X = lds + (size_t)w * K.per_env;  // [H][zu]; later the packed Hessian (N (N + 1) / 2)
   double* M = X + K.xreg;                   // [zu]
-  double* G = M + zu;                       // [N][N] Gram of the stacked X_k (lower tiles)
-  double* zb = G + N * N;                   // [nz]: z0, then A^t z0
+  double* G = M + zu;                       // Gram of the stacked X_k, packed lower (N (N + 1) / 2)
+  double* zb = G + N * (N + 1) / 2;         // [nz]: z0, then A^t z0
   double* eb = zb + nz;                     // [nz]: e_t
   for (int i = lane; i < nz; i += 64) zb[i] = z0g[(size_t)i * n + e];
   double up[8];
@@ -383,7 +388,7 @@ __global__ __launch_bounds__(64 * BL_EPW) void k_bilinear(BDev K, const double* 
   // (rows i < nz), on the f64 MFMA: the A fragment of (tile t, k-step ks) -- lane l holds
   // X[4 ks + (l >> 4)][16 t + (l & 15)] -- is also the B fragment of (t, ks), so 4 fragment loads
   // per k-step feed the <= 10 lower tiles (ta >= tb); C: lane l, register r = row (l >> 4) + 4 r,
-  // column l & 15 of the tile.  Stored to G (its lower tiles: every (max, min) index lives there).
+  // column l & 15 of the tile.  Stored packed lower (row >= col).
   {
     const int NT = (N + 15) >> 4, KS = (nz + 3) >> 2;
     d4 acc[10];
@@ -411,7 +416,7 @@ __global__ __launch_bounds__(64 * BL_EPW) void k_bilinear(BDev K, const double* 
 #pragma unroll
         for (int r = 0; r < 4; r++) {
           const int row = 16 * ta + fr + 4 * r, col = 16 * tb + fc;
-          if (ta < NT && row < N && col < N) G[row * N + col] = acc[q][r];
+          if (ta < NT && row < N && col <= row) G[row * (row + 1) / 2 + col] = acc[q][r];
         }
   }
   wsync();
@@ -425,7 +430,7 @@ __global__ __launch_bounds__(64 * BL_EPW) void k_bilinear(BDev K, const double* 
     double S = 0.0;
     for (int b = 0; b + d < H; b++) {
       const int a1 = (b + d) * nu + c1, a2 = b * nu + c2;
-      S += a1 >= a2 ? G[a1 * N + a2] : G[a2 * N + a1];
+      S += a1 >= a2 ? G[a1 * (a1 + 1) / 2 + a2] : G[a2 * (a2 + 1) / 2 + a1];
       const int s1 = H - 1 - b - d, s2 = s1 + d;
       const int R = s2 * nu + c2, Cc = s1 * nu + c1;  // (d = 0: c1 >= c2, so R <= Cc there)
       const double hv = K.q * S + ((d == 0 && c1 == c2) ? K.r : 0.0);
@@ -622,9 +627,12 @@ int sim_koopman_set_bilinear(sim_koopman* k, const double* A, const double* B, c
   BDev b{};
   b.nz = nz, b.nu = nu, b.H = H, b.N = N, b.delta = delta ? 1 : 0, b.q = q, b.r = r, b.uclip = k->kd.uclip;
   b.xreg = std::max(H * nz * nu, N * (N + 1) / 2);
-  b.per_env = (b.xreg + nz * nu + N * N + 2 * nz + 1) & ~1;
-  if (((size_t)b.per_env * BL_EPW + (size_t)nz * nz) * 8 > 160 * 1024)
-    return soarm_set_error(SIM_E_MODEL, "bilinear MPC does not fit in LDS");
+  b.per_env = (b.xreg + nz * nu + N * (N + 1) / 2 + 2 * nz + 1) & ~1;
+  // as many envs per workgroup as fit the CU's LDS with A (6 at nz 32, nu 5, H 10: 157 KB)
+  b.epw = 0;
+  for (int ep : {6, 4, 2, 1})
+    if (!b.epw && ((size_t)b.per_env * ep + (size_t)nz * nz) * 8 <= 160 * 1024) b.epw = ep;
+  if (!b.epw) return soarm_set_error(SIM_E_MODEL, "bilinear MPC does not fit in LDS");
   std::vector<double> hht((size_t)nz * nu * nz);
   for (int j = 0; j < nz; j++)
     for (int i = 0; i < nz; i++)
@@ -638,7 +646,9 @@ int sim_koopman_set_bilinear(sim_koopman* k, const double* A, const double* B, c
   KCHECK(hipMemcpy(k->d_A, A, (size_t)nz * nz * 8, hipMemcpyHostToDevice));
   KCHECK(hipMemcpy(k->d_B, B, (size_t)nz * nu * 8, hipMemcpyHostToDevice));
   KCHECK(hipMemcpy(k->d_HhT, hht.data(), hht.size() * 8, hipMemcpyHostToDevice));
-  KCHECK(hipFuncSetAttribute((const void*)k_bilinear, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  for (const void* f : {(const void*)k_bilinear<6>, (const void*)k_bilinear<4>, (const void*)k_bilinear<2>,
+                        (const void*)k_bilinear<1>})
+    KCHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   k->bd = b;
   return SIM_OK;
 }
@@ -648,8 +658,10 @@ int sim_koopman_bilinear_step(sim_koopman* k, int n, const double* z0, const dou
   if (!k || !z0 || !window || !u_prev || !action || n < 0) return soarm_set_error(SIM_E_ARG, "bad argument");
   if (!k->d_A) return soarm_set_error(SIM_E_ARG, "sim_koopman_set_bilinear was not called");
   if (n == 0) return SIM_OK;
-  hipLaunchKernelGGL(k_bilinear, dim3((n + BL_EPW - 1) / BL_EPW), dim3(64 * BL_EPW),
-                     ((size_t)k->bd.per_env * BL_EPW + (size_t)k->bd.nz * k->bd.nz) * sizeof(double), (hipStream_t)stream,
+  const int ep = k->bd.epw;
+  auto kern = ep == 6 ? k_bilinear<6> : ep == 4 ? k_bilinear<4> : ep == 2 ? k_bilinear<2> : k_bilinear<1>;
+  hipLaunchKernelGGL(kern, dim3((n + ep - 1) / ep), dim3(64 * ep),
+                     ((size_t)k->bd.per_env * ep + (size_t)k->bd.nz * k->bd.nz) * sizeof(double), (hipStream_t)stream,
                      k->bd, k->d_A, k->d_B,
                      k->d_HhT, n, z0, window, u_prev, action);
   KCHECK(hipGetLastError());
