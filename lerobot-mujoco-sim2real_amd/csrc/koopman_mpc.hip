@@ -274,6 +274,7 @@ struct BDev {
   int nz, nu, H, N, delta, per_env;  // per_env: doubles of LDS per env
   int epw;                           // envs (waves) per workgroup
   int xreg;                          // doubles of the X / packed-Hessian region
+  int greg;                          // doubles of the packed Gram (>= 64: it is the Cholesky's column buffer after)
   double q, r, uclip;
 };
 // a double of lane l (l wave-uniform) in every lane: two v_readlane
@@ -304,6 +305,19 @@ DEVI double dotn(const double* x, int sx, const double* y, int len) {
   for (; j < len; j++) s0 = fma(x[j * sx], y[j], s0);
   return (s0 + s1) + (s2 + s3);
 }
+#ifdef SOARM_BL_PROF
+// diagnostic build: per phase of k_bilinear, summed wave cycles ([0..7]) and waves ([8])
+__device__ unsigned long long g_bl[9];
+#define BL_STAMP(k)                                                                  \
+  {                                                                                  \
+    const long long t_ = clock64();                                                  \
+    if ((k) > 0 && lane == 0) atomicAdd(&g_bl[(k) - 1], (unsigned long long)(t_ - bl_t)); \
+    if ((k) == 8 && lane == 0) atomicAdd(&g_bl[8], 1ull);                            \
+    bl_t = t_;                                                                       \
+  }
+#else
+#define BL_STAMP(k)
+#endif
 template <int EPW>
 __global__ __launch_bounds__(64 * EPW) void k_bilinear(BDev K, const double* __restrict__ A,
                                                           const double* __restrict__ Bm,
@@ -314,17 +328,22 @@ __global__ __launch_bounds__(64 * EPW) void k_bilinear(BDev K, const double* __r
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int e = blockIdx.x * EPW + w;
+#ifdef SOARM_BL_PROF
+  long long bl_t = 0;
+#endif
   const int nz = K.nz, nu = K.nu, H = K.H, N = K.N, zu = nz * nu;
-  // A, shared by the workgroup's envs: every product with A reads it from LDS (a global read in
-  // each step of a dependent FMA chain costs the latency of the cache hierarchy per step)
+  // A, shared by the workgroup's envs, rows padded to an odd stride (nz + 1 doubles): lanes reading
+  // one element of different rows hit different banks (a 256-B stride puts them all on one)
+  const int as = nz + 1;
   double* As = lds + (size_t)EPW * K.per_env;
-  for (int i = threadIdx.x; i < nz * nz; i += blockDim.x) As[i] = A[i];
+  for (int i = threadIdx.x; i < nz * nz; i += blockDim.x) As[(i / nz) * as + (i % nz)] = A[i];
   __syncthreads();
   if (e >= n) return;  // (whole waves: no workgroup barrier below)
+  BL_STAMP(0);
   double* X = lds + (size_t)w * K.per_env;  // [H][zu]; later the packed Hessian (N (N + 1) / 2)
   double* M = X + K.xreg;                   // [zu]
   double* G = M + zu;                       // Gram of the stacked X_k, packed lower (N (N + 1) / 2)
-  double* zb = G + N * (N + 1) / 2;         // [nz]: z0, then A^t z0
+  double* zb = G + K.greg;                  // [nz]: z0, then A^t z0
   double* eb = zb + nz;                     // [nz]: e_t
   for (int i = lane; i < nz; i += 64) zb[i] = z0g[(size_t)i * n + e];
   double up[8];
@@ -337,36 +356,47 @@ __global__ __launch_bounds__(64 * EPW) void k_bilinear(BDev K, const double* __r
     M[o] = s, X[o] = s;
   }
   wsync();
-  // M_k = A M_{k-1}; X_k = M_k or X_{k-1} + M_k  (zu <= 512: 8 outputs per lane)
-  for (int k = 1; k < H; k++) {
-    double nm[8];
+  BL_STAMP(1);
+  // M_k = A M_{k-1}; X_k = M_k or X_{k-1} + M_k, on the f64 MFMA: A's 16-row tiles (A fragment:
+  // lane l holds A[16 t + (l & 15)][4 ks + (l >> 4)]) times M_{k-1} padded to 16 columns (B: lane l
+  // holds M[4 ks + (l >> 4)][l & 15]); C: lane l, register r = row 16 t + (l >> 4) + 4 r, column l & 15
+  {
+    const int NTz = (nz + 15) >> 4, KSz = (nz + 3) >> 2, fr = lane >> 4, fc = lane & 15;
+    for (int k = 1; k < H; k++) {
+      d4 acc[4];
 #pragma unroll
-    for (int q = 0; q < 8; q++) {
-      const int o = lane + 64 * q;
-      nm[q] = 0.0;
-      if (o < zu) {
-        const int i = o / nu, c = o - i * nu;
-        nm[q] = dotn(M + c, nu, As + i * nz, nz);
-      }
-    }
-    wsync();  // (every lane has read M_{k-1})
+      for (int t = 0; t < 4; t++) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
+      for (int ks = 0; ks < KSz; ks++) {
+        const int jr = 4 * ks + fr;
+        const double bm = (jr < nz && fc < nu) ? M[jr * nu + fc] : 0.0;
 #pragma unroll
-    for (int q = 0; q < 8; q++) {
-      const int o = lane + 64 * q;
-      if (o < zu) {
-        M[o] = nm[q];
-        X[k * zu + o] = K.delta ? X[(k - 1) * zu + o] + nm[q] : nm[q];
+        for (int t = 0; t < 4; t++) {
+          const int ar = 16 * t + fc;
+          if (t < NTz) acc[t] = mfma((ar < nz && jr < nz) ? As[ar * as + jr] : 0.0, bm, acc[t]);
+        }
       }
+      wsync();  // (every lane has read M_{k-1})
+#pragma unroll
+      for (int t = 0; t < 4; t++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int row = 16 * t + fr + 4 * r, o = row * nu + fc;
+          if (t < NTz && row < nz && fc < nu) {
+            M[o] = acc[t][r];
+            X[k * zu + o] = K.delta ? X[(k - 1) * zu + o] + acc[t][r] : acc[t][r];
+          }
+        }
+      wsync();
     }
-    wsync();
   }
+  BL_STAMP(2);
   // rhs (lane l = s nu + c): e_t = ref_t - A^{t+1} z0 - [delta] C_t u_prev, rhs[s] += q X_{t-s}' e_t
   // (before the Hessian: the packed Hessian overwrites X's storage)
   double rhs = 0.0;
   const int ls = lane / nu, lc = lane - ls * nu;
   for (int t = 0; t < H; t++) {
     double yn = 0.0;
-    if (lane < nz) yn = dotn(zb, 1, As + lane * nz, nz);
+    if (lane < nz) yn = dotn(zb, 1, As + lane * as, nz);
     wsync();
     if (lane < nz) {
       zb[lane] = yn;
@@ -384,6 +414,7 @@ __global__ __launch_bounds__(64 * EPW) void k_bilinear(BDev K, const double* __r
     }
     wsync();
   }
+  BL_STAMP(3);
   // Gram G[a][b] = sum_i X[i][a] X[i][b] over the N = H nu columns a = k nu + c of the stacked X_k
   // (rows i < nz), on the f64 MFMA: the A fragment of (tile t, k-step ks) -- lane l holds
   // X[4 ks + (l >> 4)][16 t + (l & 15)] -- is also the B fragment of (t, ks), so 4 fragment loads
@@ -420,6 +451,7 @@ __global__ __launch_bounds__(64 * EPW) void k_bilinear(BDev K, const double* __r
         }
   }
   wsync();
+  BL_STAMP(4);
   // Hessian, packed lower into X's storage (P[R (R + 1) / 2 + C], R >= C): one lane per block
   // diagonal d and (c1, c2); Hess[(s1, c1)][(s1 + d, c2)] = q sum_{b <= H-1-s1-d} W[b + d][b](c1, c2)
   // + r [d = 0, c1 = c2], W[k1][k2](c1, c2) = G[k1 nu + c1][k2 nu + c2], a running sum over b
@@ -441,44 +473,53 @@ __global__ __launch_bounds__(64 * EPW) void k_bilinear(BDev K, const double* __r
     }
   }
   wsync();
-  // Cholesky P = L L' in place (packed lower, right-looking).  Lane l keeps 1 / L[l][l].  The
-  // trailing update is spread over the lanes by packed pair index p = (ii, kk), ii >= kk: lane l
-  // walks p = l, l + 64, ... from its own start (ii0, kk0), advanced incrementally (no sqrt)
-  int ii0 = 0, kk0 = lane;
-  while (kk0 > ii0) kk0 -= ii0 + 1, ii0++;
+  BL_STAMP(5);
+  // Cholesky Hess = L L' with the rows in registers: lane i holds row i (compile-time column
+  // index, N <= 64), right-looking; column j of L goes through LDS (G's storage) and
+  // every lane reads it with same-address broadcasts.  Lane l keeps 1 / L[l][l].  (The entries
+  // right of a lane's diagonal take junk updates and are never read.)
+  double row[64];
+#pragma unroll
+  for (int k = 0; k < 64; k++) row[k] = (lane < N && k <= lane) ? P[lane * (lane + 1) / 2 + k] : 0.0;
   double idg = 0.0;
-  for (int j = 0; j < N; j++) {
-    const int jj = j * (j + 1) / 2;
-    const double dj = sqrt(P[jj + j]), id = 1.0 / dj;
-    wsync();
-    if (lane == j) idg = id;
-    const int i1 = j + 1 + lane;
-    if (i1 < N) P[i1 * (i1 + 1) / 2 + j] *= id;
-    if (lane == 0) P[jj + j] = dj;
-    wsync();
-    const int m = N - j - 1, np = m * (m + 1) / 2;
-    int ii = ii0, kk = kk0;
-    for (int p = lane; p < np; p += 64) {
-      const int i = j + 1 + ii, k2 = j + 1 + kk;
-      const int ri = i * (i + 1) / 2;
-      P[ri + k2] = fma(-P[ri + j], P[k2 * (k2 + 1) / 2 + j], P[ri + k2]);
-      kk += 64;
-      while (kk > ii) kk -= ii + 1, ii++;
+  double* colb = G;  // (64 doubles: the Gram is dead once the Hessian is built)
+#pragma unroll
+  for (int j = 0; j < 64; j++) {
+    if (j < N) {
+      const double ljj = sqrt(rdlane(row[j], j)), inv = 1.0 / ljj;
+      const double lij = lane > j ? row[j] * inv : (lane == j ? ljj : 0.0);
+      row[j] = lij;
+      if (lane == j) idg = inv;
+      colb[lane] = lij;
+      wsync();
+#pragma unroll
+      for (int k = j + 1; k < 64; k++)
+        if (k < N) row[k] = fma(-lij, colb[k], row[k]);
+      wsync();
     }
-    wsync();
   }
-  // L y = rhs, L' v = y: lane i holds row i's value; the pivot's comes by readlane
+  BL_STAMP(6);
+  // L y = rhs from the register rows; then L' v = y from L written back (packed): lane i reads
+  // row j's entry i, contiguous over the lanes.  Pivot values by readlane.
   double y = rhs;
-  for (int j = 0; j < N; j++) {
-    const double yj = rdlane(y, j) * rdlane(idg, j);
-    if (lane == j) y = yj;
-    if (lane > j && lane < N) y = fma(-P[lane * (lane + 1) / 2 + j], yj, y);
+#pragma unroll
+  for (int j = 0; j < 64; j++) {
+    if (j < N) {
+      const double yj = rdlane(y, j) * rdlane(idg, j);
+      if (lane == j) y = yj;
+      if (lane > j && lane < N) y = fma(-row[j], yj, y);
+    }
   }
+#pragma unroll
+  for (int k = 0; k < 64; k++)
+    if (lane < N && k <= lane) P[lane * (lane + 1) / 2 + k] = row[k];
+  wsync();
   for (int j = N - 1; j >= 0; j--) {
     const double vj = rdlane(y, j) * rdlane(idg, j);
     if (lane == j) y = vj;
     if (lane < j) y = fma(-P[j * (j + 1) / 2 + lane], vj, y);
   }
+  BL_STAMP(7);
   if (lane < nu) {  // u0 = v_0 + u_prev (get_control, MPC_Controler.py:147-149)
     double upl = 0.0;
 #pragma unroll
@@ -487,6 +528,7 @@ __global__ __launch_bounds__(64 * EPW) void k_bilinear(BDev K, const double* __r
     uprev[(size_t)lane * n + e] = u0;
     action[(size_t)e * nu + lane] = (float)fmin(fmax(u0, -K.uclip), K.uclip);
   }
+  BL_STAMP(8);
 }
 
 typedef void (*EncodeFn)(KDev, const double*, int, const float*, double*);
@@ -514,6 +556,19 @@ struct sim_koopman {
   } while (0)
 
 extern "C" {
+
+#ifdef SOARM_BL_PROF
+// diagnostic build only: the k_bilinear phase cycles (9 values), reset after reading
+int sim_koopman_bl_profile(double* out) {
+  unsigned long long h[9];
+  KCHECK(hipDeviceSynchronize());
+  KCHECK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_bl), sizeof(h)));
+  for (int k = 0; k < 9; k++) out[k] = (double)h[k];
+  const unsigned long long z[9] = {};
+  KCHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_bl), z, sizeof(z)));
+  return 0;
+}
+#endif
 
 int sim_koopman_create(const sim_koopman_desc* d, const double* weights, const double* gain, int device,
                        sim_koopman** out) {
@@ -627,11 +682,12 @@ int sim_koopman_set_bilinear(sim_koopman* k, const double* A, const double* B, c
   BDev b{};
   b.nz = nz, b.nu = nu, b.H = H, b.N = N, b.delta = delta ? 1 : 0, b.q = q, b.r = r, b.uclip = k->kd.uclip;
   b.xreg = std::max(H * nz * nu, N * (N + 1) / 2);
-  b.per_env = (b.xreg + nz * nu + N * (N + 1) / 2 + 2 * nz + 1) & ~1;
+  b.greg = std::max(N * (N + 1) / 2, 64);
+  b.per_env = (b.xreg + nz * nu + b.greg + 2 * nz + 1) & ~1;
   // as many envs per workgroup as fit the CU's LDS with A (6 at nz 32, nu 5, H 10: 157 KB)
   b.epw = 0;
   for (int ep : {6, 4, 2, 1})
-    if (!b.epw && ((size_t)b.per_env * ep + (size_t)nz * nz) * 8 <= 160 * 1024) b.epw = ep;
+    if (!b.epw && ((size_t)b.per_env * ep + (size_t)nz * (nz + 1)) * 8 <= 160 * 1024) b.epw = ep;
   if (!b.epw) return soarm_set_error(SIM_E_MODEL, "bilinear MPC does not fit in LDS");
   std::vector<double> hht((size_t)nz * nu * nz);
   for (int j = 0; j < nz; j++)
@@ -661,7 +717,7 @@ int sim_koopman_bilinear_step(sim_koopman* k, int n, const double* z0, const dou
   const int ep = k->bd.epw;
   auto kern = ep == 6 ? k_bilinear<6> : ep == 4 ? k_bilinear<4> : ep == 2 ? k_bilinear<2> : k_bilinear<1>;
   hipLaunchKernelGGL(kern, dim3((n + ep - 1) / ep), dim3(64 * ep),
-                     ((size_t)k->bd.per_env * ep + (size_t)k->bd.nz * k->bd.nz) * sizeof(double), (hipStream_t)stream,
+                     ((size_t)k->bd.per_env * ep + (size_t)k->bd.nz * (k->bd.nz + 1)) * sizeof(double), (hipStream_t)stream,
                      k->bd, k->d_A, k->d_B,
                      k->d_HhT, n, z0, window, u_prev, action);
   KCHECK(hipGetLastError());
