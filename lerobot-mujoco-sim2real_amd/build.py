@@ -51,14 +51,12 @@ def _stale():
     return not os.path.exists(LIB_PATH) or built_hash() != source_hash()
 
 
-def build(force=False, verbose=False):
-    """Build csrc/libsoarm_sim.so if missing or built from other sources."""
-    if not force and not _stale():
-        return LIB_PATH
-    want = source_hash()
-    tmp = f"{LIB_PATH}.{os.getpid()}.tmp"
-    # one object per translation unit, compiled concurrently, then one link
-    cflags = [f for f in FLAGS if f != "-shared"]
+def compile_lib(out, defines=(), verbose=False):
+    """Compile every translation unit (concurrently) and link `out`; defines: extra -D flags
+    (the diagnostic builds of tools/phase_prof.py and tools/bl_prof.py)."""
+    out = os.path.abspath(out)  # (hipcc runs in csrc/)
+    tmp = f"{out}.{os.getpid()}.tmp"
+    cflags = [f for f in FLAGS if f != "-shared"] + list(defines)
     objs, procs = [], []
     for src in SOURCES:
         obj = f"{tmp}.{os.path.splitext(src)[0]}.o"
@@ -80,7 +78,16 @@ def build(force=False, verbose=False):
         for o in objs:
             if os.path.exists(o):
                 os.remove(o)
-    os.replace(tmp, LIB_PATH)  # atomic: concurrent loaders never see a partial file
+    os.replace(tmp, out)  # atomic: concurrent loaders never see a partial file
+    return out
+
+
+def build(force=False, verbose=False):
+    """Build csrc/libsoarm_sim.so if missing or built from other sources."""
+    if not force and not _stale():
+        return LIB_PATH
+    want = source_hash()
+    compile_lib(LIB_PATH, verbose=verbose)
     with open(STAMP + f".{os.getpid()}.tmp", "w") as f:
         f.write(want + "\n")
     os.replace(STAMP + f".{os.getpid()}.tmp", STAMP)

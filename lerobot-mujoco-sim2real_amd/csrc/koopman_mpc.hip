@@ -362,17 +362,40 @@ __global__ __launch_bounds__(64 * EPW) void k_bilinear(BDev K, const double* __r
   // holds M[4 ks + (l >> 4)][l & 15]); C: lane l, register r = row 16 t + (l >> 4) + 4 r, column l & 15
   {
     const int NTz = (nz + 15) >> 4, KSz = (nz + 3) >> 2, fr = lane >> 4, fc = lane & 15;
+    // A's fragments for nz <= 32 (2 row tiles x 8 k-steps) stay in registers across the H steps
+    double af[2][8];
+#pragma unroll
+    for (int t = 0; t < 2; t++)
+#pragma unroll
+      for (int ks = 0; ks < 8; ks++) {
+        const int ar = 16 * t + fc, jr = 4 * ks + fr;
+        af[t][ks] = (ar < nz && jr < nz) ? As[ar * as + jr] : 0.0;
+      }
     for (int k = 1; k < H; k++) {
       d4 acc[4];
 #pragma unroll
       for (int t = 0; t < 4; t++) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
-      for (int ks = 0; ks < KSz; ks++) {
-        const int jr = 4 * ks + fr;
-        const double bm = (jr < nz && fc < nu) ? M[jr * nu + fc] : 0.0;
+      if (nz <= 32) {
+        double bm[8];
 #pragma unroll
-        for (int t = 0; t < 4; t++) {
-          const int ar = 16 * t + fc;
-          if (t < NTz) acc[t] = mfma((ar < nz && jr < nz) ? As[ar * as + jr] : 0.0, bm, acc[t]);
+        for (int ks = 0; ks < 8; ks++) {
+          const int jr = 4 * ks + fr;
+          bm[ks] = (jr < nz && fc < nu) ? M[jr * nu + fc] : 0.0;
+        }
+#pragma unroll
+        for (int ks = 0; ks < 8; ks++) {
+          acc[0] = mfma(af[0][ks], bm[ks], acc[0]);
+          if (NTz > 1) acc[1] = mfma(af[1][ks], bm[ks], acc[1]);
+        }
+      } else {
+        for (int ks = 0; ks < KSz; ks++) {
+          const int jr = 4 * ks + fr;
+          const double bm = (jr < nz && fc < nu) ? M[jr * nu + fc] : 0.0;
+#pragma unroll
+          for (int t = 0; t < 4; t++) {
+            const int ar = 16 * t + fc;
+            if (t < NTz) acc[t] = mfma((ar < nz && jr < nz) ? As[ar * as + jr] : 0.0, bm, acc[t]);
+          }
         }
       }
       wsync();  // (every lane has read M_{k-1})

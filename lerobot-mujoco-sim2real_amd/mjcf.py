@@ -287,11 +287,11 @@ def _load_hulls(path=None):
 def compile_mjcf(xml_path=SCENE_XML, kv=None, disable_contact=False, iterations=100,
                  tolerance=1e-8, obs_site="gripperframe",
                  obs_joints=("shoulder_pan", "shoulder_lift", "elbow_flex", "wrist_flex", "wrist_roll"),
-                 solver="PGS", ccd="mpr"):
+                 solver="PGS", ccd="native"):
     """Compile an MJCF file into a :class:`CompiledModel`.
 
     ccd: the convex-convex narrowphase, "native" (MuJoCo's GJK/EPA, the default of current
-    releases) or "mpr" (libccd MPR, MuJoCo's classic path); an explicit
+    releases, and so this compiler's) or "mpr" (libccd MPR, MuJoCo's classic path); an explicit
     ``<option><flag nativeccd="disable"/></option>`` in the MJCF selects MPR.
 
     solver: "PGS" (the north star's and BASELINE config 3's solver, the headline) or "Newton"

@@ -173,8 +173,7 @@ def test_contacts_match_oracle(gpu_lib, arm_model, cube_model, ccd):
     Both convex-convex narrowphases: libccd MPR and MuJoCo's native GJK/EPA (kernel vs oracle)."""
     import torch
     from lerobot_mujoco_sim2real_amd import mjcf
-    models = (arm_model, cube_model) if ccd == "mpr" else \
-        (mjcf.compile_mjcf(mjcf.SCENE_XML, ccd="native"), mjcf.compile_mjcf(mjcf.CUBE_SCENE_XML, ccd="native"))
+    models = (mjcf.compile_mjcf(mjcf.SCENE_XML, ccd=ccd), mjcf.compile_mjcf(mjcf.CUBE_SCENE_XML, ccd=ccd))
     for cm in models:
         assert cm.desc.ccd == (1 if ccd == "native" else 0)
         n = 512

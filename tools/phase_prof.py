@@ -18,10 +18,10 @@ SRC = os.path.join(ROOT, "lerobot-mujoco-sim2real_amd", "csrc", "soarm_sim.hip")
 if "--build" in sys.argv:
     sys.path.insert(0, ROOT)
     import soarm_pkg  # noqa: F401
-    from lerobot_mujoco_sim2real_amd.build import FLAGS, HIPCC, SOURCES, SRC_DIR
+    from lerobot_mujoco_sim2real_amd.build import compile_lib
 
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
-    subprocess.check_call([HIPCC] + FLAGS + ["-DSOARM_PHASE_PROF"] + [a for a in sys.argv[1:] if a.startswith("-D")] + ["-o", LIB] + [os.path.join(SRC_DIR, f) for f in SOURCES])
+    compile_lib(LIB, ["-DSOARM_PHASE_PROF"] + [a for a in sys.argv[1:] if a.startswith("-D")])
     sys.exit(0)
 
 sys.path.insert(0, ROOT)
