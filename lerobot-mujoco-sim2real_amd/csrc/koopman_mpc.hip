@@ -31,6 +31,7 @@ int soarm_set_error(int code, const std::string& msg);  // soarm_sim.hip (sim_la
 namespace {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
+typedef double d2 __attribute__((ext_vector_type(2)));
 
 constexpr int KT = SIM_KMAXW / 16;  // 16-row tiles of a layer's output (4)
 
@@ -261,20 +262,27 @@ __global__ __launch_bounds__(256) void k_feedforward(KDev K, const double* __res
 //   M_0 = B_total, M_k = A M_{k-1}; X_k = M_k ('mpc') or C_k = sum_{i<=k} M_i ('delta_mpc')
 //     (A staged in LDS once per workgroup);
 //   rhs[s] = q sum_{t >= s} X_{t-s}' e_t, e_t = ref_t - A^{t+1} z0 - [delta] C_t u_prev;
-//   G = Xs' Xs, the Gram of the stacked X_k (N = H nu columns, nz rows) on the f64 MFMA;
+//   G = Xs' Xs, the Gram of the stacked X_k (N = H nu columns, nz rows) on the f64 MFMA, in
+//     registers until every X_k is read, then stored packed lower over X's storage;
 //   Hess[s1][s2] = q sum_{t >= max(s1,s2)} X_{t-s1}' X_{t-s2} + r I -- along each block diagonal
-//     d = s2 - s1 a running sum of G's blocks W[b+d][b] (one lane per (d, c1, c2)), packed lower;
-//   v = Hess^-1 rhs by an in-LDS Cholesky (right-looking; the trailing update spread over the
-//   wave's lanes by packed pair index) and two triangular solves (pivots by readlane);
+//     a prefix sum of G's blocks: with the block order reversed, flip(s nu + c) = (H-1-s) nu + c,
+//     Hess[flip a][flip b] = q sum_{b' <= b} G[b' + a - b][b'] (blocks a >= b), so the prefix sums
+//     overwrite G in place (one lane per block diagonal and (c1, c2)) and leave
+//     P = Pi Hess Pi' packed lower, Pi the block reversal;
+//   P v' = Pi rhs by a Cholesky with the rows in registers, a forward solve and the first nu steps
+//   of the back substitution (pivots by readlane): v_0 = v'_{(H-1) nu + c} comes first there;
 //   u0 = v_0 + u_prev, action = clip(u0).
-// Shapes: nz <= 64, nu <= 8, N = H nu <= 64.  Per env LDS: the X region (X [H][nz*nu], later the
-// packed Hessian), M [nz*nu], G packed, y / e [nz] each (24.8 KB at nz 32, nu 5, H 10); up to
-// 6 envs (waves) per workgroup, or as many as the LDS holds with A [nz][nz].
+// Shapes: nz <= 64, nu <= 8, N = H nu <= 64.  Per env LDS: the X region (X [H][nz*nu], later G
+// and P), M [nz*nu] (later the Cholesky's column buffer, >= 256 doubles), y / e [nz] each
+// (15.3 KB at nz 32, nu 5, H 10); up to 8 envs (waves) per workgroup, or as many as the LDS holds
+// with A [nz][nz].
 struct BDev {
   int nz, nu, H, N, delta, per_env;  // per_env: doubles of LDS per env
   int epw;                           // envs (waves) per workgroup
-  int xreg;                          // doubles of the X / packed-Hessian region
-  int greg;                          // doubles of the packed Gram (>= 64: it is the Cholesky's column buffer after)
+  int xreg;                          // doubles of the X / Gram / packed-Hessian region
+  int xs;                            // X_k's stride (>= nz nu, = nu mod 32: the rhs phase's lanes
+                                     // (X_{t-s} column c) then fall in distinct LDS banks)
+  int mreg;                          // doubles of M (>= 256: the Cholesky's column buffer after)
   double q, r, uclip;
 };
 // a double of lane l (l wave-uniform) in every lane: two v_readlane
@@ -331,7 +339,7 @@ __global__ __launch_bounds__(64 * EPW) void k_bilinear(BDev K, const double* __r
 #ifdef SOARM_BL_PROF
   long long bl_t = 0;
 #endif
-  const int nz = K.nz, nu = K.nu, H = K.H, N = K.N, zu = nz * nu;
+  const int nz = K.nz, nu = K.nu, H = K.H, N = K.N, zu = nz * nu, xs = K.xs;
   // A, shared by the workgroup's envs, rows padded to an odd stride (nz + 1 doubles): lanes reading
   // one element of different rows hit different banks (a 256-B stride puts them all on one)
   const int as = nz + 1;
@@ -340,22 +348,53 @@ __global__ __launch_bounds__(64 * EPW) void k_bilinear(BDev K, const double* __r
   __syncthreads();
   if (e >= n) return;  // (whole waves: no workgroup barrier below)
   BL_STAMP(0);
-  double* X = lds + (size_t)w * K.per_env;  // [H][zu]; later the packed Hessian (N (N + 1) / 2)
-  double* M = X + K.xreg;                   // [zu]
-  double* G = M + zu;                       // Gram of the stacked X_k, packed lower (N (N + 1) / 2)
-  double* zb = G + K.greg;                  // [nz]: z0, then A^t z0
+  double* X = lds + (size_t)w * K.per_env;  // [H][xs]; later G and P, packed lower (N (N + 1) / 2)
+  double* M = X + K.xreg;                   // [zu]; later the Cholesky's column buffer
+  double* zb = M + K.mreg;                  // [nz]: z0, then A^t z0
   double* eb = zb + nz;                     // [nz]: e_t
   for (int i = lane; i < nz; i += 64) zb[i] = z0g[(size_t)i * n + e];
   double up[8];
 #pragma unroll
   for (int c = 0; c < 8; c++) up[c] = c < nu ? uprev[(size_t)c * n + e] : 0.0;
   wsync();
-  // B_total = B + sum_j z0_j Hhat_j  (HhT [(i nu + c)][j])
+  // B_total = B + sum_j z0_j Hhat_j  (HhT [(i nu + c)][j]); for nz <= 32 a row's loads are all
+  // issued before the FMAs (the same four chains, in the same order, as dotn)
   for (int o = lane; o < zu; o += 64) {
-    const double s = Bm[o] + dotn(HhT + (size_t)o * nz, 1, zb, nz);
+    const double* hr = HhT + (size_t)o * nz;
+    double d;
+    if (nz <= 32) {
+      double h[32];
+#pragma unroll
+      for (int j = 0; j < 32; j++) h[j] = hr[min(j, nz - 1)];
+      double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+#pragma unroll
+      for (int j = 0; j < 32; j += 4)
+        if (j + 4 <= nz) {
+          s0 = fma(h[j], zb[j], s0);
+          s1 = fma(h[j + 1], zb[j + 1], s1);
+          s2 = fma(h[j + 2], zb[j + 2], s2);
+          s3 = fma(h[j + 3], zb[j + 3], s3);
+        }
+#pragma unroll
+      for (int j = 0; j < 32; j++)
+        if (j >= (nz & ~3) && j < nz) s0 = fma(h[j], zb[j], s0);
+      d = (s0 + s1) + (s2 + s3);
+    } else {
+      d = dotn(hr, 1, zb, nz);
+    }
+    const double s = Bm[o] + d;
     M[o] = s, X[o] = s;
   }
   wsync();
+  // the reference window of the first 16 frames (lane < nz; clamped addresses, no guarded loads),
+  // issued after B_total's loads so that its latency overlaps the M_k phase (no global loads there:
+  // the load counter is waited on in order)
+  double wv[16];
+  {
+    const int li = min(lane, nz - 1);
+#pragma unroll
+    for (int t = 0; t < 16; t++) wv[t] = win[((size_t)min(t, H - 1) * nz + li) * n + e];
+  }
   BL_STAMP(1);
   // M_k = A M_{k-1}; X_k = M_k or X_{k-1} + M_k, on the f64 MFMA: A's 16-row tiles (A fragment:
   // lane l holds A[16 t + (l & 15)][4 ks + (l >> 4)]) times M_{k-1} padded to 16 columns (B: lane l
@@ -406,43 +445,48 @@ __global__ __launch_bounds__(64 * EPW) void k_bilinear(BDev K, const double* __r
           const int row = 16 * t + fr + 4 * r, o = row * nu + fc;
           if (t < NTz && row < nz && fc < nu) {
             M[o] = acc[t][r];
-            X[k * zu + o] = K.delta ? X[(k - 1) * zu + o] + acc[t][r] : acc[t][r];
+            X[k * xs + o] = K.delta ? X[(k - 1) * xs + o] + acc[t][r] : acc[t][r];
           }
         }
       wsync();
     }
   }
   BL_STAMP(2);
-  // rhs (lane l = s nu + c): e_t = ref_t - A^{t+1} z0 - [delta] C_t u_prev, rhs[s] += q X_{t-s}' e_t
-  // (before the Hessian: the packed Hessian overwrites X's storage)
+  // rhs in the reversed order (lane a holds entry flip(a) = s nu + c, s = H-1 - a / nu):
+  // e_t = ref_t - A^{t+1} z0 - [delta] C_t u_prev, rhs[s] += q X_{t-s}' e_t
   double rhs = 0.0;
-  const int ls = lane / nu, lc = lane - ls * nu;
+  const int ls = H - 1 - lane / nu, lc = lane % nu;
   for (int t = 0; t < H; t++) {
     double yn = 0.0;
     if (lane < nz) yn = dotn(zb, 1, As + lane * as, nz);
+    double wt = 0.0;
+#pragma unroll
+    for (int s = 0; s < 16; s++) wt = s == t ? wv[s] : wt;
+    if (t >= 16 && lane < nz) wt = win[((size_t)t * nz + lane) * n + e];
     wsync();
     if (lane < nz) {
       zb[lane] = yn;
-      double ev = win[((size_t)t * nz + lane) * n + e] - yn;
+      double ev = wt - yn;
       if (K.delta) {
 #pragma unroll
         for (int c = 0; c < 8; c++)
-          if (c < nu) ev = fma(-X[t * zu + lane * nu + c], up[c], ev);
+          if (c < nu) ev = fma(-X[t * xs + lane * nu + c], up[c], ev);
       }
       eb[lane] = ev;
     }
     wsync();
     if (lane < N && ls <= t) {
-      rhs = fma(K.q, dotn(X + (t - ls) * zu + lc, nu, eb, nz), rhs);
+      rhs = fma(K.q, dotn(X + (t - ls) * xs + lc, nu, eb, nz), rhs);
     }
-    wsync();
+    // (no sync here: the next frame's first sync orders these reads of eb before its writes)
   }
   BL_STAMP(3);
   // Gram G[a][b] = sum_i X[i][a] X[i][b] over the N = H nu columns a = k nu + c of the stacked X_k
   // (rows i < nz), on the f64 MFMA: the A fragment of (tile t, k-step ks) -- lane l holds
   // X[4 ks + (l >> 4)][16 t + (l & 15)] -- is also the B fragment of (t, ks), so 4 fragment loads
   // per k-step feed the <= 10 lower tiles (ta >= tb); C: lane l, register r = row (l >> 4) + 4 r,
-  // column l & 15 of the tile.  Stored packed lower (row >= col).
+  // column l & 15 of the tile.  Stored packed lower (row >= col) over X, once every lane has read X.
+  double* G = X;
   {
     const int NT = (N + 15) >> 4, KS = (nz + 3) >> 2;
     d4 acc[10];
@@ -455,7 +499,7 @@ __global__ __launch_bounds__(64 * EPW) void k_bilinear(BDev K, const double* __r
 #pragma unroll
       for (int t = 0; t < 4; t++) {
         const int a = 16 * t + fc, k = a / nu;
-        fg[t] = (t < NT && a < N && i < nz) ? X[k * zu + i * nu + (a - k * nu)] : 0.0;
+        fg[t] = (t < NT && a < N && i < nz) ? X[k * xs + i * nu + (a - k * nu)] : 0.0;
       }
 #pragma unroll
       for (int ta = 0, q = 0; ta < 4; ta++)
@@ -463,6 +507,7 @@ __global__ __launch_bounds__(64 * EPW) void k_bilinear(BDev K, const double* __r
         for (int tb = 0; tb <= ta; tb++, q++)
           if (ta < NT) acc[q] = mfma(fg[ta], fg[tb], acc[q]);
     }
+    wsync();
 #pragma unroll
     for (int ta = 0, q = 0; ta < 4; ta++)
 #pragma unroll
@@ -475,55 +520,79 @@ __global__ __launch_bounds__(64 * EPW) void k_bilinear(BDev K, const double* __r
   }
   wsync();
   BL_STAMP(4);
-  // Hessian, packed lower into X's storage (P[R (R + 1) / 2 + C], R >= C): one lane per block
-  // diagonal d and (c1, c2); Hess[(s1, c1)][(s1 + d, c2)] = q sum_{b <= H-1-s1-d} W[b + d][b](c1, c2)
-  // + r [d = 0, c1 = c2], W[k1][k2](c1, c2) = G[k1 nu + c1][k2 nu + c2], a running sum over b
-  double* P = X;
+  // P = Pi Hess Pi' in place over G: lane (d, c1, c2) walks its block diagonal's entries
+  // (a1, a2) = ((b + d) nu + c1, b nu + c2), b = 0, 1, ... (a1 >= a2: d > 0, or c1 >= c2), keeps the
+  // running sum S of G there and writes q S + r [d = 0, c1 = c2] back.  Every entry has one owner.
+  double* P = G;
   for (int tr = lane; tr < H * nu * nu; tr += 64) {
     const int d = tr / (nu * nu), c1 = (tr / nu) % nu, c2 = tr % nu;
-    if (d == 0 && c1 < c2) continue;  // (its symmetric twin writes the element)
+    if (d == 0 && c1 < c2) continue;  // (upper triangle of a diagonal block: not stored)
+    const double rd = (d == 0 && c1 == c2) ? K.r : 0.0;
     double S = 0.0;
     for (int b = 0; b + d < H; b++) {
-      const int a1 = (b + d) * nu + c1, a2 = b * nu + c2;
-      S += a1 >= a2 ? G[a1 * (a1 + 1) / 2 + a2] : G[a2 * (a2 + 1) / 2 + a1];
-      const int s1 = H - 1 - b - d, s2 = s1 + d;
-      const int R = s2 * nu + c2, Cc = s1 * nu + c1;  // (d = 0: c1 >= c2, so R <= Cc there)
-      const double hv = K.q * S + ((d == 0 && c1 == c2) ? K.r : 0.0);
-      if (R >= Cc)
-        P[R * (R + 1) / 2 + Cc] = hv;
-      else
-        P[Cc * (Cc + 1) / 2 + R] = hv;
+      const int a1 = (b + d) * nu + c1, a2 = b * nu + c2, o = a1 * (a1 + 1) / 2 + a2;
+      S += G[o];
+      P[o] = fma(K.q, S, rd);
     }
   }
   wsync();
   BL_STAMP(5);
-  // Cholesky Hess = L L' with the rows in registers: lane i holds row i (compile-time column
-  // index, N <= 64), right-looking; column j of L goes through LDS (G's storage) and
-  // every lane reads it with same-address broadcasts.  Lane l keeps 1 / L[l][l].  (The entries
-  // right of a lane's diagonal take junk updates and are never read.)
+  // Cholesky P = L L' with the rows in registers: lane i holds row i (compile-time column index,
+  // N <= 64), in blocks of 4 columns.  Inside a block, column j is updated by the block's earlier
+  // columns with L[j][q] taken by readlane (uniform), then scaled by its pivot; the trailing
+  // columns k >= jb + 4 are updated once per block from the 4 columns put in LDS (M's storage),
+  // read as same-address broadcasts.  Every row entry sees the same FMAs in the same column order
+  // as the column-by-column right-looking form.  Pivots: 1/sqrt(d) from v_rsq_f64 and two Newton
+  // steps, L[j][j] = d / sqrt(d) by that.  Lane l keeps 1 / L[l][l].  (The entries right of a
+  // lane's diagonal take junk updates and are never read.)
   double row[64];
 #pragma unroll
   for (int k = 0; k < 64; k++) row[k] = (lane < N && k <= lane) ? P[lane * (lane + 1) / 2 + k] : 0.0;
   double idg = 0.0;
-  double* colb = G;  // (64 doubles: the Gram is dead once the Hessian is built)
+  double* colb = M;  // [64][4] (>= 256 doubles: M is dead once X is complete)
 #pragma unroll
-  for (int j = 0; j < 64; j++) {
-    if (j < N) {
-      const double ljj = sqrt(rdlane(row[j], j)), inv = 1.0 / ljj;
-      const double lij = lane > j ? row[j] * inv : (lane == j ? ljj : 0.0);
-      row[j] = lij;
-      if (lane == j) idg = inv;
-      colb[lane] = lij;
-      wsync();
+  for (int jb = 0; jb < 64; jb += 4) {
+    if (jb < N) {
+      double l[4];
 #pragma unroll
-      for (int k = j + 1; k < 64; k++)
-        if (k < N) row[k] = fma(-lij, colb[k], row[k]);
-      wsync();
+      for (int m = 0; m < 4; m++) {
+        const int j = jb + m;
+        l[m] = 0.0;
+        if (j < N) {
+          double v = row[j];
+#pragma unroll
+          for (int q = 0; q < m; q++) v = fma(-l[q], rdlane(l[q], j), v);
+          const double dj = rdlane(v, j);
+          double y = __builtin_amdgcn_rsq(dj);
+          y = fma(0.5 * y, fma(-(dj * y), y, 1.0), y);
+          y = fma(0.5 * y, fma(-(dj * y), y, 1.0), y);
+          l[m] = lane > j ? v * y : (lane == j ? dj * y : 0.0);
+          row[j] = l[m];
+          if (lane == j) idg = y;
+        }
+      }
+      if (jb + 4 < N) {
+        *(d2*)(colb + 4 * lane) = d2{l[0], l[1]};
+        *(d2*)(colb + 4 * lane + 2) = d2{l[2], l[3]};
+        wsync();
+#pragma unroll
+        for (int k = jb + 4; k < 64; k++)
+          if (k < N) {
+            const d2 c01 = *(const d2*)(colb + 4 * k), c23 = *(const d2*)(colb + 4 * k + 2);
+            double v = fma(-l[0], c01[0], row[k]);
+            v = fma(-l[1], c01[1], v);
+            v = fma(-l[2], c23[0], v);
+            row[k] = fma(-l[3], c23[1], v);
+          }
+        wsync();
+      }
     }
   }
   BL_STAMP(6);
-  // L y = rhs from the register rows; then L' v = y from L written back (packed): lane i reads
-  // row j's entry i, contiguous over the lanes.  Pivot values by readlane.
+  // L y = rhs from the register rows; then L' v' = y, of which only v'_a, a >= N - nu, is wanted
+  // (u0's entries, in the reversed order): those are the back substitution's first nu steps, so
+  // only rows a >= N - nu of L go back to LDS (lane i reads row j's entry i, contiguous over the
+  // lanes).  Pivot values by readlane.
   double y = rhs;
 #pragma unroll
   for (int j = 0; j < 64; j++) {
@@ -533,23 +602,25 @@ __global__ __launch_bounds__(64 * EPW) void k_bilinear(BDev K, const double* __r
       if (lane > j && lane < N) y = fma(-row[j], yj, y);
     }
   }
+  const int a0 = N - nu;
 #pragma unroll
   for (int k = 0; k < 64; k++)
-    if (lane < N && k <= lane) P[lane * (lane + 1) / 2 + k] = row[k];
+    if (lane < N && k <= lane && k >= a0) P[lane * (lane + 1) / 2 + k] = row[k];
   wsync();
-  for (int j = N - 1; j >= 0; j--) {
+  for (int j = N - 1; j >= a0; j--) {
     const double vj = rdlane(y, j) * rdlane(idg, j);
     if (lane == j) y = vj;
-    if (lane < j) y = fma(-P[j * (j + 1) / 2 + lane], vj, y);
+    if (lane >= a0 && lane < j) y = fma(-P[j * (j + 1) / 2 + lane], vj, y);
   }
   BL_STAMP(7);
-  if (lane < nu) {  // u0 = v_0 + u_prev (get_control, MPC_Controler.py:147-149)
+  const int c0 = lane - a0;  // v_0's entry c sits in lane flip(c) = (H-1) nu + c
+  if (c0 >= 0 && c0 < nu) {  // u0 = v_0 + u_prev (get_control, MPC_Controler.py:147-149)
     double upl = 0.0;
 #pragma unroll
-    for (int c = 0; c < 8; c++) upl = lane == c ? up[c] : upl;
+    for (int c = 0; c < 8; c++) upl = c0 == c ? up[c] : upl;
     const double u0 = y + upl;
-    uprev[(size_t)lane * n + e] = u0;
-    action[(size_t)e * nu + lane] = (float)fmin(fmax(u0, -K.uclip), K.uclip);
+    uprev[(size_t)c0 * n + e] = u0;
+    action[(size_t)e * nu + c0] = (float)fmin(fmax(u0, -K.uclip), K.uclip);
   }
   BL_STAMP(8);
 }
@@ -704,12 +775,14 @@ int sim_koopman_set_bilinear(sim_koopman* k, const double* A, const double* B, c
   if (!(q > 0.0) || !(r > 0.0)) return soarm_set_error(SIM_E_ARG, "bilinear MPC: q and r must be positive");
   BDev b{};
   b.nz = nz, b.nu = nu, b.H = H, b.N = N, b.delta = delta ? 1 : 0, b.q = q, b.r = r, b.uclip = k->kd.uclip;
-  b.xreg = std::max(H * nz * nu, N * (N + 1) / 2);
-  b.greg = std::max(N * (N + 1) / 2, 64);
-  b.per_env = (b.xreg + nz * nu + b.greg + 2 * nz + 1) & ~1;
-  // as many envs per workgroup as fit the CU's LDS with A (6 at nz 32, nu 5, H 10: 157 KB)
+  b.xs = nz * nu + ((nu - nz * nu) % 32 + 32) % 32;
+  b.xreg = (std::max(H * b.xs, N * (N + 1) / 2) + 1) & ~1;  // (even: M's column buffer is read as 16-B pairs)
+  b.mreg = std::max(nz * nu, 256);
+  b.per_env = (b.xreg + b.mreg + 2 * nz + 1) & ~1;
+  // as many envs per workgroup as fit the CU's LDS with A (8 at nz 32, nu 5, H 10: 125 KB; the
+  // kernel's 215 VGPRs allow 2 waves per SIMD, so 8 is also the register limit)
   b.epw = 0;
-  for (int ep : {6, 4, 2, 1})
+  for (int ep : {8, 6, 4, 2, 1})
     if (!b.epw && ((size_t)b.per_env * ep + (size_t)nz * (nz + 1)) * 8 <= 160 * 1024) b.epw = ep;
   if (!b.epw) return soarm_set_error(SIM_E_MODEL, "bilinear MPC does not fit in LDS");
   std::vector<double> hht((size_t)nz * nu * nz);
@@ -725,8 +798,8 @@ int sim_koopman_set_bilinear(sim_koopman* k, const double* A, const double* B, c
   KCHECK(hipMemcpy(k->d_A, A, (size_t)nz * nz * 8, hipMemcpyHostToDevice));
   KCHECK(hipMemcpy(k->d_B, B, (size_t)nz * nu * 8, hipMemcpyHostToDevice));
   KCHECK(hipMemcpy(k->d_HhT, hht.data(), hht.size() * 8, hipMemcpyHostToDevice));
-  for (const void* f : {(const void*)k_bilinear<6>, (const void*)k_bilinear<4>, (const void*)k_bilinear<2>,
-                        (const void*)k_bilinear<1>})
+  for (const void* f : {(const void*)k_bilinear<8>, (const void*)k_bilinear<6>, (const void*)k_bilinear<4>,
+                        (const void*)k_bilinear<2>, (const void*)k_bilinear<1>})
     KCHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   k->bd = b;
   return SIM_OK;
@@ -738,7 +811,11 @@ int sim_koopman_bilinear_step(sim_koopman* k, int n, const double* z0, const dou
   if (!k->d_A) return soarm_set_error(SIM_E_ARG, "sim_koopman_set_bilinear was not called");
   if (n == 0) return SIM_OK;
   const int ep = k->bd.epw;
-  auto kern = ep == 6 ? k_bilinear<6> : ep == 4 ? k_bilinear<4> : ep == 2 ? k_bilinear<2> : k_bilinear<1>;
+  auto kern = ep == 8   ? k_bilinear<8>
+              : ep == 6 ? k_bilinear<6>
+              : ep == 4 ? k_bilinear<4>
+              : ep == 2 ? k_bilinear<2>
+                        : k_bilinear<1>;
   hipLaunchKernelGGL(kern, dim3((n + ep - 1) / ep), dim3(64 * ep),
                      ((size_t)k->bd.per_env * ep + (size_t)k->bd.nz * (k->bd.nz + 1)) * sizeof(double), (hipStream_t)stream,
                      k->bd, k->d_A, k->d_B,

@@ -83,8 +83,14 @@ def keyed_uniform(seed, ids, counter, k, lo, hi):
     return lo32 + (np.float32(hi) - lo32) * u
 
 
+# the bench workloads' narrowphase: libccd MPR, labelled in every bench line (`bench.py --ccd`);
+# the library's own default is native GJK/EPA (mjcf.compile_mjcf), what current MuJoCo runs
+BENCH_CCD = "mpr"
+
+
 def model(name, **kw):
     c = CONFIGS[name]
+    kw.setdefault("ccd", BENCH_CCD)
     return compile_mjcf(c["xml"], disable_contact=c["disable_contact"], **kw)
 
 
