@@ -2,7 +2,8 @@
 # Round-4 evidence in one GPU call (each step time-limited; a failure ends the script):
 # tests + smoke, the bench lines of every config, rocprofv3 kernel-trace summaries and PMC passes of
 # the headline (PGS), its Newton twin and the DBKN MPC, and the phase profile of the contact substep.
-#   usage: tools/gpu_final_r04.sh [tag] [--no-tests]
+#   usage: tools/gpu_final_r04.sh [tag] [--no-tests]; PART=bench (tests, smoke, bench lines, phase
+#   profile) or PART=prof (the rocprofv3 passes) runs one half (two GPU calls within the call limit)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-r04}
@@ -17,6 +18,8 @@ step() {  # name, limit, command...
   echo "== $name rc=$rc" >&2
   if [ $rc -ne 0 ]; then exit $rc; fi
 }
+PART=${PART:-all}
+if [ "$PART" != "prof" ]; then
 if [ "$2" != "--no-tests" ]; then
   step pytest 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1
   tail -2 $O/pytest_gpu.log
@@ -34,6 +37,8 @@ step bench_mpc_dbkn 600 python bench.py --config mpc_dbkn --steps 30 --warmup 5 
 step bench_plumbing 300 python bench.py --config plumbing > $O/bench_plumbing.json 2> $O/bench_plumbing.err
 step bench_gloo2 300 python bench.py --gpus 2 --dist-backend gloo --steps 10 --warmup 2 --no-cpu-baseline --no-steady --no-other-solver > $O/bench_gloo2.json 2> $O/bench_gloo2.err
 step phase_pgs 300 env EVERY=20 python tools/phase_prof.py 120 > $O/phase_pgs.log 2>&1
+fi
+if [ "$PART" = "bench" ]; then echo final-ok; exit 0; fi
 KRE="k_substep|k_collide|k_step|k_geom|k_mpc_step|k_bias|k_bilinear"
 cd /tmp
 for SPEC in contact:contact: contact_newton:contact:--solver_newton mpc_dbkn:mpc_dbkn:; do
