@@ -329,7 +329,7 @@ __device__ unsigned long long g_bl[9];
 template <int EPW>
 __global__ __launch_bounds__(64 * EPW) void k_bilinear(BDev K, const double* __restrict__ A,
                                                           const double* __restrict__ Bm,
-                                                          const double* __restrict__ HhT, int n,
+                                                          const double* __restrict__ Hh, int n,
                                                           const double* __restrict__ z0g,
                                                           const double* __restrict__ win,
                                                           double* __restrict__ uprev, float* __restrict__ action) {
@@ -357,15 +357,16 @@ __global__ __launch_bounds__(64 * EPW) void k_bilinear(BDev K, const double* __r
 #pragma unroll
   for (int c = 0; c < 8; c++) up[c] = c < nu ? uprev[(size_t)c * n + e] : 0.0;
   wsync();
-  // B_total = B + sum_j z0_j Hhat_j  (HhT [(i nu + c)][j]); for nz <= 32 a row's loads are all
-  // issued before the FMAs (the same four chains, in the same order, as dotn)
+  // B_total = B + sum_j z0_j Hhat_j  (Hhat [j][(i nu + c)]: a load instruction reads 64
+  // consecutive doubles); for nz <= 32 all of an output's loads are issued before its FMAs (the
+  // same four chains, in the same order, as dotn)
   for (int o = lane; o < zu; o += 64) {
-    const double* hr = HhT + (size_t)o * nz;
+    const double* hr = Hh + o;
     double d;
     if (nz <= 32) {
       double h[32];
 #pragma unroll
-      for (int j = 0; j < 32; j++) h[j] = hr[min(j, nz - 1)];
+      for (int j = 0; j < 32; j++) h[j] = hr[(size_t)min(j, nz - 1) * zu];
       double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
 #pragma unroll
       for (int j = 0; j < 32; j += 4)
@@ -380,7 +381,7 @@ __global__ __launch_bounds__(64 * EPW) void k_bilinear(BDev K, const double* __r
         if (j >= (nz & ~3) && j < nz) s0 = fma(h[j], zb[j], s0);
       d = (s0 + s1) + (s2 + s3);
     } else {
-      d = dotn(hr, 1, zb, nz);
+      d = dotn(hr, zu, zb, nz);
     }
     const double s = Bm[o] + d;
     M[o] = s, X[o] = s;
@@ -638,9 +639,9 @@ struct sim_koopman {
   KDev kd;
   double* d_frag = nullptr;    // encoder + [Gz | Gu] fragments, biases
   double* d_grfrag = nullptr;  // Gr fragments
-  // DBKN (sim_koopman_set_bilinear): A [nz][nz], B [nz][nu], Hhat as [(i nu + c)][j]
+  // DBKN (sim_koopman_set_bilinear): A [nz][nz], B [nz][nu], Hhat [j][(i nu + c)]
   BDev bd{};
-  double *d_A = nullptr, *d_B = nullptr, *d_HhT = nullptr;
+  double *d_A = nullptr, *d_B = nullptr, *d_Hh = nullptr;
 };
 
 #define KCHECK(x)                                                                                  \
@@ -763,7 +764,7 @@ void sim_koopman_free(sim_koopman* k) {
   (void)hipFree(k->d_grfrag);
   (void)hipFree(k->d_A);
   (void)hipFree(k->d_B);
-  (void)hipFree(k->d_HhT);
+  (void)hipFree(k->d_Hh);
   delete k;
 }
 
@@ -785,19 +786,17 @@ int sim_koopman_set_bilinear(sim_koopman* k, const double* A, const double* B, c
   for (int ep : {8, 6, 4, 2, 1})
     if (!b.epw && ((size_t)b.per_env * ep + (size_t)nz * (nz + 1)) * 8 <= 160 * 1024) b.epw = ep;
   if (!b.epw) return soarm_set_error(SIM_E_MODEL, "bilinear MPC does not fit in LDS");
-  std::vector<double> hht((size_t)nz * nu * nz);
-  for (int j = 0; j < nz; j++)
-    for (int i = 0; i < nz; i++)
-      for (int c = 0; c < nu; c++) hht[((size_t)i * nu + c) * nz + j] = Hhat[((size_t)j * nz + i) * nu + c];
+  // Hhat [j][i][c] is already the kernel's layout [j][(i nu + c)]
+  std::vector<double> hht(Hhat, Hhat + (size_t)nz * nz * nu);
   KCHECK(hipSetDevice(k->device));
-  (void)hipFree(k->d_A), (void)hipFree(k->d_B), (void)hipFree(k->d_HhT);
-  k->d_A = k->d_B = k->d_HhT = nullptr;
+  (void)hipFree(k->d_A), (void)hipFree(k->d_B), (void)hipFree(k->d_Hh);
+  k->d_A = k->d_B = k->d_Hh = nullptr;
   KCHECK(hipMalloc(&k->d_A, (size_t)nz * nz * 8));
   KCHECK(hipMalloc(&k->d_B, (size_t)nz * nu * 8));
-  KCHECK(hipMalloc(&k->d_HhT, hht.size() * 8));
+  KCHECK(hipMalloc(&k->d_Hh, hht.size() * 8));
   KCHECK(hipMemcpy(k->d_A, A, (size_t)nz * nz * 8, hipMemcpyHostToDevice));
   KCHECK(hipMemcpy(k->d_B, B, (size_t)nz * nu * 8, hipMemcpyHostToDevice));
-  KCHECK(hipMemcpy(k->d_HhT, hht.data(), hht.size() * 8, hipMemcpyHostToDevice));
+  KCHECK(hipMemcpy(k->d_Hh, hht.data(), hht.size() * 8, hipMemcpyHostToDevice));
   for (const void* f : {(const void*)k_bilinear<8>, (const void*)k_bilinear<6>, (const void*)k_bilinear<4>,
                         (const void*)k_bilinear<2>, (const void*)k_bilinear<1>})
     KCHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -819,7 +818,7 @@ int sim_koopman_bilinear_step(sim_koopman* k, int n, const double* z0, const dou
   hipLaunchKernelGGL(kern, dim3((n + ep - 1) / ep), dim3(64 * ep),
                      ((size_t)k->bd.per_env * ep + (size_t)k->bd.nz * (k->bd.nz + 1)) * sizeof(double), (hipStream_t)stream,
                      k->bd, k->d_A, k->d_B,
-                     k->d_HhT, n, z0, window, u_prev, action);
+                     k->d_Hh, n, z0, window, u_prev, action);
   KCHECK(hipGetLastError());
   return SIM_OK;
 }
