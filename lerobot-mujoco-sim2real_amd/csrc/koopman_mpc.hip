@@ -272,17 +272,17 @@ __global__ __launch_bounds__(256) void k_feedforward(KDev K, const double* __res
 //   P v' = Pi rhs by a Cholesky with the rows in registers, a forward solve and the first nu steps
 //   of the back substitution (pivots by readlane): v_0 = v'_{(H-1) nu + c} comes first there;
 //   u0 = v_0 + u_prev, action = clip(u0).
-// Shapes: nz <= 64, nu <= 8, N = H nu <= 64.  Per env LDS: the X region (X [H][nz*nu], later G
-// and P), M [nz*nu] (later the Cholesky's column buffer, >= 256 doubles), y / e [nz] each
-// (15.3 KB at nz 32, nu 5, H 10); up to 8 envs (waves) per workgroup, or as many as the LDS holds
-// with A [nz][nz].
+// Shapes: nz <= 64, nu <= 8, N = H nu <= 64.  Per env LDS: the X region (X [H][xs], later G
+// and P) and the M region (M [nz*nu] and Zs [H+1][nz], later Y [N][H], then the Cholesky's column
+// buffer; >= 256 doubles): 17.3 KB at nz 32, nu 5, H 10; up to 8 envs (waves) per workgroup, or as
+// many as the LDS holds with A [nz][nz].
 struct BDev {
   int nz, nu, H, N, delta, per_env;  // per_env: doubles of LDS per env
   int epw;                           // envs (waves) per workgroup
   int xreg;                          // doubles of the X / Gram / packed-Hessian region
   int xs;                            // X_k's stride (>= nz nu, = nu mod 32: the rhs phase's lanes
                                      // (X_{t-s} column c) then fall in distinct LDS banks)
-  int mreg;                          // doubles of M (>= 256: the Cholesky's column buffer after)
+  int mreg;                          // doubles of the M region (M, Zs; Y; the Cholesky's column buffer)
   double q, r, uclip;
 };
 // a double of lane l (l wave-uniform) in every lane: two v_readlane
@@ -349,10 +349,9 @@ __global__ __launch_bounds__(64 * EPW) void k_bilinear(BDev K, const double* __r
   if (e >= n) return;  // (whole waves: no workgroup barrier below)
   BL_STAMP(0);
   double* X = lds + (size_t)w * K.per_env;  // [H][xs]; later G and P, packed lower (N (N + 1) / 2)
-  double* M = X + K.xreg;                   // [zu]; later the Cholesky's column buffer
-  double* zb = M + K.mreg;                  // [nz]: z0, then A^t z0
-  double* eb = zb + nz;                     // [nz]: e_t
-  for (int i = lane; i < nz; i += 64) zb[i] = z0g[(size_t)i * n + e];
+  double* M = X + K.xreg;                   // [zu]; later Y, then the Cholesky's column buffer
+  double* Zs = M + zu;                      // [H + 1][nz]: A^t z0 (t = 0..H), later e_t over row t + 1
+  for (int i = lane; i < nz; i += 64) Zs[i] = z0g[(size_t)i * n + e];
   double up[8];
 #pragma unroll
   for (int c = 0; c < 8; c++) up[c] = c < nu ? uprev[(size_t)c * n + e] : 0.0;
@@ -371,17 +370,17 @@ __global__ __launch_bounds__(64 * EPW) void k_bilinear(BDev K, const double* __r
 #pragma unroll
       for (int j = 0; j < 32; j += 4)
         if (j + 4 <= nz) {
-          s0 = fma(h[j], zb[j], s0);
-          s1 = fma(h[j + 1], zb[j + 1], s1);
-          s2 = fma(h[j + 2], zb[j + 2], s2);
-          s3 = fma(h[j + 3], zb[j + 3], s3);
+          s0 = fma(h[j], Zs[j], s0);
+          s1 = fma(h[j + 1], Zs[j + 1], s1);
+          s2 = fma(h[j + 2], Zs[j + 2], s2);
+          s3 = fma(h[j + 3], Zs[j + 3], s3);
         }
 #pragma unroll
       for (int j = 0; j < 32; j++)
-        if (j >= (nz & ~3) && j < nz) s0 = fma(h[j], zb[j], s0);
+        if (j >= (nz & ~3) && j < nz) s0 = fma(h[j], Zs[j], s0);
       d = (s0 + s1) + (s2 + s3);
     } else {
-      d = dotn(hr, zu, zb, nz);
+      d = dotn(hr, zu, Zs, nz);
     }
     const double s = Bm[o] + d;
     M[o] = s, X[o] = s;
@@ -399,7 +398,9 @@ __global__ __launch_bounds__(64 * EPW) void k_bilinear(BDev K, const double* __r
   BL_STAMP(1);
   // M_k = A M_{k-1}; X_k = M_k or X_{k-1} + M_k, on the f64 MFMA: A's 16-row tiles (A fragment:
   // lane l holds A[16 t + (l & 15)][4 ks + (l >> 4)]) times M_{k-1} padded to 16 columns (B: lane l
-  // holds M[4 ks + (l >> 4)][l & 15]); C: lane l, register r = row 16 t + (l >> 4) + 4 r, column l & 15
+  // holds M[4 ks + (l >> 4)][l & 15]); C: lane l, register r = row 16 t + (l >> 4) + 4 r, column l & 15.
+  // Column nu of the B operand carries A^{k-1} z0, so the same products give the free response
+  // A^k z0 (k = 1..H; the last round computes only that column).
   {
     const int NTz = (nz + 15) >> 4, KSz = (nz + 3) >> 2, fr = lane >> 4, fc = lane & 15;
     // A's fragments for nz <= 32 (2 row tiles x 8 k-steps) stay in registers across the H steps
@@ -411,17 +412,18 @@ __global__ __launch_bounds__(64 * EPW) void k_bilinear(BDev K, const double* __r
         const int ar = 16 * t + fc, jr = 4 * ks + fr;
         af[t][ks] = (ar < nz && jr < nz) ? As[ar * as + jr] : 0.0;
       }
-    for (int k = 1; k < H; k++) {
+    const double* zc = Zs;  // A^{k-1} z0
+    auto bop = [&](int jr) {  // B operand of row jr (lane column fc)
+      return jr < nz ? (fc < nu ? M[jr * nu + fc] : (fc == nu ? zc[jr] : 0.0)) : 0.0;
+    };
+    for (int k = 1; k <= H; k++) {
       d4 acc[4];
 #pragma unroll
       for (int t = 0; t < 4; t++) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
       if (nz <= 32) {
         double bm[8];
 #pragma unroll
-        for (int ks = 0; ks < 8; ks++) {
-          const int jr = 4 * ks + fr;
-          bm[ks] = (jr < nz && fc < nu) ? M[jr * nu + fc] : 0.0;
-        }
+        for (int ks = 0; ks < 8; ks++) bm[ks] = bop(4 * ks + fr);
 #pragma unroll
         for (int ks = 0; ks < 8; ks++) {
           acc[0] = mfma(af[0][ks], bm[ks], acc[0]);
@@ -430,7 +432,7 @@ __global__ __launch_bounds__(64 * EPW) void k_bilinear(BDev K, const double* __r
       } else {
         for (int ks = 0; ks < KSz; ks++) {
           const int jr = 4 * ks + fr;
-          const double bm = (jr < nz && fc < nu) ? M[jr * nu + fc] : 0.0;
+          const double bm = bop(jr);
 #pragma unroll
           for (int t = 0; t < 4; t++) {
             const int ar = 16 * t + fc;
@@ -444,42 +446,45 @@ __global__ __launch_bounds__(64 * EPW) void k_bilinear(BDev K, const double* __r
 #pragma unroll
         for (int r = 0; r < 4; r++) {
           const int row = 16 * t + fr + 4 * r, o = row * nu + fc;
-          if (t < NTz && row < nz && fc < nu) {
-            M[o] = acc[t][r];
-            X[k * xs + o] = K.delta ? X[(k - 1) * xs + o] + acc[t][r] : acc[t][r];
+          if (t < NTz && row < nz) {
+            if (fc < nu && k < H) {
+              M[o] = acc[t][r];
+              X[k * xs + o] = K.delta ? X[(k - 1) * xs + o] + acc[t][r] : acc[t][r];
+            } else if (fc == nu) {
+              Zs[k * nz + row] = acc[t][r];
+            }
           }
         }
+      zc = Zs + k * nz;
       wsync();
     }
   }
   BL_STAMP(2);
-  // rhs in the reversed order (lane a holds entry flip(a) = s nu + c, s = H-1 - a / nu):
-  // e_t = ref_t - A^{t+1} z0 - [delta] C_t u_prev, rhs[s] += q X_{t-s}' e_t
-  double rhs = 0.0;
-  const int ls = H - 1 - lane / nu, lc = lane % nu;
-  for (int t = 0; t < H; t++) {
-    double yn = 0.0;
-    if (lane < nz) yn = dotn(zb, 1, As + lane * as, nz);
-    double wt = 0.0;
+  // e_t = ref_t - A^{t+1} z0 - [delta] C_t u_prev (lane i < nz), in place over row t + 1 of Zs
+  if (lane < nz) {
+#pragma unroll 2
+    for (int t = 0; t < H; t++) {
+      double wt = 0.0;
 #pragma unroll
-    for (int s = 0; s < 16; s++) wt = s == t ? wv[s] : wt;
-    if (t >= 16 && lane < nz) wt = win[((size_t)t * nz + lane) * n + e];
-    wsync();
-    if (lane < nz) {
-      zb[lane] = yn;
-      double ev = wt - yn;
+      for (int s2 = 0; s2 < 16; s2++) wt = s2 == t ? wv[s2] : wt;
+      if (t >= 16) wt = win[((size_t)t * nz + lane) * n + e];
+      double ev = wt - Zs[(t + 1) * nz + lane];
       if (K.delta) {
 #pragma unroll
         for (int c = 0; c < 8; c++)
           if (c < nu) ev = fma(-X[t * xs + lane * nu + c], up[c], ev);
       }
-      eb[lane] = ev;
+      Zs[(t + 1) * nz + lane] = ev;
     }
-    wsync();
-    if (lane < N && ls <= t) {
-      rhs = fma(K.q, dotn(X + (t - ls) * xs + lc, nu, eb, nz), rhs);
-    }
-    // (no sync here: the next frame's first sync orders these reads of eb before its writes)
+  }
+  wsync();
+  // rhs in the reversed order (lane a holds entry flip(a) = s nu + c, s = H-1 - a / nu):
+  // rhs[s] = q sum_{t >= s} X_{t-s}' e_t.  For H <= 16 from Y = Xs' E (the Gram's MFMA loop below,
+  // N x H); otherwise here, one dot product per (lane, t).
+  double rhs = 0.0;
+  const int ls = H - 1 - lane / nu, lc = lane % nu;
+  if (H > 16 && lane < N) {
+    for (int t = ls; t < H; t++) rhs = fma(K.q, dotn(X + (t - ls) * xs + lc, nu, Zs + (t + 1) * nz, nz), rhs);
   }
   BL_STAMP(3);
   // Gram G[a][b] = sum_i X[i][a] X[i][b] over the N = H nu columns a = k nu + c of the stacked X_k
@@ -490,9 +495,12 @@ __global__ __launch_bounds__(64 * EPW) void k_bilinear(BDev K, const double* __r
   double* G = X;
   {
     const int NT = (N + 15) >> 4, KS = (nz + 3) >> 2;
-    d4 acc[10];
+    const bool yk = H <= 16;  // Y = Xs' E here (B operand: lane l holds e_{l & 15}[4 ks + (l >> 4)])
+    d4 acc[10], yacc[4];
 #pragma unroll
     for (int q = 0; q < 10; q++) acc[q] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < 4; q++) yacc[q] = d4{0.0, 0.0, 0.0, 0.0};
     const int fr = lane >> 4, fc = lane & 15;
     for (int ks = 0; ks < KS; ks++) {
       double fg[4];
@@ -507,8 +515,27 @@ __global__ __launch_bounds__(64 * EPW) void k_bilinear(BDev K, const double* __r
 #pragma unroll
         for (int tb = 0; tb <= ta; tb++, q++)
           if (ta < NT) acc[q] = mfma(fg[ta], fg[tb], acc[q]);
+      if (yk) {
+        const double eo = (fc < H && i < nz) ? Zs[(fc + 1) * nz + i] : 0.0;
+#pragma unroll
+        for (int ta = 0; ta < 4; ta++)
+          if (ta < NT) yacc[ta] = mfma(fg[ta], eo, yacc[ta]);
+      }
     }
     wsync();
+    if (yk) {  // Y [a][t] over M's storage (M and E are dead), then each lane's diagonal sum
+      double* Y = M;
+#pragma unroll
+      for (int ta = 0; ta < 4; ta++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int a = 16 * ta + fr + 4 * r;
+          if (ta < NT && a < N && fc < H) Y[a * H + fc] = yacc[ta][r];
+        }
+      wsync();
+      if (lane < N)
+        for (int t = ls; t < H; t++) rhs = fma(K.q, Y[((t - ls) * nu + lc) * H + t], rhs);
+    }
 #pragma unroll
     for (int ta = 0, q = 0; ta < 4; ta++)
 #pragma unroll
@@ -778,8 +805,8 @@ int sim_koopman_set_bilinear(sim_koopman* k, const double* A, const double* B, c
   b.nz = nz, b.nu = nu, b.H = H, b.N = N, b.delta = delta ? 1 : 0, b.q = q, b.r = r, b.uclip = k->kd.uclip;
   b.xs = nz * nu + ((nu - nz * nu) % 32 + 32) % 32;
   b.xreg = (std::max(H * b.xs, N * (N + 1) / 2) + 1) & ~1;  // (even: M's column buffer is read as 16-B pairs)
-  b.mreg = std::max(nz * nu, 256);
-  b.per_env = (b.xreg + b.mreg + 2 * nz + 1) & ~1;
+  b.mreg = (std::max(std::max(nz * nu + (H + 1) * nz, N * H), 256) + 1) & ~1;
+  b.per_env = b.xreg + b.mreg;
   // as many envs per workgroup as fit the CU's LDS with A (8 at nz 32, nu 5, H 10: 125 KB; the
   // kernel's 215 VGPRs allow 2 waves per SIMD, so 8 is also the register limit)
   b.epw = 0;
