@@ -17,7 +17,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SHORT = {"k_substep": "substep", "k_collide": "collide", "k_step": "step_fused", "k_geom": "geom",
-         "k_mpc_step": "mpc_step", "k_bias": "bias"}
+         "k_mpc_step": "mpc_step", "k_bias": "bias", "k_bilinear": "bilinear", "k_encode": "encode"}
 
 
 def short(name):
