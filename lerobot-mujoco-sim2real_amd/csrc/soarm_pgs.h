@@ -258,6 +258,9 @@ struct PairMask {
   }
 };
 
+// first row past the contact rows of the scratch slab (sim_batch d_scratch): Newton's zone history
+template <int NA, int NF>
+constexpr int zhist_row() { return 4 * SIM_MAXCON * (2 * (NA + 6 * NF) + 4); }
 template <int NA, int NF>
 struct ContactRows {
   static constexpr int NV = NA + 6 * NF;

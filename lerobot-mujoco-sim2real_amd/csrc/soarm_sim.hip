@@ -382,6 +382,14 @@ __global__ __launch_bounds__(WIDE ? 256 : 64) void k_substep(const DModel* __res
   }
   // a soft reset moved the env: the collide output no longer applies
   const bool use = S.status == st0 && ccount != nullptr;
+  // Newton's frictionloss-zone history (two substeps, past the contact rows of the scratch slab):
+  // a period-2 pattern predicts this substep's zones (soarm_newton.h)
+  uint32_t zh1 = 0u, zh2 = 0u;
+  if constexpr (SOL == SIM_SOL_NEWTON) {
+    const uint32_t* zh = (const uint32_t*)(scratch + e) + (size_t)zhist_row<NA, NF>() * n;
+    zh1 = zh[0], zh2 = zh[n];
+    if ((zh1 >> 31) && (zh2 >> 31) && zh1 != zh2) S.zpred = zh2;
+  }
   PairMask pm;
   if (use) pm.load(pmask, m, n, e);  // (stays zero otherwise: no contact list)
 #ifdef SOARM_PHASE_PROF
@@ -411,6 +419,12 @@ __global__ __launch_bounds__(WIDE ? 256 : 64) void k_substep(const DModel* __res
     ncon = forward<NA, NF, true, SOL>(S, nullptr, nullptr, nullptr, n, e, L, cr);
   }
   PSTAMP(10);
+  if constexpr (SOL == SIM_SOL_NEWTON) {
+    if ((threadIdx.x & (lpe<NF>() - 1)) == 0) {
+      uint32_t* zh = (uint32_t*)(scratch + e) + (size_t)zhist_row<NA, NF>() * n;
+      zh[0] = S.zfin, zh[n] = zh1;
+    }
+  }
   if constexpr (NF == 1) {  // reload (laundered pointers: not CSE'd with the first load)
     const float* qp = launder(st.qpos);
     const float* qv = launder(st.qvel);
@@ -1151,8 +1165,10 @@ int sim_batch_create(const sim_model* m, int n_envs, int device, sim_batch** out
   }
   if (!m->desc.disable_contact) {
     const int nv = m->desc.nv;
-    B->scratch_floats = (size_t)4 * SIM_MAXCON * (2 * nv + 4) * n_envs;
+    // contact rows, then two rows of Newton's zone history (zero: none)
+    B->scratch_floats = ((size_t)4 * SIM_MAXCON * (2 * nv + 4) + 2) * n_envs;
     HIPCHECK(hipMalloc(&B->d_scratch, B->scratch_floats * sizeof(float)));
+    HIPCHECK(hipMemset(B->d_scratch, 0, B->scratch_floats * sizeof(float)));
     HIPCHECK(hipMalloc(&B->d_gpose, (size_t)m->desc.ngeom * GREC * n_envs * sizeof(float)));
     HIPCHECK(hipMalloc(&B->d_cbuf, (size_t)(m->dm.nslot > 0 ? m->dm.nslot : 1) * 7 * n_envs * sizeof(float)));
     HIPCHECK(hipMalloc(&B->d_ccount, (size_t)(m->desc.npair > 0 ? m->desc.npair : 1) * n_envs * sizeof(int)));

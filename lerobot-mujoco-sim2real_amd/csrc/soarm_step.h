@@ -33,6 +33,9 @@ struct Sim {
   float MF[NF > 0 ? NF : 1][21], LF[NF > 0 ? NF : 1][21], DFi[NF > 0 ? NF : 1][6];
   float cdofdot[NV][6];
   float fsmooth[NV], qacc_s[NV], qacc[NV], fcon[NV];
+  // Newton's zone prediction for the frictionloss rows (soarm_newton.h): 2 bits per dof (the pass's
+  // zone codes), bit 31 = set; zpred in (from the caller's history), zfin out (the solve's result)
+  uint32_t zpred = 0u, zfin = 0u;
 
   HDI Sim(const DModel* m_, float ms, float fr, float ds) : mp(m_), mscale(ms), fric(fr), dscale(ds) {}
   HDI void relaunder() {  // (through the constant address space: the model stays scalar-loaded)
