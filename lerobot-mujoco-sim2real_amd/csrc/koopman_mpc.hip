@@ -335,7 +335,12 @@ __global__ __launch_bounds__(64 * EPW) void k_bilinear(BDev K, const double* __r
                                                           double* __restrict__ uprev, float* __restrict__ action) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int e = blockIdx.x * EPW + w;
+  // XCD-aware chunking: workgroups are dealt round-robin over the 8 XCDs, so chunk the envs per
+  // XCD (workgroup b runs chunk (b % 8) G/8 + b / 8): neighbouring envs -- which share the cache
+  // lines of z0 and of the [H][nz][n] window -- land in the same L2
+  const int nwg = gridDim.x;
+  const int b = (nwg & 7) ? (int)blockIdx.x : ((int)blockIdx.x & 7) * (nwg >> 3) + ((int)blockIdx.x >> 3);
+  const int e = b * EPW + w;
 #ifdef SOARM_BL_PROF
   long long bl_t = 0;
 #endif

@@ -932,6 +932,31 @@ def test_newton_solver_matches_oracle(gpu_lib, t0):
     assert_pct(np.abs(og - oc).max(1), 1e-6, 2e-6, 2e-4, what="obs")
 
 
+def test_newton_zone_prediction_same_optimum(gpu_lib):
+    """The Newton zone prediction (soarm_newton.h: the first iteration takes the frictionloss rows'
+    zones of two substeps back when the last two differ) changes the path, not the optimum: after
+    4 device substeps from t = 100 bench states (each env's zone history filled), one more substep
+    against the oracle's exact Newton from the device's own state, and against a fresh batch
+    (empty history) from the same state."""
+    from lerobot_mujoco_sim2real_amd import workloads as W
+    _, _, st, _ = _bench_states("contact", 1024, 100, nthreads=16)
+    cm = W.model("contact", solver="Newton")
+    S = make_sim(cm, 1024)
+    load_state(S, st)
+    S.substeps(4)
+    s4 = dict(st)
+    s4.update(qpos=to_np(S.qpos).T, qvel=to_np(S.qvel).T, warm=to_np(S.qacc_warmstart).T,
+              ctrl=to_np(S.ctrl).T)
+    ref = _exact_newton_substep(cm, s4)
+    S.substeps(1)
+    F = make_sim(cm, 1024)
+    load_state(F, s4)
+    F.substeps(1)
+    v = to_np(S.qvel).T
+    assert_pct(np.abs(v - ref["qvel"]).max(1), 1e-5, 5e-5, 5e-4, what="qvel vs oracle")
+    assert_pct(np.abs(v - to_np(F.qvel).T).max(1), 1e-5, 5e-5, 5e-4, what="with vs without history")
+
+
 def test_newton_solver_contact_free(gpu_lib):
     """Newton on the contact-free scene (frictionloss + limits): fused k_step vs the oracle."""
     from lerobot_mujoco_sim2real_amd import mjcf
