@@ -227,10 +227,18 @@ __global__ __launch_bounds__(64) void k_step(const DModel* __restrict__ dm, int 
 // geom world poses from the current qpos (collision input); GEOM_LPE lanes per env split
 // the geoms (the FK chain runs on each of them)
 constexpr int GEOM_LPE = 4;
+// XCD-aware block index: workgroups are dealt round-robin over the 8 XCDs, so renumber them to give
+// each XCD a contiguous range of envs.  A 16-env workgroup touches half of each 128-B line of the
+// [row][env] state; its neighbour, which reads the other half, is then in the same L2.
+__device__ __forceinline__ int xcd_block() {
+  const int g = (int)gridDim.x, b = (int)blockIdx.x;
+  return (g & 7) ? b : (b & 7) * (g >> 3) + (b >> 3);
+}
+
 template <int NA, int NF>
 __global__ __launch_bounds__(64) void k_geom(const DModel* __restrict__ dm, int n, sim_state st,
                                              float* __restrict__ gpose) {
-  const int e = blockIdx.x * (64 / GEOM_LPE) + (int)threadIdx.x / GEOM_LPE;
+  const int e = xcd_block() * (64 / GEOM_LPE) + (int)threadIdx.x / GEOM_LPE;
   if (e >= n) return;
   Sim<NA, NF> S(dm, 1.f, -1.f, 1.f);
   load_state(S, st, n, e);
@@ -323,7 +331,7 @@ __global__ __launch_bounds__(WIDE ? 256 : 64) void k_substep(const DModel* __res
                                                 uint32_t* __restrict__ pmask,
                                                 float* __restrict__ gpose, const float* gpose_in) {
   // lpe<NF>() lanes per env (soarm_pgs.h): they run the same per-env code
-  const int e = blockIdx.x * (64 / lpe<NF>()) + (int)threadIdx.x / lpe<NF>();
+  const int e = xcd_block() * (64 / lpe<NF>()) + (int)threadIdx.x / lpe<NF>();
   __shared__ std::conditional_t<WIDE, WideLds, char> s_wide;
   if constexpr (WIDE) {
     static_assert(NF == 1 && SOL == SIM_SOL_PGS && 64 / lpe<NF>() == WIDE_COLS, "wide kernel: PGS, quad, 16 envs");
@@ -337,7 +345,7 @@ __global__ __launch_bounds__(WIDE ? 256 : 64) void k_substep(const DModel* __res
           // per env (the FK chain on each, every 12th geom of a body); no closing barrier -- the
           // next round is wave 0's EXIT
           const int h = (int)threadIdx.x - 64, c = h / 12, k = h - 12 * c;
-          const int eg = blockIdx.x * WIDE_COLS + c;
+          const int eg = xcd_block() * WIDE_COLS + c;
           Sim<NA, NF> G(dm, 1.f, -1.f, 1.f);
 #pragma unroll
           for (int i = 0; i < Sim<NA, NF>::NQ; i++) G.qpos[i] = s_wide.qpos[c][i];
