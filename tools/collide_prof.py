@@ -17,7 +17,7 @@ from lerobot_mujoco_sim2real_amd import workloads as W  # noqa: E402
 from lerobot_mujoco_sim2real_amd.sim import BatchSim  # noqa: E402
 
 n = 4096
-cm = W.model(os.environ.get("CONFIG", "contact"))
+cm = W.model(os.environ.get("CONFIG", "contact"), ccd=os.environ.get("CCD", W.BENCH_CCD))
 ids = np.arange(n)
 sim = BatchSim(cm, n, 0)
 q0 = W.initial_qpos(cm, ids, 0)
