@@ -257,7 +257,9 @@ __global__ __launch_bounds__(256, SOARM_COLLIDE_WAVES) void k_collide(const DMod
                                                  uint32_t* __restrict__ pmask,
                                                  float* __restrict__ sepax,
                                                  unsigned long long* __restrict__ pcyc) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  // (env chunks numbered per XCD as in k_geom / k_substep: the geom records this reads and the
+  // contact buffer it writes stay in the L2 of the XCD whose substep waves own those envs)
+  const int e = xcd_block() * blockDim.x + threadIdx.x;
   const int p = gridDim.y - 1 - blockIdx.y;  // later pairs (self / cube-arm: MPR-heavy) dispatch first
   if (e >= n) return;
   const long long t0 = pcyc ? clock64() : 0;
