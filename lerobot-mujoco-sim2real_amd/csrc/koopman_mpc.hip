@@ -326,10 +326,11 @@ __device__ unsigned long long g_bl[9];
 #else
 #define BL_STAMP(k)
 #endif
-// HS / NUS: a static horizon and input count (0: read from K) -- the reference's configuration
-// (horizon 10, u_dim 5: N = 50) gets an instantiation in which every loop bound and guard on N, nu
-// and H is a constant (the Cholesky's and the solves' unrolled loops lose their per-column branches)
-template <int EPW, int HS = 0, int NUS = 0>
+// HS / NUS / NZS: a static horizon, input count and lifted dimension (0: read from K) -- the
+// reference's configuration (horizon 10, u_dim 5, nz = 8 + 24 = 32: N = 50) gets an instantiation in
+// which every loop bound and guard on N, nu, H and nz is a constant (the Cholesky's and the solves'
+// unrolled loops lose their per-column branches)
+template <int EPW, int HS = 0, int NUS = 0, int NZS = 0>
 __global__ __launch_bounds__(64 * EPW) void k_bilinear(BDev K, const double* __restrict__ A,
                                                           const double* __restrict__ Bm,
                                                           const double* __restrict__ Hh, int n,
@@ -347,7 +348,7 @@ __global__ __launch_bounds__(64 * EPW) void k_bilinear(BDev K, const double* __r
 #ifdef SOARM_BL_PROF
   long long bl_t = 0;
 #endif
-  const int nz = K.nz, nu = NUS ? NUS : K.nu, H = HS ? HS : K.H, N = (HS && NUS) ? HS * NUS : K.N;
+  const int nz = NZS ? NZS : K.nz, nu = NUS ? NUS : K.nu, H = HS ? HS : K.H, N = (HS && NUS) ? HS * NUS : K.N;
   const int zu = nz * nu, xs = K.xs;
   // A, shared by the workgroup's envs, rows padded to an odd stride (nz + 1 doubles): lanes reading
   // one element of different rows hit different banks (a 256-B stride puts them all on one)
@@ -834,7 +835,7 @@ int sim_koopman_set_bilinear(sim_koopman* k, const double* A, const double* B, c
   KCHECK(hipMemcpy(k->d_B, B, (size_t)nz * nu * 8, hipMemcpyHostToDevice));
   KCHECK(hipMemcpy(k->d_Hh, hht.data(), hht.size() * 8, hipMemcpyHostToDevice));
   for (const void* f : {(const void*)k_bilinear<8>, (const void*)k_bilinear<6>, (const void*)k_bilinear<4>,
-                        (const void*)k_bilinear<2>, (const void*)k_bilinear<1>, (const void*)k_bilinear<8, 10, 5>})
+                        (const void*)k_bilinear<2>, (const void*)k_bilinear<1>, (const void*)k_bilinear<8, 10, 5, 32>})
     KCHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   k->bd = b;
   return SIM_OK;
@@ -846,8 +847,8 @@ int sim_koopman_bilinear_step(sim_koopman* k, int n, const double* z0, const dou
   if (!k->d_A) return soarm_set_error(SIM_E_ARG, "sim_koopman_set_bilinear was not called");
   if (n == 0) return SIM_OK;
   const int ep = k->bd.epw;
-  const bool ref_shape = k->bd.H == 10 && k->bd.nu == 5 && ep == 8;  // (the static-shape instantiation)
-  auto kern = ref_shape ? k_bilinear<8, 10, 5>
+  const bool ref_shape = k->bd.H == 10 && k->bd.nu == 5 && k->bd.nz == 32 && ep == 8;  // (static shapes)
+  auto kern = ref_shape ? k_bilinear<8, 10, 5, 32>
               : ep == 8 ? k_bilinear<8>
               : ep == 6 ? k_bilinear<6>
               : ep == 4 ? k_bilinear<4>
