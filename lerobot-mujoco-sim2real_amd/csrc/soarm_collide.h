@@ -1140,7 +1140,9 @@ HDI bool cached_apart(const DModel& m, int p, int g1, int g2, const GeomPose& P1
   return minkowski_ub(m, g1, g2, P1, P2, d) < -(m.pair_margin[p] + SEP_MARGIN);
 }
 
-// narrowphase of a pair that passed the midphase (geom types are uniform over a pair)
+// narrowphase of a pair that passed the midphase (geom types are uniform over a pair); CCD: the
+// convex-convex narrowphase fixed at compile time (SIM_CCD_*), or -1 to read it from the model
+template <int CCD = -1>
 HDI void narrowphase(const DModel& m, int p, const GeomPose& P1, const GeomPose& P2, PairOut& o,
                       const SepCache& sc) {
   o.n = 0;
@@ -1220,7 +1222,8 @@ HDI void narrowphase(const DModel& m, int p, const GeomPose& P1, const GeomPose&
   }
   MPair mp{m, g1, g2, P1, P2};
   float depth, dir[3], pos[3], sep[3] = {0.f, 0.f, 0.f};
-  if (m.ccd == SIM_CCD_NATIVE ? ccd_native(mp, depth, dir, pos, sep) : mpr(mp, depth, dir, pos, sep)) {
+  const bool native = CCD < 0 ? m.ccd == SIM_CCD_NATIVE : CCD == SIM_CCD_NATIVE;
+  if (native ? ccd_native(mp, depth, dir, pos, sep) : mpr(mp, depth, dir, pos, sep)) {
     emit(o, -depth, pos, dir);
     o.xc = 5;
   } else {
@@ -1233,10 +1236,11 @@ HDI void narrowphase(const DModel& m, int p, const GeomPose& P1, const GeomPose&
 
 namespace soarm {
 // midphase + narrowphase of candidate pair p of env e (geom records in gpose)
+template <int CCD = -1>
 HDI void collide_pair(const DModel& m, int p, const float* __restrict__ gpose, int n, int e, PairOut& o,
                        const SepCache& sc = SepCache{nullptr, 0, 0}) {
   o.n = 0;
   GeomPose P1, P2;
-  if (midphase(m, p, gpose, n, e, P1, P2)) narrowphase(m, p, P1, P2, o, sc);
+  if (midphase(m, p, gpose, n, e, P1, P2)) narrowphase<CCD>(m, p, P1, P2, o, sc);
 }
 }  // namespace soarm

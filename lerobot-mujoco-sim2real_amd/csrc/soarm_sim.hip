@@ -251,6 +251,9 @@ inline dim3 geom_grid(int n) { return dim3((n + 64 / GEOM_LPE - 1) / (64 / GEOM_
 #ifndef SOARM_COLLIDE_WAVES
 #define SOARM_COLLIDE_WAVES 3  // min waves per SIMD (VGPR cap 512 / 3 = 168)
 #endif
+// CCD: one instantiation per narrowphase, so the MPR kernel carries none of EPA's private-memory
+// polytope (2.2 KB of scratch per lane)
+template <int CCD>
 __global__ __launch_bounds__(256, SOARM_COLLIDE_WAVES) void k_collide(const DModel* __restrict__ dm, int n,
                                                  const float* __restrict__ gpose,
                                                  float* __restrict__ cbuf, int* __restrict__ ccount,
@@ -265,7 +268,7 @@ __global__ __launch_bounds__(256, SOARM_COLLIDE_WAVES) void k_collide(const DMod
   const long long t0 = pcyc ? clock64() : 0;
   const DModel& m = *dm;
   PairOut o{cbuf, n, e, m.pair_slot[p], m.pair_cap[p], 0};
-  collide_pair(m, p, gpose, n, e, o, SepCache{sepax, n, e});
+  collide_pair<CCD>(m, p, gpose, n, e, o, SepCache{sepax, n, e});
   // (no per-pair count is stored: the pair mask bit and, for multi-contact pairs, its 2-bit
   // count word carry it -- an empty pair costs no store)
   (void)ccount;
@@ -289,7 +292,8 @@ __global__ __launch_bounds__(256, SOARM_COLLIDE_WAVES) void k_collide(const DMod
 
 // the collide launch: (env, pair) lanes, 256-env blocks x npair
 static void launch_collide(const sim_batch* b, hipStream_t q, unsigned long long* pcyc) {
-  hipLaunchKernelGGL(k_collide, dim3((b->n + 255) / 256, b->model->desc.npair), dim3(256), 0, q, b->d_model, b->n,
+  auto kern = b->model->desc.ccd == SIM_CCD_NATIVE ? k_collide<SIM_CCD_NATIVE> : k_collide<SIM_CCD_MPR>;
+  hipLaunchKernelGGL(kern, dim3((b->n + 255) / 256, b->model->desc.npair), dim3(256), 0, q, b->d_model, b->n,
                      b->d_gpose, b->d_cbuf, b->d_ccount, b->d_pmask, b->d_sepax, pcyc);
 }
 

@@ -10,3 +10,5 @@ timeout -k 10 600 python bench.py --no-cpu-baseline > gpurun_out/bench_contact_x
 python -c "import json; d=json.loads(open('gpurun_out/bench_contact_x.json').read().strip().split(chr(10))[-1]); print('contact', round(d['value']), {k: round(x,4) for k,x in d['roofline']['kernel_ms_per_step'].items()}, d.get('other_solver'))"
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-other-solver > gpurun_out/bench_drv_x.json 2> gpurun_out/bench_drv_x.err || exit $?
 python -c "import json; d=json.loads(open('gpurun_out/bench_drv_x.json').read().strip().split(chr(10))[-1]); print('driver window', round(d['value']), d['ms_per_step'])"
+timeout -k 10 600 python bench.py --ccd native --no-cpu-baseline --no-other-solver > gpurun_out/bench_native_x.json 2> gpurun_out/bench_native_x.err || exit $?
+python -c "import json; d=json.loads(open('gpurun_out/bench_native_x.json').read().strip().split(chr(10))[-1]); print('native', round(d['value']), {k: round(x,4) for k,x in d['roofline']['kernel_ms_per_step'].items()})"
