@@ -136,3 +136,13 @@ def test_old_calibration_model():
     assert abs(d.actuator_ctrlrange[1][0] + 3.31612) < 1e-9 and abs(d.actuator_ctrlrange[2][1] - 3.14159) < 1e-9
     new = mjcf.compile_mjcf(mjcf.POSITION_SCENE_XML)
     assert not np.allclose(np.array(d.body_pos[2]), np.array(new.desc.body_pos[2]))  # other calibration
+
+
+def test_narrowphase_defaults(arm_model):
+    """The library compiles what current MuJoCo runs (native GJK/EPA, `nativeccd`) unless asked for
+    MPR; the bench workloads ask for MPR explicitly (their bench line states it)."""
+    from lerobot_mujoco_sim2real_amd import mjcf, workloads as W
+    assert arm_model.desc.ccd == 1  # SIM_CCD_NATIVE
+    assert mjcf.compile_mjcf(mjcf.SCENE_XML, ccd="mpr").desc.ccd == 0
+    assert W.BENCH_CCD == "mpr" and W.model("contact").desc.ccd == 0
+    assert W.model("contact", ccd="native").desc.ccd == 1
