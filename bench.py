@@ -38,7 +38,9 @@ def parse():
     p.add_argument("--envs", type=int, default=None, help="envs per GPU (default 4096; 8192 for dr)")
     p.add_argument("--config", default="contact",
                    choices=["contact", "nocontact", "dr", "rollout", "mpc", "mpc_dbkn", "plumbing"])
-    p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal on one GPU)")
+    p.add_argument("--dist-backend", default=None,
+                   help="nccl (= RCCL; the default for --gpus > 1) or gloo (rehearsal on one GPU); given with "
+                        "--gpus 1 it initialises a one-rank process group, so the rollout gather runs through it")
     p.add_argument("--solver", default="pgs", choices=["pgs", "newton"],
                    help="constraint solver: PGS (BASELINE config 3) or MuJoCo's default Newton")
     p.add_argument("--ccd", default="mpr", choices=["native", "mpr"],
@@ -56,16 +58,21 @@ def parse():
     return p.parse_args()
 
 
-def launch_ranks(args):
-    """`--gpus N` without a torchrun environment: start N rank processes of this script (one per
-    GPU) with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, wait, return the worst exit status.
-    Called before anything touches the GPU (this process never initialises HIP)."""
+def _free_port():
     import socket
-    import subprocess
     sk = socket.socket()
     sk.bind(("127.0.0.1", 0))
     port = sk.getsockname()[1]
     sk.close()
+    return port
+
+
+def launch_ranks(args):
+    """`--gpus N` without a torchrun environment: start N rank processes of this script (one per
+    GPU) with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, wait, return the worst exit status.
+    Called before anything touches the GPU (this process never initialises HIP)."""
+    import subprocess
+    port = _free_port()
     procs = []
     for r in range(args.gpus):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
@@ -95,10 +102,12 @@ def launch_ranks(args):
     return bad[0] if bad else 0
 
 
-def cpu_backend_leg(cm, cfg, seed, n, T, threads):
+def cpu_backend_leg(cm, cfg, seed, n, T, threads, t0=2, min_s=0.0):
     """The library's own CPU backend (sim_batch_create(..., -1, ...): the kernels' per-env code
     compiled for the host, fp32) on `threads` host threads: n envs x T env-steps of the workload
-    (after 2 untimed env-steps).  A measured side line, not the bench's cpu_baseline (the oracle)."""
+    after t0 untimed env-steps (the steady window: t0 = 20, T = 100), repeated from the reset
+    until at least min_s seconds are timed.  A measured side line, not the bench's cpu_baseline
+    (the oracle)."""
     import numpy as np
     from lerobot_mujoco_sim2real_amd import workloads as W
     from lerobot_mujoco_sim2real_amd.sim import BatchSim
@@ -115,21 +124,27 @@ def cpu_backend_leg(cm, cfg, seed, n, T, threads):
         rng = np.random.default_rng(seed)
         acts = [np.zeros((n, 5), np.float32) if cfg["action"] == "zero" else
                 W.chirp_action(tab, t).astype(np.float32) if cfg["action"] == "chirp" else
-                rng.uniform(-0.5, 0.5, (n, 5)).astype(np.float32) for t in range(T + 2)]
-        for t in range(2):
-            S.step(acts[t])
-        t0 = time.perf_counter()
-        for t in range(2, T + 2):
-            S.step(acts[t])
-        dt = time.perf_counter() - t0
+                rng.uniform(-0.5, 0.5, (n, 5)).astype(np.float32) for t in range(T + t0)]
+        dt, reps = 0.0, 0
+        while reps == 0 or dt < min_s:
+            if reps:
+                S.reset(init_qpos=q[:, :5], extra_qpos=q, seed=seed)
+            for t in range(t0):
+                S.step(acts[t])
+            ts = time.perf_counter()
+            for t in range(t0, T + t0):
+                S.step(acts[t])
+            dt += time.perf_counter() - ts
+            reps += 1
         S.close()
     finally:
         if old is None:
             os.environ.pop("SOARM_CPU_THREADS", None)
         else:
             os.environ["SOARM_CPU_THREADS"] = old
-    return {"value": n * T / dt, "unit": "env-steps/s", "threads": threads, "dtype": "f32",
-            "sample": f"{n} envs x {T} env-steps of the library's CPU backend (device = -1), {dt:.2f} s"}
+    return {"value": reps * n * T / dt, "unit": "env-steps/s", "threads": threads, "dtype": "f32",
+            "sample": f"{reps} x {n} envs x env-steps {t0}-{t0 + T} of the library's CPU backend (device = -1), "
+                      f"{dt:.2f} s timed"}
 
 
 def cpu_baseline(cfg_name, seconds, seed, solver="pgs", ccd="mpr"):
@@ -144,12 +159,16 @@ def cpu_baseline(cfg_name, seconds, seed, solver="pgs", ccd="mpr"):
     cm = W.model(cfg_name, solver=solver, ccd=ccd)
     orc = Oracle(cm)
     try:
-        cores = len(os.sched_getaffinity(0))
+        affinity = len(os.sched_getaffinity(0))
     except AttributeError:
-        cores = os.cpu_count()
-    cores = max(1, min(cores, 16))  # the GPU box's CPU share is 16
-    T = 10
+        affinity = os.cpu_count()
+    # the GPU box gives a job a 16-CPU share (OMP_NUM_THREADS=16 there) whatever the affinity
+    # mask shows: at most 16 threads
+    cores = max(1, min(affinity, 16))
     mpc = None
+    # the sampled window: the steady window of the GPU line (env-steps 20-120: chunks start from the
+    # oracle's own states at t = 20, reached untimed); the Koopman-MPC configs: 10 frames from the reset
+    T0, T = (0, 10) if cfg["action"] == "koopman_mpc" else (20, 100)
     if cfg["action"] == "koopman_mpc":
         import koopman_mpc as KO
         net, _ = _mpc_net(seed, cfg.get("koopman", "DKUC"))
@@ -176,7 +195,10 @@ def cpu_baseline(cfg_name, seconds, seed, solver="pgs", ccd="mpr"):
             sref = np.concatenate([cart, np.repeat(q[None, :, :5].astype(np.float64), T, 0)], -1)
             zref = KO.encode(layers, sref.reshape(T * n, 8)).reshape(T, n, -1)
             x, up = sref[0], np.zeros((n, 5))
-        for t in range(T):
+        ts = None
+        for t in range(T0 + T):
+            if t == T0:
+                ts = time.perf_counter()
             if mpc:
                 if Hhat is None:
                     up, a = KO.get_control(A, B, KO.encode(layers, x), KO.lifted_window(zref, t, 10), up, qp=qp)
@@ -192,7 +214,7 @@ def cpu_baseline(cfg_name, seconds, seed, solver="pgs", ccd="mpr"):
             else:
                 a = rng.uniform(-0.5, 0.5, (n, 5))
             orc.step(st, a, params=prm, nthreads=nthreads)
-        return n * T
+        return n * T, time.perf_counter() - ts
 
     if cfg_name == "plumbing":  # config 1: one env, zero action, 1000 env-steps on one core
         t0 = time.perf_counter()
@@ -206,17 +228,15 @@ def cpu_baseline(cfg_name, seconds, seed, solver="pgs", ccd="mpr"):
                 "sample": f"1 env x 1000 env-steps (zero action) of the float64 C oracle on 1 thread, {dt:.2f} s",
                 "nproc": os.cpu_count(), "fp32_cpu_backend": cpu_backend_leg(cm, cfg, seed, 1, 1000, 1)}
     n = 256
-    done, chunk, t0 = 0, 0, time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        done += run_chunk(np.arange(chunk * n, (chunk + 1) * n), cores)
-        chunk += 1
-    dt = time.perf_counter() - t0
-    # the same workload on ONE core (SURVEY 8d asks for both), a shorter sample of 64-env chunks
-    d1, c1, t1 = 0, 0, time.perf_counter()
-    while time.perf_counter() - t1 < max(1.0, seconds / 4):
-        d1 += run_chunk(np.arange(c1 * 64, (c1 + 1) * 64), 1)
-        c1 += 1
-    t1 = time.perf_counter() - t1
+    done, chunk, dt, tw = 0, 0, 0.0, time.perf_counter()
+    while chunk == 0 or time.perf_counter() - tw < seconds:
+        k, d = run_chunk(np.arange(chunk * n, (chunk + 1) * n), cores)
+        done, dt, chunk = done + k, dt + d, chunk + 1
+    # the same workload on ONE core (SURVEY 8d asks for both), a shorter sample of 32-env chunks
+    d1, c1, t1, tw = 0, 0, 0.0, time.perf_counter()
+    while c1 == 0 or time.perf_counter() - tw < max(1.0, seconds / 4):
+        k, d = run_chunk(np.arange(c1 * 32, (c1 + 1) * 32), 1)
+        d1, t1, c1 = d1 + k, t1 + d, c1 + 1
     cpu_name = "unknown"
     try:
         with open("/proc/cpuinfo") as f:
@@ -228,14 +248,16 @@ def cpu_baseline(cfg_name, seconds, seed, solver="pgs", ccd="mpr"):
     what = "float64 C oracle" + (" + numpy MPC restatement" if mpc else "")
     fp32 = None
     if cfg["action"] in ("chirp", "random"):  # the library's CPU backend on the same workload
-        fp32 = cpu_backend_leg(cm, cfg, seed, 256, T, cores)
-        fp32["single_core"] = cpu_backend_leg(cm, cfg, seed, 64, T, 1)
+        fp32 = cpu_backend_leg(cm, cfg, seed, 512, T, cores, t0=T0, min_s=1.0)
+        fp32["single_core"] = cpu_backend_leg(cm, cfg, seed, 32, T, 1, t0=T0, min_s=1.0)
     return {"value": done / dt, "unit": "env-steps/s", "cores": cores, "kind": "port",
             "fp32_cpu_backend": fp32,
-            "sample": f"{done} env-steps ({chunk} chunks of {n} envs x {T} steps, {cfg_name} workload) "
-                      f"of the {what}, OpenMP over envs, {dt:.1f} s",
-            "single_core": {"value": d1 / t1, "sample": f"{d1} env-steps ({c1} chunks of 64 envs x {T} steps) "
-                                                         f"on 1 thread, {t1:.1f} s"},
+            "sample": f"{done} env-steps ({chunk} chunks of {n} envs x env-steps {T0}-{T0 + T}, {cfg_name} "
+                      f"workload, each chunk from the oracle's own states at t = {T0}) of the {what}, "
+                      f"threads over envs, {dt:.1f} s timed",
+            "single_core": {"value": d1 / t1, "sample": f"{d1} env-steps ({c1} chunks of 32 envs x env-steps "
+                                                         f"{T0}-{T0 + T}) on 1 thread, {t1:.1f} s timed"},
+            "affinity_cores": affinity, "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
             "cpu_model": cpu_name, "nproc": os.cpu_count(), "mujoco": mj}
 
 
@@ -281,11 +303,18 @@ def main():
     gpu = local % max(torch.cuda.device_count(), 1)  # > 1 rank per GPU only in gloo rehearsals
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
-    if world > 1:
-        if args.dist_backend == "nccl":
+    backend = args.dist_backend or "nccl"
+    use_pg = world > 1 or args.dist_backend is not None  # one rank: only when asked (the RCCL path on one GPU)
+    if use_pg:
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
+        if backend == "nccl":
             dist.init_process_group("nccl", init_method="env://", device_id=dev)
         else:
-            dist.init_process_group(args.dist_backend, init_method="env://")
+            dist.init_process_group(backend, init_method="env://")
         if dist.get_world_size() != args.gpus:
             print(f"bench: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}", file=sys.stderr)
             sys.exit(2)
@@ -391,14 +420,14 @@ def main():
     def max_over_ranks(*vals):
         if world == 1:
             return vals
-        x = torch.tensor(vals, dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
+        x = torch.tensor(vals, dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(x, op=dist.ReduceOp.MAX)
         return tuple(float(v) for v in x)
 
     def sum_over_ranks(*vals):
         if world == 1:
             return vals
-        x = torch.tensor(vals, dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
+        x = torch.tensor(vals, dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(x, op=dist.ReduceOp.SUM)
         return tuple(float(v) for v in x)
 
@@ -417,15 +446,17 @@ def main():
     for _ in range(args.steps):
         one_step(t)
         t += 1
-    gather_s = None
+    gather_s, gather_exact = None, None
     if rollout:
         rec["i"] = -1
-        if world > 1:  # rollout rows of every rank to rank 0 (RCCL gather over xGMI)
+        if use_pg:  # rollout rows of every rank to rank 0 (RCCL gather over xGMI)
             torch.cuda.synchronize()
             tg = time.perf_counter()
-            shard.gather_rollouts(rows if args.dist_backend == "nccl" else rows.cpu(), dst=0)
+            got = shard.gather_rollouts(rows if backend == "nccl" else rows.cpu(), dst=0)
             torch.cuda.synchronize()
             gather_s = time.perf_counter() - tg
+            if world == 1:  # one rank: the gathered rows are this rank's, bit for bit
+                gather_exact = bool(torch.equal(got.to(rows.device), rows))
     sync()
     dt = time.perf_counter() - t0
     (dt,) = max_over_ranks(dt)
@@ -583,8 +614,11 @@ def main():
                        "parallelism": f"env-sharded x{world} (no per-step collective)"},
             "steady_state": steady,
             "other_solver": other_solver,
-            "dist": {"world_size": world, "backend": (args.dist_backend if world > 1 else None),
-                     "launcher": launcher, "rollout_gather_s": gather_s},
+            "dist": {"world_size": world, "backend": (backend if use_pg else None),
+                     "launcher": launcher, "rollout_gather_s": gather_s,
+                     "rollout_gather_bytes": (int(rows.numel() * rows.element_size() * world) if gather_s is not None
+                                              else None),
+                     "rollout_gather_exact": gather_exact},
             "roofline": roof, "cpu_baseline": cpu,
             "validity": {"state_finite": finite, "envs_status_nonzero": nbad,
                          "library": build.library_info()},
@@ -592,7 +626,7 @@ def main():
         print(json.dumps(line), flush=True)
         if not finite:
             print("bench: non-finite simulation state after the timed region", file=sys.stderr)
-    if world > 1:
+    if use_pg:
         dist.barrier()
         dist.destroy_process_group()
     if not finite:

@@ -18,6 +18,7 @@ SOURCES = ["soarm_sim.hip", "koopman_mpc.hip", "soarm_cpu.hip"]
 # translation units compiled for the host only (the CPU backend: no kernels)
 HOST_ONLY = {"soarm_cpu.hip"}
 HEADERS = ["dmodel.h", "soarm_kernels.h", "soarm_step.h", "soarm_collide.h", "soarm_pgs.h", "soarm_newton.h",
+           "soarm_substep.h",
            "soarm_env.h", "sim_internal.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # -fno-slp-vectorize: the per-lane algebra gains nothing from v_pk_* packing; the

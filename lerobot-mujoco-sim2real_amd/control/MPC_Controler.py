@@ -149,6 +149,17 @@ class MPCController:
             action = torch.empty((n, self.u_dim), dtype=torch.float32, device=self.device)
         z0 = z0.contiguous()
         window = window.contiguous()
+        # k_bilinear reads raw pointers: float64 z0 [nz, n], a window of exactly H rows [H, nz, n]
+        # (short tails are zero-padded by the caller, lifted_window), float64 u_prev [u_dim, n] and a
+        # float32 action [n, u_dim], all contiguous on this device -- anything else is refused here
+        dev = torch.device(self.device) if not isinstance(self.device, torch.device) else self.device
+        want = {"z0": (z0, torch.float64, (self.Nkoopman, n)), "window": (window, torch.float64, (self.H, self.Nkoopman, n)),
+                "u_prev": (u_prev, torch.float64, (self.u_dim, n)), "action": (action, torch.float32, (n, self.u_dim))}
+        for name, (t, dt, shape) in want.items():
+            if t.dtype != dt or tuple(t.shape) != shape or not t.is_contiguous() or t.device.type != "cuda" or \
+                    (dev.index is not None and t.device.index != dev.index):
+                raise ValueError(f"step_bilinear: {name} must be a contiguous {dt} tensor of shape {shape} on {dev}; "
+                                 f"got {t.dtype} {tuple(t.shape)} on {t.device} (contiguous: {t.is_contiguous()})")
         abi.check(self.lib, self.lib.sim_koopman_bilinear_step(self._h, n, _ptr(z0), _ptr(window), _ptr(u_prev),
                                                                _ptr(action), self._stream()))
         return action

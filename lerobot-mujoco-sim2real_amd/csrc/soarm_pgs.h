@@ -139,78 +139,122 @@ constexpr int XS_LIST = SIM_MAXCON;           // ext[0, XS_LIST): the env's cont
 constexpr int XS_EXT = XS_LIST + 98;           // + extra-slot scratch beyond the limit list
 enum { L_DOF = 0, L_SGN = 1, L_AREF = 2, L_R = 3, L_ARD = 4, L_IARD = 5, L_FRC = 6 };
 
-// ---- Wide block sweep (PGS, scene with a free body; the 4-wave workgroup of k_substep).
-// The pure block's ~95 Gauss-Seidel sweeps over the 16 pyramid edges of the cube's 4 resting
-// contacts are most of a pure wave's time, and at 4096 envs the quad layout (4 lanes per env,
-// 16 envs per wave) leaves 3 of a CU's 4 SIMDs idle.  The wide kernel adds 3 helper waves per
-// 16 envs: wave 0 runs the per-env code as before; once the arm's rows retire (ysweeps), it
-// hands the block to all 4 waves through LDS, and the remaining sweeps run with one lane per
-// edge -- 4 envs x 16 lanes per wave.  Lane r of an env holds edge r's scaled residual
-// s_r = -res_r / ARdiag_r, its force f_r and row r of the scaled edge-space Delassus matrix
-// C[r][q] = -(J_r M^-1 J_q' + R_r delta_rq) / ARdiag_r (the quad sweep's C01/C23).  Step q of a
-// sweep: every lane forms max(s, -f) (the projected step, valid in lane q), lane q's value is
-// broadcast within the 16-lane row (DPP row_newbcast), every lane moves its residual by C[r][q]
-// times it, and lane q adds it to its force: MuJoCo's row order, one row at a time.  The sweep's
-// improvement (mj_solPGS's stopping test) is its exact total: with r = A f + b,
-// cost(f0) - cost(f1) = sum_r ARdiag_r / 2 (f1 - f0)_r (s0 + s1)_r, summed over the row.
-constexpr int WIDE_R = 16;       // block edges = lanes per env in the wide sweep
-constexpr int WIDE_COLS = 16;    // envs per workgroup
-enum { WIDE_WORK = 1, WIDE_EXIT = 2, WIDE_GEOM = 3 };
-struct WideLds {
-  float qpos[WIDE_COLS][SIM_MAXQ];     // WIDE_GEOM: the new positions whose geom poses the helpers write
-  float C[WIDE_COLS][WIDE_R][WIDE_R];  // [env][row][step]
-  float s[WIDE_COLS][WIDE_R], f[WIDE_COLS][WIDE_R], hd[WIDE_COLS][WIDE_R];
-  int it[WIDE_COLS];                   // first sweep index (>= iterations: nothing to do)
-  int flag;
-};
+// ---- Row-space PGS (the RS kernel: k_substep<..., RS>, 16 lanes per env, 4 envs per wave).
+// MuJoCo's mj_solPGS sweeps the dual on the dense matrix AR = J M^-1 J' + R (efc_AR): row i's
+// residual is AR_i f + b_i, its force steps by -res / AR_ii and is projected (frictionloss
+// rows into [-fl, fl], limit rows and pyramid edges to f >= 0), rows in order.  The RS kernel
+// holds that system directly: lane r of an env's 16-lane DPP row owns constraint rows r
+// (slot A) and 16 + r (slot B) -- every frictionloss, limit and pyramid-edge row, from the
+// first sweep to the last -- with the row's scaled residual s_r = -res_r / AR_rr and its row of
+// the scaled matrix C[r][q] = -AR_rq / AR_rr (C[r][r] = -1) in registers.  Step q of a sweep:
+// the projected step d = clamp(s_q, lo_q - f_q, hi_q - f_q) is formed from lane q's residual by
+// a DPP row broadcast fused into the max (v_max_f32_dpp row_newbcast), every lane moves its
+// residuals by C[r][q] d (one packed FMA per slot), and the step's bound registers (-f_q,
+// kept broadcast in every lane of the env) take it: two dependent instructions per row.
+// The improvement of mj_solPGS's stopping test is the sweep's exact cost change: with
+// res = AR f + b, cost(f0) - cost(f1) = sum_r AR_rr / 2 (f1 - f0)_r (s0 + s1)_r, and each
+// row's force change over the sweep comes from a second accumulator beside s that takes
+// the off-diagonal steps only (u_r = sum_{q != r} C_rq d_q, so Delta f_r = u_r - Delta s_r).
+constexpr int RS_MAXROW = 32;               // rows of one env (2 slots x 16 lanes)
+constexpr int RS_WROW = 12;                 // floats per row of W = M^-1 J' in LDS (NV <= 12)
+constexpr int RS_WENV = RS_MAXROW * RS_WROW + 4;  // per env (+4: the 4 envs of a wave on distinct banks)
+constexpr int RS_EPW = 4;                   // envs per wave (workgroup)
 template <int Q>
 DEVI float rowbcast(float x) {  // lane Q of each 16-lane row
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x150 + Q, 0xF, 0xF, true));
 }
 // sum over the 16-lane row, bit-identical in all 16 lanes (the stop test must agree)
+// (the permutes fused into the adds, v_add_f32_dpp; every stage adds two values that are equal
+// bit for bit within each pair of partners -- quad xor 1, quad xor 2, the 8-lane mirror, the
+// 16-lane mirror -- and fp addition is commutative, so all 16 lanes end with the same bits)
 DEVI float rowsum16(float x) {
-  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xF, 0xF, false));   // quad xor 1
-  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x4E, 0xF, 0xF, false));   // quad xor 2
-  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x124, 0xF, 0xF, false));  // row_ror:4
-  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x128, 0xF, 0xF, false));  // row_ror:8
-  return rowbcast<0>(x);
+  asm("s_nop 1\n\tv_add_f32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "+v"(x));
+  asm("s_nop 1\n\tv_add_f32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf" : "+v"(x));
+  asm("s_nop 1\n\tv_add_f32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf" : "+v"(x));
+  asm("s_nop 1\n\tv_add_f32_dpp %0, %0, %0 row_mirror row_mask:0xf bank_mask:0xf" : "+v"(x));
+  return x;
 }
-// one row step: the projected step max(s, -f) is broadcast from lane Q, every row moves by its
-// C entry, lane Q's force takes the step (oh: one-hot of the lane's row)
-template <int Q>
-DEVI void wide_step(const float (&Cr)[WIDE_R], const float (&oh)[WIDE_R], float& s, float& f) {
-  float cand;
-  asm("v_max_f32_e64 %0, %1, -%2" : "=v"(cand) : "v"(s), "v"(f));  // max(s, -f), see max_neg
-  s = fmaf(Cr[Q], rowbcast<Q>(cand), s);
-  f = fmaf(oh[Q], cand, f);
+// max(lane Q's x, b): the row broadcast fused into the max (VOP2 DPP).  A DPP read of a VGPR needs
+// 2 wait states after the VALU write of it, and the compiler's hazard recognizer does not look into
+// inline asm: the caller states how many instructions (NOPS = 2 - that count) must be padded.
+template <int Q, int NOPS = 2>
+DEVI float max_bcast(float x, float b) {
+  float r;
+  if constexpr (NOPS >= 2)
+    asm volatile("s_nop 1\n\tv_max_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "=v"(r) : "v"(x), "v"(b), "i"(Q));
+  else if constexpr (NOPS == 1)
+    asm volatile("s_nop 0\n\tv_max_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "=v"(r) : "v"(x), "v"(b), "i"(Q));
+  else
+    asm volatile("v_max_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "=v"(r) : "v"(x), "v"(b), "i"(Q));
+  return r;
 }
-template <int... Qs>
-DEVI void wide_sweep(const float (&Cr)[WIDE_R], const float (&oh)[WIDE_R], float& s, float& f,
-                     std::integer_sequence<int, Qs...>) {
-  (wide_step<Qs>(Cr, oh, s, f), ...);
+DEVI float vmin(float a, float b) {  // v_min without the IEEE-mode canonicalising of fminf
+  float r;
+  asm("v_min_f32_e32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
 }
-// The wide sweeps of the envs handed over in W, by every thread t of the workgroup (env t / 16,
-// edge t % 16); each env continues from its own sweep index until its stopping test passes.
-DEVI void wide_sweeps(const DModel& m, WideLds& W, int t) {
-  const int c = t >> 4, r = t & 15;
-  float Cr[WIDE_R], oh[WIDE_R];
-#pragma unroll
-  for (int q = 0; q < WIDE_R; q++) Cr[q] = W.C[c][r][q], oh[q] = q == r ? 1.f : 0.f;
-  float s = W.s[c][r], f = W.f[c][r];
-  const float hd = W.hd[c][r], scale = m.pgs_scale, tol = m.tolerance;
-  int it = min(max(W.it[c], 0), m.iterations);  // (bounded whatever the LDS holds: the loop always ends)
-  const int iters = m.iterations;
-  for (; it < iters; it++) {
-    const float s0 = s, f0 = f;
-    wide_sweep(Cr, oh, s, f, std::make_integer_sequence<int, WIDE_R>{});
-    const float imp = rowsum16(hd * (f - f0) * (s0 + s));
-    if (imp * scale < tol) {
-      it++;
-      break;
-    }
+// f(std::integral_constant<int, i>) for i = 0 .. N-1 (compile-time lane / register indices)
+template <class F, int... Is>
+DEVI void sfor_impl(F&& f, std::integer_sequence<int, Is...>) {
+  (f(std::integral_constant<int, Is>{}), ...);
+}
+template <int N, class F>
+DEVI void sfor(F&& f) {
+  sfor_impl(f, std::make_integer_sequence<int, N>{});
+}
+// Row layout of one wave's RS solve (compile time).  Steps in mj_solPGS order: the NA dof
+// frictionloss rows (F), then the edges of up to KAT arm-only contacts (AT: arm on the table /
+// floor, arm self-contacts), of up to 4 contacts on the free body alone (CT: the cube on the
+// table), of up to KAC contacts between the arm and the free body (AC) -- the order the pair
+// list produces (arm-only pairs precede the free body's, its world pairs precede its arm pairs).
+// Rows touching arm dofs (F, AT, AC) live in slot B, the CT edges in slot A: M is block diagonal,
+// so an F / AT step moves slot B alone and a CT step slot A alone (and slot B's AC rows when the
+// wave has an AC contact); a step therefore costs one residual update where the systems decouple.
+// Steps an env has no row for are zero rows (exact no-ops).
+template <int NA, int KAT, int KAC>
+struct RsLayout {
+  static_assert(NA + 4 * (KAT + KAC) <= 16, "slot B holds the F, AT and AC rows");
+  static constexpr int CT0 = NA + 4 * KAT, AC0 = CT0 + 16, NS = AC0 + 4 * KAC;
+  static constexpr int slot(int q) { return (q >= CT0 && q < AC0) ? 0 : 1; }
+  static constexpr int lane(int q) { return q < CT0 ? q : q < AC0 ? q - CT0 : q - 16; }
+  static constexpr bool upd_a(int q) { return q >= CT0; }                 // CT, AC
+  static constexpr bool upd_b(int q) { return q < CT0 || q >= AC0 || KAC > 0; }
+  // instructions after step q's write of slot sl before step q+1 (see rs_sweep's order)
+  static constexpr int after_write(int q, int sl) {
+    return (sl == 0 ? upd_a(q) : upd_b(q)) ? ((upd_a(q) && upd_b(q)) ? 1 : 0) + 1 + (q < NA ? 1 : 0) : 2;
   }
-  W.f[c][r] = f;
-  if (r == 0) W.it[c] = it;
+};
+// one sweep of the row-space PGS (see above): s = (residual, off-diagonal accumulator) per slot,
+// C = (C, G) pairs per step, NF = lo - f of every row, NH = hi - f of the NA frictionloss rows (the
+// others have hi = +inf).  Instruction order is pinned (sched_barrier): a DPP op waits for every
+// VALU op in flight, so a step is its broadcast-max, the residual update of the slot the NEXT step
+// broadcasts from, then the other slot's update and the bound updates -- which are also the 2 wait
+// states the next broadcast needs after that write (padded with s_nop where a step has fewer)
+template <int NA, class LY>
+DEVI void rs_sweep(f2& sA, f2& sB, const f2 (&CA)[LY::NS], const f2 (&CB)[LY::NS], float (&NF)[LY::NS],
+                   float (&NH)[NA]) {
+  sfor<LY::NS>([&](auto qc) {
+    constexpr int Q = decltype(qc)::value;
+    constexpr int SL = LY::slot(Q), LN = LY::lane(Q);
+    constexpr int after = Q == 0 ? 0 : LY::after_write(Q - 1, SL);
+    float d = max_bcast<LN, (after >= 2 ? 0 : 2 - after)>(SL == 0 ? sA.x : sB.x, NF[Q]);
+    if constexpr (Q < NA) d = vmin(d, NH[Q]);
+    __builtin_amdgcn_sched_barrier(0);
+    constexpr int NSL = Q + 1 < LY::NS ? LY::slot(Q + 1) : SL;  // the next step's source slot
+    auto upd = [&](auto slc) {
+      if constexpr (decltype(slc)::value == 0) {
+        if constexpr (LY::upd_a(Q)) sA = __builtin_elementwise_fma(CA[Q], f2{d, d}, sA);
+      } else {
+        if constexpr (LY::upd_b(Q)) sB = __builtin_elementwise_fma(CB[Q], f2{d, d}, sB);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    upd(std::integral_constant<int, NSL>{});
+    upd(std::integral_constant<int, 1 - NSL>{});
+    NF[Q] -= d;
+    if constexpr (Q < NA) NH[Q] -= d;
+    __builtin_amdgcn_sched_barrier(0);
+  });
 }
 
 // Per-env LDS state, [field][column]: one column per env of the workgroup (64 / lanes per
@@ -224,7 +268,7 @@ struct RowLds {
   int lane;     // thread in the workgroup
   int col;      // this env's column
   int cols;     // columns (envs per workgroup)
-  WideLds* wide = nullptr;  // the wide block sweep's hand-over area (4-wave PGS kernel), else null
+  float* rsw = nullptr;  // RS kernel: [env column][RS_WENV] rows of W = M^-1 J' (row-space PGS), else null
   DEVI float& at(int c, int f) const { return a[(c * CF + f) * cols + col]; }
   DEVI float& lm(int l, int f) const { return lim[(l * LF + f) * cols + col]; }
   DEVI float& lraw(int k) const { return lim[k * cols + col]; }
@@ -426,7 +470,7 @@ namespace soarm {
 // soarm_newton.h), sets S.qacc / S.fcon.
 // Contacts are read straight from the collide output (pair mask + cbuf, pair
 // order).  Returns the number of contacts used.
-template <int NA, int NF, bool CON, int SOL = SIM_SOL_PGS, bool WIDE = false>
+template <int NA, int NF, bool CON, int SOL = SIM_SOL_PGS, bool RS = false>
 DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const int* __restrict__ ccount,
                            const uint32_t* __restrict__ pmask, int n, int e, const RowLds& L,
                            const ContactRows<NA, NF>& cr, const PairMask& pm) {
@@ -439,6 +483,11 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   if constexpr (!NEWT) Mi.build(S);
   PSTAMP(6);
 
+  // RS kernel: whether every env of the wave takes the row-space solve (decided once the contacts
+  // are listed: no overflow rows, at most RS_MAXROW rows); it then needs neither the records'
+  // Gram blocks / edge ARdiag nor the warm start below (rs_solve builds its own)
+  bool rs_fast = false;
+  int rs_nat = 0, rs_nct = 0, rs_nac = 0;  // contacts per category (RsLayout): arm-only, free body alone, both
   // ---- dof frictionloss rows (MuJoCo row order: all of them first)
   float ff[NA], fa[NA], fR[NA], fhD[NA], fiD[NA];
 #pragma unroll
@@ -566,8 +615,8 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       // width (jd is zero on the halves the contact does not touch; branch-free code
       // avoids running both sides of a divergent flag test) unless no lane's contact
       // touches the arm: then the free-body half alone (diagonal M^-1).
-      float W0[NV], W1[NV], W2[NV], G[6];
-      if constexpr (!NEWT) {
+      float W0[NV], W1[NV], W2[NV], G[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (!NEWT && !rs_fast) {
         const bool arm_any = NF == 0 || !__all(!ta);
         Mi.mul(jd[0], W0, arm_any, true);
         Mi.mul(jd[1], W1, arm_any, true);
@@ -580,7 +629,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
 #pragma unroll
       for (int i = 0; i < NV; i++)
         vq[0] += jd[0][i] * S.qvel[i], vq[1] += jd[1][i] * S.qvel[i], vq[2] += jd[2][i] * S.qvel[i];
-      if constexpr (!NEWT)
+      if (!NEWT && !rs_fast)
         if (lds) {
 #pragma unroll
           for (int k2 = 0; k2 < 6; k2++) wrec(c, F_GRAM + k2, G[k2], split);
@@ -596,7 +645,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
         const float ar = -KB1 * vel - KB0 * imp * (cdist - margin);
         if (lds) {
           wrec(c, F_AREF + ed, ar, split);
-          if constexpr (!NEWT) {
+          if (!NEWT && !rs_fast) {
             wrec(c, F_HARD + ed, 0.5f * ard, split);
             wrec(c, F_IARD + ed, 1.f / ard, split);
           }
@@ -652,13 +701,33 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
         build_row(c, rw, m.pair_body1[p], m.pair_body2[p], S.fric >= 0.f ? S.fric : m.pair_friction[p],
                   m.pair_tran[p], m.pair_margin[p], m.pair_KB[p][0], m.pair_KB[p][1], si, split);
       };
+      if constexpr (RS) {  // the contact categories of the RS layout (RsLayout): AT* CT* AC* in list order
+        bool ok = nlim == 0 && ncon <= LDS_CON;
+        int stage = 0;
+        for (int c = 0; c < ncon; c++) {
+          const int p = __float_as_int(L.ex(c)) >> 3;
+          const int b1 = m.pair_body1[p], b2 = m.pair_body2[p];
+          const bool ta = (b1 >= 2 && b1 < 2 + NA) || (b2 >= 2 && b2 < 2 + NA), tf = b1 >= 2 + NA || b2 >= 2 + NA;
+          const int cat = tf ? (ta ? 2 : 1) : 0;
+          ok = ok && cat >= stage;
+          stage = cat;
+          rs_nat += cat == 0, rs_nct += cat == 1, rs_nac += cat == 2;
+        }
+        // the layouts instantiated: (KAT, KAC) = (0, 0) the cube resting alone, (1, 0) plus one
+        // arm-only contact, (0, 1) plus one arm-cube contact; other waves take the v-form sweeps
+        ok = ok && rs_nct <= 4 && rs_nat <= 1 && rs_nac <= 1;
+        rs_fast = __all(ok) && !(__any(rs_nat >= 1) && __any(rs_nac >= 1));
+      }
       const int nlds = ncon < LDS_CON ? ncon : LDS_CON;
-      for (int c0 = 0; c0 < nlds; c0 += 4) {
-        const int c = c0 + (L.lane & 3);
+      constexpr int SPL = RS ? 16 : 4;  // the RS kernel: the env's 16 lanes split the build
+      for (int c0 = 0; c0 < nlds; c0 += SPL) {
+        const int c = c0 + (L.lane & (SPL - 1));
         if (c < nlds) build_listed(c, true);
       }
       wave_sync();  // the quad's records, written by its 4 lanes
       for (int c = LDS_CON; c < ncon; c++) build_listed(c, false);
+    } else if constexpr (RS) {
+      rs_fast = true;  // no contacts: the NA frictionloss rows and the active limits
     }
   } else if constexpr (CON) {
     if (ccount != nullptr) {
@@ -857,7 +926,18 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   // ---- projected Gauss-Seidel sweeps (mj_solPGS's improvement criterion, scaled by the model
   // constant 1 / (meaninertia * max(1, nv)), meaninertia = trace(M(qpos0)) / nv)
   const float scale = m.pgs_scale;
-  if (L.keep) {  // park what only the post-solve stages need (restored below)
+  if constexpr (RS) {  // the RS kernel: the damped Euler step's factor instead (Sim::damp_factor)
+    S.damp_factor();
+    int k = 0;
+#pragma unroll
+    for (int i = 0; i < NA * (NA + 1) / 2; i++) L.kp(k++) = S.LH[i];
+#pragma unroll
+    for (int i = 0; i < NA; i++) L.kp(k++) = S.DHi[i];
+#pragma unroll
+    for (int i = 0; i < 6 * NF; i++) L.kp(k++) = S.kf[i / 6][i % 6];
+#pragma unroll
+    for (int i = 0; i < 3; i++) L.kp(k++) = S.ee[i];
+  } else if (L.keep) {  // park what only the post-solve stages need (restored below)
     int k = 0;
 #pragma unroll
     for (int i = 0; i < NA * (NA + 1) / 2; i++) L.kp(k++) = S.MA[i];
@@ -1048,7 +1128,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   }
   float cfo[FC][4], ccf[FC][12];
   int cslot[FC];
-  if constexpr (NF == 1 && CON) {
+  if (NF == 1 && CON && !rs_fast) {
 #pragma unroll
     for (int k = 0; k < FC; k++) {
       const bool on = k < nrun;
@@ -1814,44 +1894,6 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   // extras in row order: F = the first of two (arm-only), E = the last one
   const int cE = npost >= 1 ? xidx(npost - 1) : LDS_CON, cF = npost == 2 ? xidx(0) : LDS_CON;
   const bool hasE = npost >= 1, hasF = npost == 2;
-  // The wide kernel's hand-over round (see WideLds).  Wave 0 writes the rows, the 4 waves sweep,
-  // wave 0 reads the forces back; the helper waves wait at the workgroup barrier between rounds
-  // (a solve may run none).  Each quad lane writes its block contact's 4 rows (scaled residuals,
-  // forces, ARdiag/2, its rows of C).  Called with every lane of wave 0 active (a wave-uniform
-  // call site): the round's barriers and wave 0's own share of the sweeps (threads 0-63 = the
-  // edges of envs 0-3, whose lanes belong to quads 0-15) need all 64 lanes.  part: this env
-  // takes part; the others hand over their state with a first sweep index of `iterations`
-  // (nothing to do) and read nothing back.
-  auto wide_round = [&](int it0, auto pk, bool part) {
-    WideLds& W = *L.wide;
-    if constexpr (decltype(pk)::value && QUAD) {
-      const int col = L.col;
-#pragma unroll
-      for (int ed = 0; ed < 4; ed++) {
-        const int row = 4 * sub + ed;
-        W.s[col][row] = ed == 0 ? ro01.x : ed == 1 ? ro01.y : ed == 2 ? ro23.x : ro23.y;
-        W.f[col][row] = sub == 0 ? cfo[0][ed] : sub == 1 ? cfo[1][ed] : sub == 2 ? cfo[2][ed] : cfo[3][ed];
-        W.hd[col][row] = sub == 0 ? yhd[0][ed] : sub == 1 ? yhd[1][ed] : sub == 2 ? yhd[2][ed] : yhd[3][ed];
-#pragma unroll
-        for (int j = 0; j < FC; j++)
-#pragma unroll
-          for (int d = 0; d < 4; d++) {
-            const f2 cc = ed < 2 ? C01[j][d] : C23[j][d];
-            W.C[col][row][4 * j + d] = (ed & 1) ? cc.y : cc.x;
-          }
-      }
-      if (sub == 0) W.it[col] = part ? it0 : m.iterations;
-      W.flag = WIDE_WORK;
-      __syncthreads();
-      wide_sweeps(m, W, L.lane);
-      __syncthreads();
-      if (!part) return;
-#pragma unroll
-      for (int k = 0; k < FC; k++)
-#pragma unroll
-        for (int ed = 0; ed < 4; ed++) cfo[k][ed] = W.f[col][4 * k + ed];
-    }
-  };
   auto ysweeps = [&](auto ext, auto coupled, auto ext2) {
     yblock_setup();
     using PK = std::integral_constant<bool, QUAD>;
@@ -2003,15 +2045,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
         }
         vpin(ro01), vpin(ro23);
       }
-      if constexpr (WIDE) {  // the 4-wave kernel sweeps the block one lane per edge
-        if (__any(!done)) {  // (wave-uniform)
-          const bool part = !done;
-          wide_round(it, std::bool_constant<PK::value>{}, part);
-#ifdef SOARM_PHASE_PROF
-          if (part) it = L.wide->it[L.col] - 1, done = it + 1 < m.iterations;
-#endif
-        }
-      } else if (!done)
+      if (!done)
         for (; it < m.iterations; it++) {
           float unused = 0.f, unused2 = 0.f;
           if (sweep(std::false_type{}, std::false_type{}, unused, unused2) * scale < m.tolerance) {
@@ -2060,8 +2094,171 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       }
     }
   };
+  // ---- row-space PGS (RS kernel; see RS_MAXROW above).  Rows in mj_solPGS order: the NA dof
+  // frictionloss rows, the active limits, 4 pyramid edges per contact; NRB (compile time) bounds
+  // the rows of every env of the wave (rows past an env's own are zero rows: J = 0, so C's row and
+  // column are 0 and their steps are exact no-ops).  Lane r16 holds rows r16 (slot A) and 16 + r16
+  // (slot B, when NRB > 16).  v: the velocity after the warm start; on return, qacc.
+  auto rs_solve = [&](auto kat_c, auto kac_c) {
+    if constexpr (RS && NF == 1 && CON) {
+      using LY = RsLayout<NA, decltype(kat_c)::value, decltype(kac_c)::value>;
+      constexpr int NS = LY::NS, KAT = decltype(kat_c)::value, KAC = decltype(kac_c)::value;
+      const int r16 = L.lane & 15;
+      float* const Wl = L.rsw + L.col * RS_WENV;
+      // this lane's rows: slot A = CT edge r16, slot B = frictionloss row / AT edge / AC edge r16;
+      // kind 0 frictionloss, 1 pyramid edge, -1 none; c, ed: the edge's contact and edge index;
+      // qA / qB: the rows' step indices (their W rows in LDS)
+      const int cA = rs_nat + (r16 >> 2), qA = LY::CT0 + r16;
+      const int kindA = (r16 >> 2) < rs_nct ? 1 : -1;
+      int kindB = -1, cB = 0;
+      if (r16 < NA) {
+        kindB = 0;
+      } else if (r16 < LY::CT0) {
+        cB = (r16 - NA) >> 2, kindB = cB < rs_nat ? 1 : -1;
+      } else if (r16 < LY::CT0 + 4 * KAC) {
+        const int k = (r16 - LY::CT0) >> 2;
+        cB = rs_nat + rs_nct + k, kindB = k < rs_nac ? 1 : -1;
+      }
+      const int qB = r16 < LY::CT0 ? r16 : r16 + 16;
+      // row data: J (NV), aref, R, the warm-start force (the warm start above)
+      auto row_of = [&](int kind, int c, int ed, float (&J)[NV], float& ar, float& R, float& f) {
+#pragma unroll
+        for (int i = 0; i < NV; i++) J[i] = 0.f;
+        ar = 0.f, R = 1.f, f = 0.f;
+        if (kind == 0) {  // dof frictionloss row ed: J = e_ed
+#pragma unroll
+          for (int i = 0; i < NA; i++)
+            if (ed == i) J[i] = 1.f, ar = fa[i], R = fR[i], f = ff[i];
+        } else if (kind == 1) {  // pyramid edge J_n +- mu J_t of contact c
+          const float mu = L.at(c, F_MU), s = (ed & 1) ? -mu : mu;
+          const int t = 12 * (1 + (ed >> 1));
+#pragma unroll
+          for (int i = 0; i < NV; i++) J[i] = fmaf(s, L.at(c, t + i), L.at(c, i));
+          ar = L.at(c, F_AREF + ed), R = L.at(c, F_R), f = L.at(c, F_FRC + ed);
+        }
+      };
+      float JA[NV], JB[NV], WA[NV], WB[NV], arA, arB, RA, RB, fA, fB;
+      row_of(kindA, cA, r16 & 3, JA, arA, RA, fA);
+      row_of(kindB, cB, kindB == 0 ? r16 : (r16 - NA) & 3, JB, arB, RB, fB);
+      Mi.mul(JA, WA, false, true);  // (CT rows touch the free body alone)
+      Mi.mul(JB, WB, true, KAC > 0);
+      // W rows to LDS, by step (the 4 copies of a quad write identical values)
+#pragma unroll
+      for (int i = 0; i < NV; i++) Wl[qA * RS_WROW + i] = WA[i];
+      if (qB < NS)
+#pragma unroll
+        for (int i = 0; i < NV; i++) Wl[qB * RS_WROW + i] = WB[i];
+      // AR_rr = J_r W_r + R_r
+      float ardA = RA, ardB = RB;
+#pragma unroll
+      for (int i = 0; i < NV; i++) ardA = fmaf(JA[i], WA[i], ardA), ardB = fmaf(JB[i], WB[i], ardB);
+      const float iA = 1.f / ardA, iB = 1.f / ardB;
+      const float hdA = 0.5f * ardA, hdB = 0.5f * ardB;
+      wave_sync();
+      // the bound registers, broadcast over the env's row: -f_q (edges) and the frictionloss
+      // rows' lo - f, hi - f
+      float NF_[NS], NH_[NA];
+      sfor<NS>([&](auto qc) {
+        constexpr int q = decltype(qc)::value;
+        const float fq = -rowbcast<LY::lane(q)>(LY::slot(q) == 0 ? fA : fB);
+        if constexpr (q < NA) {
+          const float fl = m.dof_frictionloss[q];
+          NF_[q] = fq - fl, NH_[q] = fq + fl;
+        } else {
+          NF_[q] = fq;
+        }
+      });
+      float jvA = -arA, jvB = -arB;
+#pragma unroll
+      for (int i = 0; i < NV; i++) jvA = fmaf(JA[i], v[i], jvA), jvB = fmaf(JB[i], v[i], jvB);
+      f2 sA = f2{-fmaf(RA, fA, jvA) * iA, 0.f}, sB = f2{-fmaf(RB, fB, jvB) * iB, 0.f};
+      // the scaled matrix: C[r][q] = -J_r W_q / AR_rr, C[r][r] = -1, as (C, G) pairs: G is C with a
+      // zero diagonal (the accumulator of the off-diagonal steps); only the blocks a step updates
+      f2 CA[NS], CB[NS];
+      sfor<NS>([&](auto qc) {
+        constexpr int q = decltype(qc)::value;
+        constexpr bool UA = LY::upd_a(q), UB = LY::upd_b(q);
+        f2 a = f2{0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < NV; i++)
+          a = fma2(f2{UA ? JA[i] : 0.f, UB ? JB[i] : 0.f}, splat2(Wl[q * RS_WROW + i]), a);
+        const float ca = -a.x * iA, cb = -a.y * iB;
+        CA[q] = qA == q ? f2{-1.f, 0.f} : f2{ca, ca};
+        CB[q] = qB == q ? f2{-1.f, 0.f} : f2{cb, cb};
+        // (the W rows of two steps in flight at a time: hoisting every step's 12 LDS loads to
+        // the top would hold hundreds of values)
+        if constexpr (q & 1) __builtin_amdgcn_sched_barrier(0);
+      });
+      const float scale = m.pgs_scale, tol = m.tolerance;
+      int iters = m.iterations;
+      asm volatile("" : "+s"(iters));  // (loaded once: the sweeps' asm keeps LICM from hoisting it)
+      bool done = false;
+#ifdef SOARM_PHASE_PROF
+      // (the RS solve's split, in the Newton profiler's slots: PGS builds leave them unused)
+      // [8] setup, [9] sweeps, [10] final qacc, summed over waves; [11] waves; [16] sum of wave sweeps
+      const long long rp0 = clock64();
+      int wsw = 0;
+#endif
+      for (int it = 0; it < iters; it++) {
+#ifdef SOARM_PHASE_PROF
+        wsw = it + 1;
+#endif
+        if (!done) {
+#ifdef SOARM_PHASE_PROF
+          nsweep = it + 1;
+#endif
+          const float s0A = sA.x, s0B = sB.x;
+          sA.y = 0.f, sB.y = 0.f;
+          rs_sweep<NA, LY>(sA, sB, CA, CB, NF_, NH_);
+          // Delta f_r = u_r - Delta s_r; improvement = sum_r AR_rr / 2 Delta f_r (s0 + s1)_r
+          float P = hdA * (sA.y - (sA.x - s0A)) * (s0A + sA.x);
+          P = fmaf(hdB * (sB.y - (sB.x - s0B)), s0B + sB.x, P);
+          done = rowsum16(P) * scale < tol;
+        }
+        if (__all(done)) break;
+      }
+#ifdef SOARM_PHASE_PROF
+      const long long rp1 = clock64();
+#endif
+      // qacc = qacc_smooth + sum_q W_q f_q (NH_ = fl - f on the frictionloss rows, NF_ = -f on the
+      // others): lane i < NV sums dof i, then the row broadcasts it
+      float acc = 0.f;
+      const int di = r16 < NV ? r16 : 0;
+#pragma unroll
+      for (int q = 0; q < NS; q++)
+        acc = fmaf(Wl[q * RS_WROW + di], q < NA ? m.dof_frictionloss[q] - NH_[q] : -NF_[q], acc);
+      sfor<NV>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        v[i] = S.qacc_s[i] + rowbcast<i>(acc);
+      });
+#ifdef SOARM_PHASE_PROF
+      if ((threadIdx.x & 63) == 0) {
+        const long long rp2 = clock64();
+        atomicAdd(&g_newton[8], (unsigned long long)(rp0 - g_pgs_prof[8 * e]));
+        atomicAdd(&g_newton[9], (unsigned long long)(rp1 - rp0));
+        atomicAdd(&g_newton[10], (unsigned long long)(rp2 - rp1));
+        atomicAdd(&g_newton[11], 1ull);
+        atomicAdd(&g_newton[16], (unsigned long long)wsw);
+      }
+#endif
+    }
+  };
   // wave-uniform choice: separate copies of the loop, no branch inside the sweep
-  if (ypure) {
+  if constexpr (RS) {
+    if (rs_fast) {
+      using Z = std::integral_constant<int, 0>;
+      using O = std::integral_constant<int, 1>;
+      const int kat = __any(rs_nat >= 1) ? 1 : 0, kac = __any(rs_nac >= 1) ? 1 : 0;
+      if (kac == 1)
+        rs_solve(Z{}, O{});
+      else if (kat == 1)
+        rs_solve(O{}, Z{});
+      else
+        rs_solve(Z{}, Z{});
+    } else {
+      sweeps(std::false_type{});
+    }
+  } else if (ypure) {
     ysweeps(std::false_type{}, std::false_type{}, std::false_type{});
   } else if (yext && yext2 && ycoupled) {
     ysweeps(std::true_type{}, std::true_type{}, std::true_type{});
@@ -2076,14 +2273,24 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   } else {
     sweeps(std::false_type{});
   }
-  if constexpr (NF == 1 && CON) {  // the block's forces back to their records (for J' f)
+  if (NF == 1 && CON && !rs_fast) {  // the block's forces back to their records (for J' f)
 #pragma unroll
     for (int k = 0; k < FC; k++)
       if (k < nrun)
 #pragma unroll
         for (int ed = 0; ed < 4; ed++) L.at(c0 + k, F_FRC + ed) = cfo[k][ed];
   }
-  if (L.keep) {
+  if constexpr (RS) {
+    int k = 0;
+#pragma unroll
+    for (int i = 0; i < NA * (NA + 1) / 2; i++) S.LH[i] = L.kp(k++);
+#pragma unroll
+    for (int i = 0; i < NA; i++) S.DHi[i] = L.kp(k++);
+#pragma unroll
+    for (int i = 0; i < 6 * NF; i++) S.kf[i / 6][i % 6] = L.kp(k++);
+#pragma unroll
+    for (int i = 0; i < 3; i++) S.ee[i] = L.kp(k++);
+  } else if (L.keep) {
     int k = 0;
 #pragma unroll
     for (int i = 0; i < NA * (NA + 1) / 2; i++) S.MA[i] = L.kp(k++);
@@ -2114,6 +2321,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
     S.qacc[i] = v[i];
     S.fcon[i] = 0.f;
   }
+  if constexpr (CON && RS) return ncon;  // (the RS kernel's Euler step needs qacc alone: integrate_qacc)
   if constexpr (CON) {
     // qacc = qacc_smooth + M^-1 J' f, so J' f = M qacc - qfrc_smooth (M qacc_smooth = qfrc_smooth):
     // the Euler step's right-hand side qfrc_smooth + qfrc_constraint is M qacc.  One 6x6 product

@@ -337,6 +337,12 @@ struct Sim {
 #pragma unroll
       for (int i = 0; i < NV; i++) qa[i] = qacc[i];
     }
+    advance(qa);
+  }
+  // qvel += h a; qpos += h qvel (free bodies: quaternion by the angular velocity); warm start = qacc
+  HDI void advance(const float (&qa)[NV]) {
+    const DModel& m = *mp;
+    const float h = m.timestep;
 #pragma unroll
     for (int i = 0; i < NV; i++) qvel[i] += h * qa[i];
 #pragma unroll
@@ -362,6 +368,50 @@ struct Sim {
     }
 #pragma unroll
     for (int i = 0; i < NV; i++) warm[i] = qacc[i];
+  }
+
+  // The implicit-damping Euler step in two halves (the RS contact kernel): (M + h D) a = qfrc_smooth
+  // + qfrc_constraint = M qacc, so a = qacc - (M + h D)^-1 h D qacc.  damp_factor() factors H = M + h D
+  // before the constraint solve (arm block: LDL' into LH / DHi; free bodies: their diagonal blocks,
+  // a_i = qacc_i M_ii / (M_ii + h d_i)), integrate_qacc() finishes the step from qacc alone -- no
+  // mass matrix, no qfrc_smooth and no factorization after the solve.
+  float LH[NLA], DHi[NA], kf[NF > 0 ? NF : 1][6];
+  HDI void damp_factor() {
+    const DModel& m = *mp;
+    const float h = m.timestep;
+#pragma unroll
+    for (int k = 0; k < NLA; k++) LH[k] = MA[k];
+#pragma unroll
+    for (int i = 0; i < NA; i++) LH[i * (i + 1) / 2 + i] += h * m.dof_damping[i] * dscale;
+    ldl_factor<NA>(LH, DHi);
+#pragma unroll
+    for (int f = 0; f < NF; f++)
+#pragma unroll
+      for (int i = 0; i < 6; i++) {
+        const float mi = MF[f][i * (i + 1) / 2 + i];
+        kf[f][i] = mi / (mi + h * m.dof_damping[NA + 6 * f + i] * dscale);
+      }
+  }
+  HDI void integrate_qacc() {
+    const DModel& m = *mp;
+    const float h = m.timestep;
+    float qa[NV];
+    if (m.eulerdamp) {
+      float y[NA], x[NA];
+#pragma unroll
+      for (int i = 0; i < NA; i++) y[i] = h * m.dof_damping[i] * dscale * qacc[i];
+      ldl_solve<NA>(LH, DHi, x, y);
+#pragma unroll
+      for (int i = 0; i < NA; i++) qa[i] = qacc[i] - x[i];
+#pragma unroll
+      for (int f = 0; f < NF; f++)
+#pragma unroll
+        for (int i = 0; i < 6; i++) qa[NA + 6 * f + i] = kf[f][i] * qacc[NA + 6 * f + i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < NV; i++) qa[i] = qacc[i];
+    }
+    advance(qa);
   }
 
   // mj_resetData for this env (MuJoCo's auto-reset on a bad state)

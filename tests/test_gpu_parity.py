@@ -283,13 +283,13 @@ def _bench_states(name, n, steps, seed=0, nthreads=8):
     return cm, orc, f32(st), prm
 
 
-@pytest.mark.parametrize("wide", ["0", "1"])
-def test_one_substep_bench_state_mixed_contacts(gpu_lib, wide, monkeypatch):
+@pytest.mark.parametrize("rs", ["1", "0"])
+def test_one_substep_bench_state_mixed_contacts(gpu_lib, rs, monkeypatch):
     """One substep from late bench states (t = 120 env-steps of the contact workload): the
     cube's 4 resting contacts plus, in some envs, arm-table contacts (the waves that take
-    the general contact paths).  wide = "1": the opt-in 4-wave kernel (SOARM_WIDE=1, 512 envs
-    = 32 whole workgroups), whose block sweeps run one lane per pyramid edge."""
-    monkeypatch.setenv("SOARM_WIDE", wide)
+    the general contact paths).  rs = "1": the row-space kernel (the default; soarm_pgs.h
+    RsLayout), "0": the quad kernel (SOARM_RS=0)."""
+    monkeypatch.setenv("SOARM_RS", rs)
     cm, orc, st, _ = _bench_states("contact", 512, 120)
     S = make_sim(cm, 512)
     st["ncon"][:] = 0

@@ -355,6 +355,7 @@ def test_step_with_applied_force(gpu_lib, arm_model_nocontact, arm_model):
         a = rng.uniform(-0.5, 0.5, (n, 5)).astype(np.float32)
         og = to_np(S.step(a))
         app64 = app.astype(np.float32).astype(np.float64)
+        st0 = {k: v.copy() for k, v in st.items()}  # (Oracle.step advances st in place)
         oc = orc.step(st, a.astype(np.float64), applied=app64)
         err = np.abs(og - oc).max(1)  # per env
         # a missing or mis-scaled applied force moves every env by ~h^2 |f| / M ~ 1e-3; the bulk is
@@ -362,10 +363,11 @@ def test_step_with_applied_force(gpu_lib, arm_model_nocontact, arm_model):
         # test_gpu_parity's shadowing tests) amplify fp32 rounding within one env-step: they are
         # held to the oracle's own sensitivity there -- the same env-step from the state with qvel
         # perturbed by one fp32 ulp (the shadowing envelope) -- and p99.9 to 5e-4.
-        pert = {k: v.copy() for k, v in st.items()}
+        pert = {k: v.copy() for k, v in st0.items()}  # the same env-step, from the perturbed start state
         pert["qvel"] = np.nextafter(pert["qvel"].astype(np.float32), np.float32(np.inf)).astype(np.float64)
         env = np.abs(orc.step(pert, a.astype(np.float64), applied=app64) - oc).max(1)
-        assert np.median(err) < 1e-6 and np.percentile(err, 99.9) < 5e-4, (np.median(err), np.percentile(err, 99.9))
+        assert np.median(err) < 1e-6 and np.percentile(err, 99) < 5e-5 and np.percentile(err, 99.9) < 5e-4, \
+            (np.median(err), np.percentile(err, 99), np.percentile(err, 99.9))
         bad = err > 10 * env + 1e-5
         assert bad.sum() == 0, (np.nonzero(bad)[0], err[bad], env[bad])
         S.reset(init_qpos=np.zeros((n, 5), np.float32))

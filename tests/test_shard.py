@@ -66,3 +66,46 @@ def test_gather_world2(tmp_path):
     assert tuple(g.shape) == (4, total, 13)
     np.testing.assert_array_equal(g[0, :, 1].numpy(), np.arange(total))
     np.testing.assert_array_equal(g[:, 3, 0].numpy(), np.arange(4))
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.gpu
+def test_rccl_gather_one_rank_device_rollout(gpu_lib):
+    """The RCCL path of the rollout gather on one GPU (BASELINE.json configs[4]):
+    a one-rank ``nccl`` process group gathers a device rollout [T+1, N, 13] produced by the
+    simulator (DLS-IK actions on the arm scene) through shard.gather_rollouts -- the collective
+    config 5 ends with -- and rank 0 gets the local tensor back bit for bit.  (N > 1 ranks need an
+    8-GPU node; that path stays unmeasured on hardware.)"""
+    from lerobot_mujoco_sim2real_amd.sim import BatchSim
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cm = W.model("rollout")
+    n, T = 256, 8
+    ids = np.arange(n)
+    sim = BatchSim(cm, n)
+    q0 = W.initial_qpos(cm, ids, 0)
+    sim.reset(init_qpos=q0[:, :5], extra_qpos=q0, seed=0)
+    phase = torch.as_tensor(W.ik_phase(ids, 0), dtype=torch.float32, device=sim.device)
+    rows = torch.empty((T + 1, n, 13), dtype=torch.float32, device=sim.device)
+    rows[0, :, 5:] = sim.obs
+    qstar = sim.qpos.clone()
+    act = sim.action_buffer()
+    for t in range(T):
+        qstar, _, _ = sim.ik(W.fig8_targets(float(t), phase, lib=torch), q=qstar)
+        act.copy_(W.ik_action(qstar[:5].T, sim.obs[:, 3:8], lib=torch))
+        rows[t, :, :5] = act
+        rows[t + 1, :, 5:] = sim.step(act)
+    torch.cuda.synchronize()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_port()}", rank=0, world_size=1,
+                            device_id=sim.device)
+    try:
+        assert dist.get_backend() == "nccl"
+        g = shard.gather_rollouts(rows, dst=0)
+        torch.cuda.synchronize()
+    finally:
+        dist.destroy_process_group()
+    assert g.device == rows.device and g.shape == rows.shape
+    assert torch.equal(g, rows)
+    assert torch.isfinite(rows).all()

@@ -88,6 +88,11 @@ for t in range(T):
                                      "mean_pgs_cycles": v[69 + i] / max(v[61 + i], 1),
                                      "mean_retire_sweep": v[73 + i] / max(v[61 + i], 1)}
                                  for i, k in enumerate(["E", "E_coupled", "EF", "EF_coupled"])}
+        if v[77 + 11] > 0:  # RS kernel split (soarm_pgs.h rs_solve, Newton profiler slots)
+            w = v[77 + 11]
+            r["rs"] = {"setup_cycles_per_wave": v[77 + 8] / w, "sweep_cycles_per_wave": v[77 + 9] / w,
+                       "final_cycles_per_wave": v[77 + 10] / w, "sweeps_per_wave": v[77 + 16] / w,
+                       "cycles_per_sweep": v[77 + 9] / max(v[77 + 16], 1)}
         if v[77] > 0:
             r["newton"] = {"solves": v[77], "mean_iters": v[78] / v[77], "mean_ls_evals": v[79] / v[77],
                            "coupled_frac": v[80] / v[77], "mean_cycles": v[81] / v[77], "max_cycles": v[82],
