@@ -477,6 +477,11 @@ HDI int mpr(const MPair& P, float& depth, float dir[3], float pos[3], float sep[
 // arrays: EPA_KV vertices (v and the geom1 support point; geom2's is v1 - v), EPA_KF faces.
 constexpr int CCD_ITERS = 50;
 constexpr int EPA_KV = 32, EPA_KF = 64, EPA_KE = 48;
+// a face is seen from w when w lies beyond its plane by more than EPA_VIS: support points within
+// rounding of a face's plane (flat sides of box-shaped Minkowski differences put them there,
+// several collinear) would otherwise see it by the sign of the rounding, and the horizon stops
+// being one loop.  Half the EPA tolerance: the expanded face itself is always seen
+constexpr float EPA_VIS = 0.5f * MPR_TOLF;
 HDI void copy3(float d[3], const float s[3]) { d[0] = s[0], d[1] = s[1], d[2] = s[2]; }
 // closest point of simplex p[0..n) (n <= 3) to the origin; the carrying sub-simplex moves to the front
 HDI int gjk_reduce(MSup p[4], int n, float x[3]) {
@@ -590,8 +595,42 @@ HDI int tet_contains(MSup p[4], float x[3], int& n) {
   n = gjk_reduce(p, 3, x);
   return 0;
 }
-// GJK: true with p a tetrahedron enclosing the origin; false apart (sep = a separating axis when
-// a support plane proved it) or touching
+// support point along d or, when the Minkowski difference reaches no further than the tolerance
+// along d, along -d (d negated then); false if neither
+HDI bool ccd_extend(const MPair& P, float d[3], MSup& s) {
+  P.sup(d, s);
+  if (dot3(d, s.v) > MPR_TOLF) return true;
+  d[0] = -d[0], d[1] = -d[1], d[2] = -d[2];
+  P.sup(d, s);
+  return dot3(d, s.v) > MPR_TOLF;
+}
+// GJK ended with the origin ON the segment p[0..1] (n = 2) or the triangle p[0..2] (n = 3):
+// centred symmetric shapes, whose second support point is exactly minus the first.  nativeccd
+// starts EPA from such simplices (polytope2 / polytope3); here a support point off the simplex's
+// span per missing dimension completes a tetrahedron with the origin on its boundary (the
+// oracle's gjk_complete).  false: no extent off the span (touching).
+HDI bool gjk_complete(const MPair& P, MSup p[4], int n) {
+  if (n == 2) {  // a direction normal to the segment: u x (the axis of u's smallest component)
+    float u[3], d[3];
+    sub(u, p[1].v, p[0].v);
+    const float ax = fabsf(u[0]), ay = fabsf(u[1]), az = fabsf(u[2]);
+    const int k = ax <= ay && ax <= az ? 0 : ay <= az ? 1 : 2;
+    const float e[3] = {k == 0 ? 1.f : 0.f, k == 1 ? 1.f : 0.f, k == 2 ? 1.f : 0.f};
+    cross(d, u, e);
+    if (!(dot3(d, d) > 0.f)) return false;
+    nrm(d);
+    if (!ccd_extend(P, d, p[2])) return false;
+  }
+  float ab[3], ac[3], nn[3];
+  sub(ab, p[1].v, p[0].v);
+  sub(ac, p[2].v, p[0].v);
+  cross(nn, ab, ac);
+  if (!(dot3(nn, nn) > 0.f)) return false;
+  nrm(nn);
+  return ccd_extend(P, nn, p[3]);
+}
+// GJK: true with p a tetrahedron enclosing the origin (possibly on its boundary: gjk_complete);
+// false apart (sep = a separating axis when a support plane proved it) or touching
 HDI bool gjk_enclose(const MPair& P, MSup p[4], float sep[3]) {
   float c1[3], c2[3], x[3];
   geom_center(P.m, P.g1, P.P1, c1);
@@ -599,6 +638,7 @@ HDI bool gjk_enclose(const MPair& P, MSup p[4], float sep[3]) {
   sub(x, c1, c2);
   if (dot3(x, x) == 0.f) x[0] = 1e-9f;
   int n = 0;
+  float xx_prev = 3.0e38f;
   for (int it = 0; it < CCD_ITERS; it++) {
     const float d[3] = {-x[0], -x[1], -x[2]};
     MSup s;
@@ -615,13 +655,26 @@ HDI bool gjk_enclose(const MPair& P, MSup p[4], float sep[3]) {
     for (int k = 0; k < 4; k++) sel(p[k], k == n, s);
     n++;
     if (n == 4) {
+      const MSup q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
       const int r = tet_contains(p, x, n);
       if (r == 1) return true;
-      if (r < 0) return false;
+      if (r < 0) {  // flat: the previous triangle p[0..2], completed if it carries the origin
+        n = gjk_reduce(p, 3, x);
+        if (!(dot3(x, x) < 1e-12f * dot3(s.v, s.v))) return false;
+      } else if (!(dot3(x, x) < xx_prev)) {
+        // no progress: the origin is within rounding of this tetrahedron's face (a large flat
+        // Minkowski difference -- the table box -- whose closest-point direction fp32 resolves
+        // to ~1e-7 only, so the support along it returns the same vertex again): EPA from the
+        // tetrahedron decides (a face with d < 0 at the end: apart)
+        p[0] = q0, p[1] = q1, p[2] = q2, p[3] = q3;
+        return true;
+      }
     } else {
       n = gjk_reduce(p, n, x);
     }
-    if (dot3(x, x) < 1e-30f) return false;  // origin on a lower-dimensional simplex: touching
+    xx_prev = dot3(x, x);
+    // the origin on the simplex up to rounding (|x| < 1e-6 of the support point's scale)
+    if (dot3(x, x) < 1e-12f * dot3(s.v, s.v)) return n >= 2 && gjk_complete(P, p, n);
   }
   return false;
 }
@@ -674,7 +727,7 @@ HDI int epa(const MPair& P, const MSup p[4], float& depth, float dir[3], float p
       const int a = F[i].abc & 255, b = (F[i].abc >> 8) & 255, c = (F[i].abc >> 16) & 255;
       float aw[3];
       sub(aw, w.v, V[a]);
-      if (dot3(F[i].n, aw) <= 0.f) continue;
+      if (dot3(F[i].n, aw) <= EPA_VIS) continue;  // (w on a face's plane does not see it)
       vis |= 1ull << i;
       nvis++;
       const int ed[3][2] = {{a, b}, {b, c}, {c, a}};
@@ -1024,14 +1077,15 @@ HDI void box_box(const DModel& m, int g1, int g2, const GeomPose& P1, const Geom
   emit(o, -best / 1.05f, pos, bn);
 }
 
-// world records (pose + midphase bound, GREC floats) of every collidable geom of this env
+// world records (pose + midphase bound, GREC floats) of every collidable geom of this env;
+// lane g0 of gstep writes geoms g0, g0 + gstep, ... of the body-grouped geom order (geom_bybody),
+// so the geoms spread evenly over an env's lanes whatever the bodies' geom counts
 template <int NA, int NF>
-// geoms g0, g0 + gstep, ... of each body (quad mode: lane k of the quad writes every 4th)
 HDI void write_geom_poses(const Sim<NA, NF>& S, float* __restrict__ gpose, int n, int e, int g0 = 0,
                            int gstep = 1) {
   // bodies in compile-time order, each body's geoms from a wave-uniform list: the body frame
   // is read with constant indices (a per-lane body id would select it with 12 v_cndmask per
-  // body); g0/gstep split a body's geoms over the lanes of an env
+  // body)
   const DModel& m = *S.mp;
   constexpr int NB = Sim<NA, NF>::NB;
 #pragma unroll
@@ -1044,7 +1098,7 @@ HDI void write_geom_poses(const Sim<NA, NF>& S, float* __restrict__ gpose, int n
       for (int c = 0; c < 9; c++) bR[c] = S.xmat[b][c];
     }
     const int adr = m.body_gadr[b], num = m.body_gnum[b];
-    for (int t = g0; t < num; t += gstep) {
+    for (int t = ((g0 - adr) % gstep + gstep) % gstep; t < num; t += gstep) {
       const int g = m.geom_bybody[adr + t];
       const float gp[3] = {m.geom_pos[g][0], m.geom_pos[g][1], m.geom_pos[g][2]};
       float w[3], R[9];

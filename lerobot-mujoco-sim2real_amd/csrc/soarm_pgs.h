@@ -825,7 +825,9 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   float vw[NV];
 #pragma unroll
   for (int i = 0; i < NV; i++) vw[i] = 0.f;
-  const int cstep = QUADR ? 4 : 1, cfirst = QUADR ? (L.lane & 3) : 0;
+  // (the RS kernel: the env's 16 lanes split the contacts, one each)
+  const int cstep = RS ? 16 : QUADR ? 4 : 1, cfirst = RS ? (L.lane & 15) : QUADR ? (L.lane & 3) : 0;
+  auto env_sum = [&](float x) { return RS ? rowsum16(x) : QUADR ? qsum(x) : x; };
   for (int c = cfirst; c < nl; c += cstep) {
     float jn[NV], jt1[NV], jt2[NV];
 #pragma unroll
@@ -851,7 +853,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
     for (int i = 0; i < NV; i++) vw[i] += w[i];
   }
 #pragma unroll
-  for (int i = 0; i < NV; i++) v[i] += QUADR ? qsum(vw[i]) : vw[i];
+  for (int i = 0; i < NV; i++) v[i] += env_sum(vw[i]);
   for (int c = nl; c < ncon; c++)
     for (int ed = 0; ed < 4; ed++) {
       const int r = 4 * c + ed;
@@ -894,7 +896,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
                0.5f * fr * (jq[0] + s * jq[1 + (ed >> 1)] - ar);
     }
   }
-  cost += QUADR ? qsum(ccost) : ccost;
+  cost += env_sum(ccost);
   if constexpr (QUADR) wave_sync();  // F_FRC of the quad's contacts, written by their lanes
   for (int c = nl; c < ncon; c++)
     for (int ed = 0; ed < 4; ed++) {
@@ -2189,9 +2191,11 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
         // the top would hold hundreds of values)
         if constexpr (q & 1) __builtin_amdgcn_sched_barrier(0);
       });
-      const float scale = m.pgs_scale, tol = m.tolerance;
+      float scale = m.pgs_scale, tol = m.tolerance;
       int iters = m.iterations;
-      asm volatile("" : "+s"(iters));  // (loaded once: the sweeps' asm keeps LICM from hoisting it)
+      // (loaded once: the sweeps' asm statements keep LICM from hoisting the model loads, which would
+      // otherwise be re-issued and waited for in every sweep)
+      asm volatile("" : "+s"(iters), "+s"(scale), "+s"(tol));
       bool done = false;
 #ifdef SOARM_PHASE_PROF
       // (the RS solve's split, in the Newton profiler's slots: PGS builds leave them unused)

@@ -284,6 +284,44 @@ def _load_hulls(path=None):
     return out
 
 
+def hull_with_graph(verts_f32):
+    """Convex hull of a vertex cloud plus its vertex adjacency graph (the hill-climbing support
+    queries walk it): hull vertices (float32, ascending input order), CSR neighbour lists."""
+    from scipy.spatial import ConvexHull
+    pts = np.unique(np.asarray(verts_f32, dtype=np.float32), axis=0)
+    h = ConvexHull(pts.astype(np.float64))
+    hv = np.sort(h.vertices)
+    local = -np.ones(len(pts), dtype=np.int64)
+    local[hv] = np.arange(len(hv))
+    nbr = [set() for _ in range(len(hv))]
+    for tri in h.simplices:
+        a, b, c = local[tri]
+        nbr[a].update((b, c))
+        nbr[b].update((a, c))
+        nbr[c].update((a, b))
+    adr = np.zeros(len(hv) + 1, dtype=np.int32)
+    adj = []
+    for i, s in enumerate(nbr):
+        lst = sorted(s)
+        adj.extend(lst)
+        adr[i + 1] = adr[i] + len(lst)
+    return pts[hv].astype(np.float32), np.asarray(adj, dtype=np.int32), adr
+
+
+def vertex_hull(verts_f32):
+    """hulls.npz-style record of an inline ``<mesh vertex="...">`` asset: MuJoCo makes such a
+    mesh the convex hull of its vertices, and its centre the hull's volume centroid."""
+    from scipy.spatial import ConvexHull
+    v, adj, adr = hull_with_graph(verts_f32)
+    p = v.astype(np.float64)
+    h = ConvexHull(p)
+    o = p.mean(0)
+    a, b, c = (p[h.simplices[:, k]] for k in range(3))
+    vol = np.abs(np.einsum("ij,ij->i", a - o, np.cross(b - o, c - o))) / 6.0
+    com = (vol[:, None] * (a + b + c + o) / 4.0).sum(0) / vol.sum()
+    return {"v": v, "adj": adj, "adr": adr, "com": com}
+
+
 def compile_mjcf(xml_path=SCENE_XML, kv=None, disable_contact=False, iterations=100,
                  tolerance=1e-8, obs_site="gripperframe",
                  obs_joints=("shoulder_pan", "shoulder_lift", "elbow_flex", "wrist_flex", "wrist_roll"),
@@ -322,14 +360,24 @@ def compile_mjcf(xml_path=SCENE_XML, kv=None, disable_contact=False, iterations=
             else:
                 defaults.classes["main"].setdefault(ch.tag, {}).update(ch.attrib)
 
-    # mesh assets: name -> file stem
+    # mesh assets: name -> file stem (hull in hulls.npz) or, for an inline ``vertex`` mesh, its
+    # own hull computed here
     meshes = {}
+    hulls = _load_hulls()
     for asec in root.findall("asset"):
         for m in asec.findall("mesh"):
             f = m.get("file")
+            if f is None and m.get("vertex") is not None:
+                nm = m.get("name")
+                if not nm:
+                    raise ValueError("an inline (vertex) mesh needs a name")
+                v = np.asarray(_floats(m.get("vertex")), dtype=np.float32).reshape(-1, 3)
+                v = v * np.asarray(_floats(m.get("scale", "1 1 1")), dtype=np.float32)
+                hulls[nm] = vertex_hull(v)
+                meshes[nm] = nm
+                continue
             nm = m.get("name") or os.path.splitext(os.path.basename(f))[0]
             meshes[nm] = os.path.splitext(os.path.basename(f))[0]
-    hulls = _load_hulls()
 
     # option (none in the reference scene -> MuJoCo defaults)
     opt = {}

@@ -450,7 +450,12 @@ static int mpr_penetration(const mpair* P, double* depth, double dir[3], double 
    until upper - lower < tolerance.  Contact: depth = the closest face's distance, normal = its
    outward normal (geom1 -> geom2), witness points x1, x2 = the barycentric weights of the
    origin's projection on that face applied to the two shapes' support points, pos = (x1+x2)/2.
-   Touching configurations (the origin on the boundary of the final simplex) give no contact. */
+   GJK may end with the origin ON a segment or triangle of its simplex (centred symmetric
+   shapes: the second support point is exactly minus the first).  nativeccd then builds EPA's
+   start from that simplex (polytope2 / polytope3); gjk_complete restates it as adding a support
+   point off the simplex's span per missing dimension, giving a tetrahedron with the origin on
+   its boundary, from which EPA expands as usual.  A lone vertex at the origin, or no extent off
+   the span in either direction, is a touching configuration: no contact. */
 #define CCD_TOL 1e-6
 #define CCD_ITER 50
 #define EPA_MAXV (4 + CCD_ITER)
@@ -567,7 +572,40 @@ static int tet_contains(msup* p, double x[3], int* nout) {
   return 0;
 }
 
-/* GJK: 1 with p[0..3] a tetrahedron enclosing the origin, 0 if apart or touching */
+/* support point along d or, when the Minkowski difference has no extent along d beyond the
+   tolerance, along -d (d is negated then); 0 if neither */
+static int ccd_extend(const mpair* P, double d[3], msup* s) {
+  msupport(P, d, s);
+  if (dot3(d, s->v) > CCD_TOL) return 1;
+  for (int k = 0; k < 3; k++) d[k] = -d[k];
+  msupport(P, d, s);
+  return dot3(d, s->v) > CCD_TOL;
+}
+
+/* the origin lies on the segment p[0..1] (n = 2) or the triangle p[0..2] (n = 3): complete a
+   tetrahedron p[0..3] around it (the origin on its boundary); 0 when touching */
+static int gjk_complete(const mpair* P, msup* p, int n) {
+  if (n == 2) { /* a direction normal to the segment: u x (the axis of u's smallest component) */
+    double u[3], e[3] = {0, 0, 0}, d[3];
+    sub3(u, p[1].v, p[0].v);
+    const double ax = fabs(u[0]), ay = fabs(u[1]), az = fabs(u[2]);
+    e[ax <= ay && ax <= az ? 0 : ay <= az ? 1 : 2] = 1;
+    cross3(d, u, e);
+    if (!(norm3(d) > 0)) return 0;
+    normalize3(d);
+    if (!ccd_extend(P, d, &p[2])) return 0;
+  }
+  double ab[3], ac[3], nn[3];
+  sub3(ab, p[1].v, p[0].v);
+  sub3(ac, p[2].v, p[0].v);
+  cross3(nn, ab, ac);
+  if (!(norm3(nn) > 0)) return 0;
+  normalize3(nn);
+  return ccd_extend(P, nn, &p[3]);
+}
+
+/* GJK: 1 with p[0..3] a tetrahedron enclosing the origin (possibly on its boundary, see
+   gjk_complete), 0 if apart or touching */
 static int gjk_enclose(const mpair* P, msup* p) {
   double c1[3], c2[3], x[3];
   geom_center(P->om, P->d, P->g1, c1);
@@ -575,6 +613,7 @@ static int gjk_enclose(const mpair* P, msup* p) {
   sub3(x, c1, c2);
   if (dot3(x, x) == 0) x[0] = 1e-9;
   int n = 0;
+  double xx_prev = 1e300;
   for (int it = 0; it < CCD_ITER; it++) {
     double dir[3] = {-x[0], -x[1], -x[2]};
     msup s;
@@ -585,13 +624,25 @@ static int gjk_enclose(const mpair* P, msup* p) {
     if (xx - dot3(x, s.v) <= CCD_TOL * CCD_TOL) return 0;
     p[n++] = s;
     if (n == 4) {
+      msup q[4] = {p[0], p[1], p[2], p[3]};
       int r = tet_contains(p, x, &n);
       if (r == 1) return 1;
-      if (r < 0) return 0;
+      if (r < 0) { /* flat: the previous triangle p[0..2], completed if it carries the origin */
+        n = gjk_reduce(p, 3, x);
+        if (!(dot3(x, x) < 1e-12 * dot3(s.v, s.v))) return 0;
+      } else if (!(dot3(x, x) < xx_prev)) {
+        /* no progress (the support along x returns a vertex already held): the origin is within
+           rounding of this tetrahedron, EPA from it decides (the kernel's fp32 GJK stalls so on
+           the table box's large flat Minkowski difference) */
+        memcpy(p, q, sizeof(q));
+        return 1;
+      }
     } else {
       n = gjk_reduce(p, n, x);
     }
-    if (dot3(x, x) < 1e-30) return 0; /* origin on a lower-dimensional simplex: touching */
+    xx_prev = dot3(x, x);
+    /* the origin on the simplex up to rounding (|x| < 1e-6 of the support point's scale) */
+    if (dot3(x, x) < 1e-12 * dot3(s.v, s.v)) return n >= 2 && gjk_complete(P, p, n);
   }
   return 0;
 }
@@ -639,7 +690,7 @@ static int epa(const mpair* P, msup* V, double* depth, double dir[3], double pos
       if (!F[i].live) continue;
       double aw[3];
       sub3(aw, w.v, V[F[i].a].v);
-      if (dot3(F[i].n, aw) <= 0) continue;
+      if (dot3(F[i].n, aw) <= 0.5 * CCD_TOL) continue; /* (on its plane: not seen, as the kernel) */
       vis[i] = 1;
       nvis++;
       const int ed[3][2] = {{F[i].a, F[i].b}, {F[i].b, F[i].c}, {F[i].c, F[i].a}};

@@ -407,3 +407,33 @@ def test_cpu_thread_count_invariance(cpu_lib, cube_model, monkeypatch):
         out.append((S.obs.clone(), S.qpos.clone(), S.qvel.clone(), S.ncon.clone()))
     for x, y in zip(*out):
         assert bool((x == y).all())
+
+
+def test_cpu_native_ccd_centred_symmetric_overlap(cpu_lib, tmp_path):
+    """The kernels' GJK completion (soarm_collide.h gjk_complete) on the host: a mesh cube
+    centred inside the table box (test_oracle.test_native_ccd_centred_symmetric_overlap) gives
+    the oracle's contact.  The two faces normal to the smallest extent tie, so the normal is
+    compared up to sign; depth to fp32 rounding of the 0.13 m overlap."""
+    from lerobot_mujoco_sim2real_amd import mjcf
+    from test_oracle import probe_states, write_probe_scene
+    cm = mjcf.compile_mjcf(write_probe_scene(tmp_path))
+    qs = probe_states(cm)
+    check_probe_contacts(cm, make_sim(cm, len(qs)), qs)
+
+
+def check_probe_contacts(cm, S, qs):
+    import torch
+    orc = Oracle(cm)
+    gt, gp = cm.geom_names.index("table"), cm.geom_names.index("probe")
+    S.qpos.copy_(torch.as_tensor(qs.T, dtype=torch.float32))
+    out, nc = S.contacts()
+    out, nc = to_np(out), to_np(nc).astype(int)
+    pid = out.astype(np.float32).view(np.int32)[..., 7]
+    d = cm.desc
+    for e, q in enumerate(qs.astype(np.float32).astype(np.float64)):
+        rc = [r for r in orc.forward(q)["contacts"] if {int(r[7]), int(r[8])} == {gt, gp}]
+        got = [k for k in range(nc[e]) if {d.pair_geom1[pid[e, k]], d.pair_geom2[pid[e, k]]} == {gt, gp}]
+        assert len(rc) == 1 and len(got) == 1, (e, rc, got)
+        r, k = rc[0], got[0]
+        assert abs(out[e, k, 0] - r[0]) <= 2e-6, (e, out[e, k, 0], r[0])
+        assert abs(abs(out[e, k, 4:7] @ r[4:7]) - 1) <= 1e-5, (e, out[e, k, 4:7], r[4:7])

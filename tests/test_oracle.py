@@ -284,3 +284,69 @@ def test_native_ccd_is_minimum_penetration(xml):
                     assert hn >= depth - 2e-6, (e, g1, g2, hn, depth)
                 n_conv += 1
         assert n_conv >= 20, (ccd, n_conv)
+
+
+# ---- centred, centrally symmetric convex overlap (GJK ends with the origin ON its simplex)
+PROBE_H = 0.03
+TABLE_C, TABLE_H = np.array([0.0, 0.0, -0.1009]), np.array([0.61, 0.37, 0.1])
+
+
+def write_probe_scene(dirpath, h=PROBE_H):
+    """The arm, floor and table box plus one free body whose geom is an inline-vertex MESH cube
+    of half-size h (MJCF ``<mesh vertex=...>``): the table/probe pair runs the convex-convex
+    narrowphase (box vs mesh) instead of box_box."""
+    corners = " ".join(f"{sx * h} {sy * h} {sz * h}" for sx in (-1, 1) for sy in (-1, 1) for sz in (-1, 1))
+    xml = f"""<mujoco model="probe">
+  <include file="{mjcf.ASSET_DIR}/so101_new_calib_v.xml"/>
+  <asset><mesh name="probe" vertex="{corners}"/></asset>
+  <worldbody>
+    <geom name="floor" size="0 0 0.05" pos="0 0 -.75" type="plane"/>
+    <geom name="table" pos="0 0 -0.1009" size="0.61 0.37 0.1" type="box" class="collision"/>
+    <body name="probe" pos="0.3 0 0.2">
+      <freejoint name="probe_free"/>
+      <inertial pos="0 0 0" mass="0.05" diaginertia="2e-5 2e-5 2e-5"/>
+      <geom name="probe" type="mesh" mesh="probe"/>
+    </body>
+  </worldbody>
+</mujoco>"""
+    path = str(dirpath / "probe_scene.xml")
+    with open(path, "w") as f:
+        f.write(xml)
+    return path
+
+
+def probe_states(cm, n_random=6, seed=11):
+    """qpos with the probe centred on the table box: axis-aligned, a quarter turn, random turns."""
+    rng = np.random.default_rng(seed)
+    quats = [np.array([1.0, 0, 0, 0]), np.array([np.cos(np.pi / 4), 0, 0, np.sin(np.pi / 4)])]
+    quats += [q / np.linalg.norm(q) for q in rng.normal(size=(n_random, 4))]
+    qs = np.zeros((len(quats), cm.nq))
+    qs[:, 6:9] = TABLE_C
+    qs[:, 9:13] = quats
+    return qs
+
+
+def test_native_ccd_centred_symmetric_overlap(tmp_path):
+    """a mesh cube centred inside the table box.  A - B is centrally symmetric, so
+    GJK's second support point is exactly minus its first and the origin lands ON the segment:
+    the old shortcut called that touching and reported no contact.  nativeccd starts EPA from
+    such simplices (polytope2 / polytope3; the oracle's gjk_complete): the contact must exist and
+    be the minimum penetration -- h(n) = depth and no sampled direction below it; axis-aligned,
+    depth = table half-height + h exactly, along z."""
+    cm = mjcf.compile_mjcf(write_probe_scene(tmp_path))
+    assert cm.desc.ccd == 1
+    orc = Oracle(cm)
+    gt, gp = cm.geom_names.index("table"), cm.geom_names.index("probe")
+    dirs = np.random.default_rng(5).normal(size=(20000, 3))
+    dirs /= np.linalg.norm(dirs, axis=1, keepdims=True)
+    for i, q in enumerate(probe_states(cm)):
+        rc = [r for r in orc.forward(q)["contacts"] if {int(r[7]), int(r[8])} == {gt, gp}]
+        assert len(rc) == 1, (i, rc)
+        r = rc[0]
+        xp, xm = orc.geom_frames(q)
+        A, B = _world_hull(cm, xp, xm, gt), _world_hull(cm, xp, xm, gp)
+        n, depth = r[4:7], -r[0]
+        assert abs((A @ n).max() - (B @ n).min() - depth) <= 2e-6, (i, depth)
+        assert ((A @ dirs.T).max(0) - (B @ dirs.T).min(0)).min() >= depth - 1e-9, (i, depth)
+        if i < 2:
+            assert abs(depth - (TABLE_H[2] + PROBE_H)) <= 1e-9 and abs(abs(n[2]) - 1) <= 1e-9, (i, r)

@@ -88,7 +88,7 @@ def test_rccl_gather_one_rank_device_rollout(gpu_lib):
     q0 = W.initial_qpos(cm, ids, 0)
     sim.reset(init_qpos=q0[:, :5], extra_qpos=q0, seed=0)
     phase = torch.as_tensor(W.ik_phase(ids, 0), dtype=torch.float32, device=sim.device)
-    rows = torch.empty((T + 1, n, 13), dtype=torch.float32, device=sim.device)
+    rows = torch.zeros((T + 1, n, 13), dtype=torch.float32, device=sim.device)  # (row T: no action)
     rows[0, :, 5:] = sim.obs
     qstar = sim.qpos.clone()
     act = sim.action_buffer()

@@ -23,7 +23,10 @@ import shutil
 import sys
 
 import numpy as np
-from scipy.spatial import ConvexHull
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+import soarm_pkg  # noqa: E402,F401
+from lerobot_mujoco_sim2real_amd.mjcf import hull_with_graph  # noqa: E402
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 OUT = os.path.join(HERE, "..", "lerobot-mujoco-sim2real_amd", "assets", "so101")
@@ -48,28 +51,6 @@ def volume_centroid(tri):
     a, b, c = (tri[:, k].astype(np.float64) for k in range(3))
     vol = np.einsum("ij,ij->i", a, np.cross(b, c)) / 6.0
     return (vol[:, None] * (a + b + c) / 4.0).sum(0) / vol.sum()
-
-
-def hull_with_graph(verts_f32):
-    pts = np.unique(verts_f32, axis=0)
-    h = ConvexHull(pts.astype(np.float64))
-    # keep hull vertices in ascending input order -> deterministic local ids
-    hv = np.sort(h.vertices)
-    local = -np.ones(len(pts), dtype=np.int64)
-    local[hv] = np.arange(len(hv))
-    nbr = [set() for _ in range(len(hv))]
-    for tri in h.simplices:
-        a, b, c = local[tri]
-        nbr[a].update((b, c))
-        nbr[b].update((a, c))
-        nbr[c].update((a, b))
-    adr = np.zeros(len(hv) + 1, dtype=np.int32)
-    adj = []
-    for i, s in enumerate(nbr):
-        lst = sorted(s)
-        adj.extend(lst)
-        adr[i + 1] = adr[i] + len(lst)
-    return pts[hv].astype(np.float32), np.asarray(adj, dtype=np.int32), adr
 
 
 def main(ref_root, xml_only=False):
