@@ -40,6 +40,17 @@ __device__ long long g_pgs_prof[65536 * 8];
 __device__ long long g_stamp[65536 * 16];
 #define PSTAMP(k) \
   if (e < 65536) g_stamp[16 * e + (k)] = clock64()
+// per-wave accumulators of k_substep's phase profile (layout: soarm_substep.h g_phase; [77..81] the
+// RS solve's split).  Lane 0 of each wave owns its row and launches are stream-ordered, so plain
+// read-modify-writes: shared-address atomics from every wave queued behind the profiled kernel's own
+// loads and inflated the phases after the solve ~15x (r05).  sim_phase_profile reduces the rows.
+// [82..84]: RS-kernel waves that took the v-form fallback -- count, max and summed wave cycles.
+constexpr int WPH = 85, WPH_MAXW = 16384;
+__device__ unsigned long long g_wphase[WPH_MAXW * WPH];
+#define WPH_ID() (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6)
+#define WPH_ADD(k, v) g_wphase[WPH_ID() * WPH + (k)] += (unsigned long long)(v)
+#define WPH_MAX(k, v) \
+  g_wphase[WPH_ID() * WPH + (k)] = max(g_wphase[WPH_ID() * WPH + (k)], (unsigned long long)(v))
 // contact-row build split: [0] loads + frame, [1] Jacobian, [2] Gram / M^-1 / velocities, [3] edges + LDS writes
 __device__ long long g_rowprof[65536 * 4];
 #define RP_INIT long long rp_acc[4] = {0, 0, 0, 0}, rp_t = clock64()
@@ -2236,13 +2247,13 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
         v[i] = S.qacc_s[i] + rowbcast<i>(acc);
       });
 #ifdef SOARM_PHASE_PROF
-      if ((threadIdx.x & 63) == 0) {
+      if ((threadIdx.x & 63) == 0 && WPH_ID() < WPH_MAXW) {
         const long long rp2 = clock64();
-        atomicAdd(&g_newton[8], (unsigned long long)(rp0 - g_pgs_prof[8 * e]));
-        atomicAdd(&g_newton[9], (unsigned long long)(rp1 - rp0));
-        atomicAdd(&g_newton[10], (unsigned long long)(rp2 - rp1));
-        atomicAdd(&g_newton[11], 1ull);
-        atomicAdd(&g_newton[16], (unsigned long long)wsw);
+        WPH_ADD(77, rp0 - g_pgs_prof[8 * e]);
+        WPH_ADD(78, rp1 - rp0);
+        WPH_ADD(79, rp2 - rp1);
+        WPH_ADD(80, 1);
+        WPH_ADD(81, wsw);
       }
 #endif
     }
@@ -2315,7 +2326,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
     g_pgs_prof[8 * e + 3] = (ypure ? 0 : yext ? 1 : block_first ? 2 : 3) | (npost > 0 && npost_free ? 16 : 0) |
                             (min(npost, 3) << 8) | (min(nfree_x, 3) << 12) | ((nl > 5) << 16) | ((nlim > 0) << 17) |
                             ((nl != ncon) << 18) | ((long long)min(armstop, 255) << 20) |
-                            ((long long)(yext ? 4 + 2 * yext2 + ycoupled : 0) << 28),
+                            ((long long)(yext ? 4 + 2 * yext2 + ycoupled : 0) << 28) | ((long long)(RS && !rs_fast) << 40),
     g_pgs_prof[8 * e + 4] = nlim, g_pgs_prof[8 * e + 5] = ncon;
 #endif
 

@@ -995,11 +995,20 @@ int sim_step(sim_batch* b, const sim_state* s, const float* action, int frame_sk
             epb = RS_EPW;
           }
         }
-        hipLaunchKernelGGL(kern, dim3((b->n + epb - 1) / epb), dim3(64), 0, q,
+        size_t lds_pad = 0;
+#ifdef SOARM_PHASE_PROF
+        // (diagnostic build: SOARM_LDS_PAD bytes of unused dynamic LDS cap the workgroups per CU)
+        if (const char* v = getenv("SOARM_LDS_PAD")) lds_pad = (size_t)atol(v);
+        // (SOARM_DIAG_NOGPOSE: the substep writes no geom records -- timing only, wrong contacts)
+        const bool nogpose = getenv("SOARM_DIAG_NOGPOSE") != nullptr;
+#else
+        constexpr bool nogpose = false;
+#endif
+        hipLaunchKernelGGL(kern, dim3((b->n + epb - 1) / epb), dim3(64), lds_pad, q,
                            b->d_model, b->n, *s,
                            sub == 0 ? action : nullptr, last ? obs : nullptr, b->params, b->d_scratch,
                            b->d_cbuf, np > 0 ? b->d_ccount : nullptr, np > 0 ? b->d_pmask : nullptr,
-                           last ? nullptr : b->d_gpose, b->d_gpose);
+                           last || nogpose ? nullptr : b->d_gpose, b->d_gpose);
         prof_mark(b, -1, q);
       }
      });
@@ -1107,15 +1116,33 @@ int sim_collide_profile(sim_batch* b, const sim_state* s, double* cycles, void* 
 int sim_phase_profile(double* out, int reset) {
   if (!out) return fail(SIM_E_ARG, "null output");
 #ifdef SOARM_PHASE_PROF
-  unsigned long long h[77], nw[24];
+  unsigned long long nw[24];
+  std::vector<unsigned long long> w((size_t)WPH_MAXW * WPH);
   HIPCHECK(hipDeviceSynchronize());
-  HIPCHECK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_phase), sizeof(h)));
+  HIPCHECK(hipMemcpyFromSymbol(w.data(), HIP_SYMBOL(g_wphase), w.size() * sizeof(w[0])));
   HIPCHECK(hipMemcpyFromSymbol(nw, HIP_SYMBOL(g_newton), sizeof(nw)));
+  // per-wave rows (soarm_pgs.h g_wphase): maxima where g_phase's layout keeps a max, sums elsewhere
+  const auto is_max = [](int k) {
+    return k == 8 || k == 10 || k == 15 || (k >= 23 && k <= 26) || k == 59 || k == 60 || (k >= 65 && k <= 68) ||
+           k == 83;
+  };
+  unsigned long long h[WPH] = {};
+  for (int r = 0; r < WPH_MAXW; r++)
+    for (int k = 0; k < WPH; k++) {
+      const unsigned long long v = w[(size_t)r * WPH + k];
+      h[k] = is_max(k) ? std::max(h[k], v) : h[k] + v;
+    }
   for (int k = 0; k < 77; k++) out[k] = (double)h[k];
   for (int k = 0; k < 24; k++) out[77 + k] = (double)nw[k];
+  // the RS solve's split, in the slots the Newton profiler leaves free in PGS builds
+  out[77 + 8] = (double)h[77], out[77 + 9] = (double)h[78], out[77 + 10] = (double)h[79];
+  out[77 + 11] = (double)h[80], out[77 + 16] = (double)h[81];
+  out[77 + 17] = (double)h[82], out[77 + 18] = (double)h[83], out[77 + 19] = (double)h[84];  // RS fallback waves
   if (reset) {
-    const unsigned long long z[77] = {};
-    HIPCHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof(z)));
+    void* a = nullptr;
+    HIPCHECK(hipGetSymbolAddress(&a, HIP_SYMBOL(g_wphase)));
+    HIPCHECK(hipMemset(a, 0, w.size() * sizeof(w[0])));
+    const unsigned long long z[24] = {};
     HIPCHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_newton), z, sizeof(nw)));
   }
   return SIM_OK;

@@ -21,7 +21,8 @@ namespace soarm {
 //   [19..22] waves per sweep variant (y-pure, y+arm slot, block-first general, other),
 //   [23..26] max wave cycles per variant, [27] waves with a non-block contact on the free body
 //   [28..42] wave cycles between consecutive fine stamps (g_stamp, see PSTAMP sites)
-__device__ unsigned long long g_phase[77];  // [53..56] contact-row build split (g_rowprof),
+// (accumulated per wave in g_wphase, soarm_pgs.h; this is the layout)
+//                                          [53..56] contact-row build split (g_rowprof),
                                             // [57] waves that retired the arm rows, [58] sum of their retire sweeps,
                                             // [59] / [60] max wave cycles of the waves that did not / did retire
                                             // y+arm slot waves by (F slot, E coupled to the cube) = 2 F + coupled:
@@ -242,57 +243,67 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
   const int nsw = (int)g_pgs_prof[8 * e + 2];
   const bool anylim = __any(g_pgs_prof[8 * e + 4] > 0), anyslow = __any(g_pgs_prof[8 * e + 3] == 0),
              anyovf = __any(g_pgs_prof[8 * e + 5] > LDS_CON), anyfree = __any(g_pgs_prof[8 * e + 3] & 16);
-  atomicMax(&g_phase[15], (unsigned long long)g_pgs_prof[8 * e + 5]);
-  atomicAdd(&g_phase[6], (unsigned long long)nsw);
-  atomicAdd(&g_phase[7], 1ull);
-  int wmax = nsw;
+  // (wave reductions first: one row per wave in g_wphase, no shared-address atomics)
+  auto wsum = [](int x) {
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, __shfl_xor(wmax, o));
-  {  // per-lane census of lanes in waves on a non-y sweep: [43..46] npost 0..3+, [47..49] extras
-     // on the free body 0/1/2+, [50] > 5 contacts, [51] active limit, [52] overflow rows
-    const long long v = g_pgs_prof[8 * e + 3];
-    if ((v & 15) >= 2) {
-      atomicAdd(&g_phase[43 + ((v >> 8) & 3)], 1ull);
-      atomicAdd(&g_phase[47 + min((int)((v >> 12) & 3), 2)], 1ull);
-      atomicAdd(&g_phase[50], (unsigned long long)((v >> 16) & 1));
-      atomicAdd(&g_phase[51], (unsigned long long)((v >> 17) & 1));
-      atomicAdd(&g_phase[52], (unsigned long long)((v >> 18) & 1));
-    }
-  }
-  if ((threadIdx.x & 63) == 0) {
-    atomicAdd(&g_phase[0], (unsigned long long)(t1 - t0));
-    atomicAdd(&g_phase[1], (unsigned long long)(t2 - t1));
-    atomicAdd(&g_phase[2], (unsigned long long)(p0 - t2));
-    atomicAdd(&g_phase[3], (unsigned long long)(p1 - p0));
-    atomicAdd(&g_phase[4], (unsigned long long)(t5 - p1));
-    atomicMax(&g_phase[8], (unsigned long long)(t5 - t0));
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+    return x;
+  };
+  int wmax = nsw, cmax = (int)g_pgs_prof[8 * e + 5];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, __shfl_xor(wmax, o)), cmax = max(cmax, __shfl_xor(cmax, o));
+  // per-lane census of lanes in waves on a non-y sweep: [43..46] npost 0..3+, [47..49] extras on
+  // the free body 0/1/2+, [50] > 5 contacts, [51] active limit, [52] overflow rows
+  const long long cv = g_pgs_prof[8 * e + 3];
+  const bool ny = (cv & 15) >= 2;
+  int census[10];
+#pragma unroll
+  for (int k = 0; k < 4; k++) census[k] = wsum(ny && ((cv >> 8) & 3) == k);
+#pragma unroll
+  for (int k = 0; k < 3; k++) census[4 + k] = wsum(ny && min((int)((cv >> 12) & 3), 2) == k);
+  census[7] = wsum(ny && ((cv >> 16) & 1)), census[8] = wsum(ny && ((cv >> 17) & 1)),
+  census[9] = wsum(ny && ((cv >> 18) & 1));
+  const int nsw_sum = wsum(nsw), lanes = wsum(1);
+  if ((threadIdx.x & 63) == 0 && WPH_ID() < WPH_MAXW) {
+    WPH_MAX(15, cmax);
+    WPH_ADD(6, nsw_sum);
+    WPH_ADD(7, lanes);
+#pragma unroll
+    for (int k = 0; k < 10; k++) WPH_ADD(43 + k, census[k]);
+    WPH_ADD(0, t1 - t0);
+    WPH_ADD(1, t2 - t1);
+    WPH_ADD(2, p0 - t2);
+    WPH_ADD(3, p1 - p0);
+    WPH_ADD(4, t5 - p1);
+    WPH_MAX(8, t5 - t0);
     {
       int var = (int)g_pgs_prof[8 * e + 3] & 15;
-      atomicAdd(&g_phase[9], (unsigned long long)(var == 0));
-      atomicAdd(&g_phase[19 + var], 1ull);
-      atomicMax(&g_phase[23 + var], (unsigned long long)(t5 - t0));
+      WPH_ADD(9, var == 0);
+      WPH_ADD(19 + var, 1);
+      WPH_MAX(23 + var, t5 - t0);
     }
-    atomicAdd(&g_phase[27], (unsigned long long)anyfree);
-    for (int k = 0; k < 15; k++) atomicAdd(&g_phase[28 + k], (unsigned long long)(g_stamp[16 * e + k + 1] - g_stamp[16 * e + k]));
-    for (int k = 0; k < 4; k++) atomicAdd(&g_phase[53 + k], (unsigned long long)g_rowprof[4 * e + k]);
-    atomicAdd(&g_phase[16], (unsigned long long)(g_pgs_prof[8 * e + 6] - t2));
-    atomicAdd(&g_phase[17], (unsigned long long)(g_pgs_prof[8 * e + 7] - g_pgs_prof[8 * e + 6]));
-    atomicAdd(&g_phase[18], (unsigned long long)(p0 - g_pgs_prof[8 * e + 7]));
-    atomicAdd(&g_phase[12], (unsigned long long)anylim);
-    atomicAdd(&g_phase[13], (unsigned long long)anyslow);
-    atomicAdd(&g_phase[14], (unsigned long long)anyovf);
-    atomicMax(&g_phase[10], (unsigned long long)(p1 - p0));
-    atomicAdd(&g_phase[11], (unsigned long long)wmax);
-    atomicAdd(&g_phase[5], 1ull);
+    WPH_ADD(27, anyfree);
+    for (int k = 0; k < 15; k++) WPH_ADD(28 + k, g_stamp[16 * e + k + 1] - g_stamp[16 * e + k]);
+    for (int k = 0; k < 4; k++) WPH_ADD(53 + k, g_rowprof[4 * e + k]);
+    WPH_ADD(16, g_pgs_prof[8 * e + 6] - t2);
+    WPH_ADD(17, g_pgs_prof[8 * e + 7] - g_pgs_prof[8 * e + 6]);
+    WPH_ADD(18, p0 - g_pgs_prof[8 * e + 7]);
+    WPH_ADD(12, anylim);
+    WPH_ADD(13, anyslow);
+    WPH_ADD(14, anyovf);
+    WPH_MAX(10, p1 - p0);
+    WPH_ADD(11, wmax);
+    WPH_ADD(5, 1);
+    if (__any((g_pgs_prof[8 * e + 3] >> 40) & 1)) WPH_ADD(82, 1), WPH_MAX(83, t5 - t0), WPH_ADD(84, t5 - t0);
     const int ast = (int)((g_pgs_prof[8 * e + 3] >> 20) & 255);
-    if (ast) atomicAdd(&g_phase[57], 1ull), atomicAdd(&g_phase[58], (unsigned long long)ast);
-    atomicMax(&g_phase[ast ? 60 : 59], (unsigned long long)(t5 - t0));
+    if (ast) WPH_ADD(57, 1), WPH_ADD(58, ast);
+    WPH_MAX(ast ? 60 : 59, t5 - t0);
     const int xv = (int)((g_pgs_prof[8 * e + 3] >> 28) & 7);
     if (xv >= 4) {
-      atomicAdd(&g_phase[61 + xv - 4], 1ull);
-      atomicMax(&g_phase[65 + xv - 4], (unsigned long long)(t5 - t0));
-      atomicAdd(&g_phase[69 + xv - 4], (unsigned long long)(p1 - p0));
-      atomicAdd(&g_phase[73 + xv - 4], (unsigned long long)ast);
+      WPH_ADD(61 + xv - 4, 1);
+      WPH_MAX(65 + xv - 4, t5 - t0);
+      WPH_ADD(69 + xv - 4, p1 - p0);
+      WPH_ADD(73 + xv - 4, ast);
     }
   }
 #endif

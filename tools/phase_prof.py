@@ -92,7 +92,9 @@ for t in range(T):
             w = v[77 + 11]
             r["rs"] = {"setup_cycles_per_wave": v[77 + 8] / w, "sweep_cycles_per_wave": v[77 + 9] / w,
                        "final_cycles_per_wave": v[77 + 10] / w, "sweeps_per_wave": v[77 + 16] / w,
-                       "cycles_per_sweep": v[77 + 9] / max(v[77 + 16], 1)}
+                       "cycles_per_sweep": v[77 + 9] / max(v[77 + 16], 1),
+                       "fallback_waves_per_launch": v[77 + 17] / max(v[5] / (n // 4), 1),
+                       "fallback_max_cycles": v[77 + 18], "fallback_mean_cycles": v[77 + 19] / max(v[77 + 17], 1)}
         if v[77] > 0:
             r["newton"] = {"solves": v[77], "mean_iters": v[78] / v[77], "mean_ls_evals": v[79] / v[77],
                            "coupled_frac": v[80] / v[77], "mean_cycles": v[81] / v[77], "max_cycles": v[82],
