@@ -313,8 +313,10 @@ int sim_collide_profile(sim_batch* b, const sim_state* s, double* cycles, void* 
    cycles, waves on the register fast path, max wave PGS cycles, sum of per-wave
    max sweeps, waves with an active limit / a non-block contact / contact
    overflow past LDS, max contacts per env; then the rows phase split: contact rows,
-   warm start + cost, register-block setup; the rest to 77: see g_phase in soarm_sim.hip; 77..100:
-   the Newton solver's counters, g_newton in soarm_newton.h);
+   warm start + cost, register-block setup; the rest to 77: see g_phase in soarm_substep.h; 77..100:
+   the Newton solver's counters, g_newton in soarm_newton.h, with the RS kernel's solve split in
+   85..88, 93 and its fallback waves in 94..96; 101..107: the fallback lanes by cause -- out holds
+   108 doubles);
    returns SIM_E_ARG in a regular build. */
 int sim_phase_profile(double* out, int reset);
 

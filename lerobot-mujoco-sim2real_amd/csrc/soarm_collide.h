@@ -483,24 +483,53 @@ constexpr int EPA_KV = 32, EPA_KF = 64, EPA_KE = 48;
 // being one loop.  Half the EPA tolerance: the expanded face itself is always seen
 constexpr float EPA_VIS = 0.5f * MPR_TOLF;
 HDI void copy3(float d[3], const float s[3]) { d[0] = s[0], d[1] = s[1], d[2] = s[2]; }
+// GJK runs in fp64 on the fp32 support points: a simplex vertex is the Minkowski point
+// v = s1 - s2 (exact in fp64) with geom1's support point s1 (EPA's witness).  In fp32 the
+// closest-point direction resolves to ~1e-7 only; against the table box's 1.2 m Minkowski
+// difference that stalled GJK a few 1e-5 m from the origin and lost sub-mm contacts the fp64
+// oracle keeps (tools/ccd_mismatch.py: 2 in 4096 stress poses).  EPA stays fp32.
+struct GSup {
+  double v[3];
+  float v1[3];
+};
+HDI double dotd(const double a[3], const double b[3]) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+HDI void subd(double r[3], const double a[3], const double b[3]) {
+  r[0] = a[0] - b[0], r[1] = a[1] - b[1], r[2] = a[2] - b[2];
+}
+HDI void crossd(double r[3], const double a[3], const double b[3]) {
+  r[0] = a[1] * b[2] - a[2] * b[1], r[1] = a[2] * b[0] - a[0] * b[2], r[2] = a[0] * b[1] - a[1] * b[0];
+}
+HDI void copyd(double d[3], const double s[3]) { d[0] = s[0], d[1] = s[1], d[2] = s[2]; }
+HDI void gsel(GSup& dst, bool c, const GSup& src) {  // (value selects: see sel)
+#pragma unroll
+  for (int k = 0; k < 3; k++) dst.v[k] = c ? src.v[k] : dst.v[k], dst.v1[k] = c ? src.v1[k] : dst.v1[k];
+}
+// support point of the Minkowski difference along the fp64 direction d (queried in fp32)
+HDI void gsup(const MPair& P, const double d[3], GSup& g) {
+  const float df[3] = {(float)d[0], (float)d[1], (float)d[2]};
+  MSup s;
+  P.sup(df, s);
+#pragma unroll
+  for (int k = 0; k < 3; k++) g.v[k] = (double)s.v1[k] - (double)s.v2[k], g.v1[k] = s.v1[k];
+}
 // closest point of simplex p[0..n) (n <= 3) to the origin; the carrying sub-simplex moves to the front
-HDI int gjk_reduce(MSup p[4], int n, float x[3]) {
+HDI int gjk_reduce(GSup p[4], int n, double x[3]) {
   if (n == 1) {
-    copy3(x, p[0].v);
+    copyd(x, p[0].v);
     return 1;
   }
   if (n == 2) {
-    float ab[3];
-    sub(ab, p[1].v, p[0].v);
-    float t = -dot3(p[0].v, ab);
-    const float l2 = dot3(ab, ab);
-    if (t <= 0.f || l2 <= 0.f) {
-      copy3(x, p[0].v);
+    double ab[3];
+    subd(ab, p[1].v, p[0].v);
+    double t = -dotd(p[0].v, ab);
+    const double l2 = dotd(ab, ab);
+    if (t <= 0.0 || l2 <= 0.0) {
+      copyd(x, p[0].v);
       return 1;
     }
     if (t >= l2) {
       p[0] = p[1];
-      copy3(x, p[0].v);
+      copyd(x, p[0].v);
       return 1;
     }
     t /= l2;
@@ -508,53 +537,53 @@ HDI int gjk_reduce(MSup p[4], int n, float x[3]) {
     for (int k = 0; k < 3; k++) x[k] = p[0].v[k] + t * ab[k];
     return 2;
   }
-  float ab[3], ac[3];
-  sub(ab, p[1].v, p[0].v);
-  sub(ac, p[2].v, p[0].v);
-  const float ap[3] = {-p[0].v[0], -p[0].v[1], -p[0].v[2]};
-  const float d1 = dot3(ab, ap), d2 = dot3(ac, ap);
-  if (d1 <= 0.f && d2 <= 0.f) {
-    copy3(x, p[0].v);
+  double ab[3], ac[3];
+  subd(ab, p[1].v, p[0].v);
+  subd(ac, p[2].v, p[0].v);
+  const double ap[3] = {-p[0].v[0], -p[0].v[1], -p[0].v[2]};
+  const double d1 = dotd(ab, ap), d2 = dotd(ac, ap);
+  if (d1 <= 0.0 && d2 <= 0.0) {
+    copyd(x, p[0].v);
     return 1;
   }
-  const float bp[3] = {-p[1].v[0], -p[1].v[1], -p[1].v[2]};
-  const float d3 = dot3(ab, bp), d4 = dot3(ac, bp);
-  if (d3 >= 0.f && d4 <= d3) {
+  const double bp[3] = {-p[1].v[0], -p[1].v[1], -p[1].v[2]};
+  const double d3 = dotd(ab, bp), d4 = dotd(ac, bp);
+  if (d3 >= 0.0 && d4 <= d3) {
     p[0] = p[1];
-    copy3(x, p[0].v);
+    copyd(x, p[0].v);
     return 1;
   }
-  const float vc = d1 * d4 - d3 * d2;
-  if (vc <= 0.f && d1 >= 0.f && d3 <= 0.f) {
-    const float t = d1 / (d1 - d3);
+  const double vc = d1 * d4 - d3 * d2;
+  if (vc <= 0.0 && d1 >= 0.0 && d3 <= 0.0) {
+    const double t = d1 / (d1 - d3);
 #pragma unroll
     for (int k = 0; k < 3; k++) x[k] = p[0].v[k] + t * ab[k];
     return 2;
   }
-  const float cp[3] = {-p[2].v[0], -p[2].v[1], -p[2].v[2]};
-  const float d5 = dot3(ab, cp), d6 = dot3(ac, cp);
-  if (d6 >= 0.f && d5 <= d6) {
+  const double cp[3] = {-p[2].v[0], -p[2].v[1], -p[2].v[2]};
+  const double d5 = dotd(ab, cp), d6 = dotd(ac, cp);
+  if (d6 >= 0.0 && d5 <= d6) {
     p[0] = p[2];
-    copy3(x, p[0].v);
+    copyd(x, p[0].v);
     return 1;
   }
-  const float vb = d5 * d2 - d1 * d6;
-  if (vb <= 0.f && d2 >= 0.f && d6 <= 0.f) {
-    const float t = d2 / (d2 - d6);
+  const double vb = d5 * d2 - d1 * d6;
+  if (vb <= 0.0 && d2 >= 0.0 && d6 <= 0.0) {
+    const double t = d2 / (d2 - d6);
 #pragma unroll
     for (int k = 0; k < 3; k++) x[k] = p[0].v[k] + t * ac[k];
     p[1] = p[2];
     return 2;
   }
-  const float va = d3 * d6 - d5 * d4;
-  if (va <= 0.f && (d4 - d3) >= 0.f && (d5 - d6) >= 0.f) {
-    const float t = (d4 - d3) / ((d4 - d3) + (d5 - d6));
+  const double va = d3 * d6 - d5 * d4;
+  if (va <= 0.0 && (d4 - d3) >= 0.0 && (d5 - d6) >= 0.0) {
+    const double t = (d4 - d3) / ((d4 - d3) + (d5 - d6));
 #pragma unroll
     for (int k = 0; k < 3; k++) x[k] = p[1].v[k] + t * (p[2].v[k] - p[1].v[k]);
     p[0] = p[2];
     return 2;
   }
-  const float den = 1.f / (va + vb + vc), v = vb * den, w = vc * den;
+  const double den = 1.0 / (va + vb + vc), v = vb * den, w = vc * den;
 #pragma unroll
   for (int k = 0; k < 3; k++) x[k] = p[0].v[k] + ab[k] * v + ac[k] * w;
   return 3;
@@ -566,30 +595,30 @@ __device__
 constexpr int TETF[4][3] = {{1, 2, 3}, {0, 3, 2}, {0, 1, 3}, {0, 2, 1}};
 // 1: origin inside tetrahedron p; 0: reduced to the face the origin lies beyond (n, x set);
 // -1: flat tetrahedron
-HDI int tet_contains(MSup p[4], float x[3], int& n) {
-  float best = 0.f;
+HDI int tet_contains(GSup p[4], double x[3], int& n) {
+  double best = 0.0;
   int bk = -1;
 #pragma unroll
   for (int k = 0; k < 4; k++) {
-    const float *a = p[TETF[k][0]].v, *b = p[TETF[k][1]].v, *c = p[TETF[k][2]].v;
-    float ab[3], ac[3], nn[3], ak[3];
-    sub(ab, b, a);
-    sub(ac, c, a);
-    cross(nn, ab, ac);
-    sub(ak, p[k].v, a);
-    const float sg = dot3(nn, ak) > 0.f ? -1.f : 1.f;
-    const float ln = sqrtf(dot3(nn, nn));
-    if (!(ln > 0.f)) return -1;
-    const float sd = -sg * dot3(nn, a) / ln;
+    const double *a = p[TETF[k][0]].v, *b = p[TETF[k][1]].v, *c = p[TETF[k][2]].v;
+    double ab[3], ac[3], nn[3], ak[3];
+    subd(ab, b, a);
+    subd(ac, c, a);
+    crossd(nn, ab, ac);
+    subd(ak, p[k].v, a);
+    const double sg = dotd(nn, ak) > 0.0 ? -1.0 : 1.0;
+    const double ln = sqrt(dotd(nn, nn));
+    if (!(ln > 0.0)) return -1;
+    const double sd = -sg * dotd(nn, a) / ln;
     if (sd > best) best = sd, bk = k;
   }
   if (bk < 0) return 1;
-  MSup t[3];
+  GSup t[3];
 #pragma unroll
   for (int j = 0; j < 3; j++) {
     t[j] = p[TETF[0][j]];
 #pragma unroll
-    for (int k = 1; k < 4; k++) sel(t[j], bk == k, p[TETF[k][j]]);
+    for (int k = 1; k < 4; k++) gsel(t[j], bk == k, p[TETF[k][j]]);
   }
   p[0] = t[0], p[1] = t[1], p[2] = t[2];
   n = gjk_reduce(p, 3, x);
@@ -597,86 +626,102 @@ HDI int tet_contains(MSup p[4], float x[3], int& n) {
 }
 // support point along d or, when the Minkowski difference reaches no further than the tolerance
 // along d, along -d (d negated then); false if neither
-HDI bool ccd_extend(const MPair& P, float d[3], MSup& s) {
-  P.sup(d, s);
-  if (dot3(d, s.v) > MPR_TOLF) return true;
+HDI bool ccd_extend(const MPair& P, double d[3], GSup& s) {
+  gsup(P, d, s);
+  if (dotd(d, s.v) > (double)MPR_TOLF) return true;
   d[0] = -d[0], d[1] = -d[1], d[2] = -d[2];
-  P.sup(d, s);
-  return dot3(d, s.v) > MPR_TOLF;
+  gsup(P, d, s);
+  return dotd(d, s.v) > (double)MPR_TOLF;
 }
 // GJK ended with the origin ON the segment p[0..1] (n = 2) or the triangle p[0..2] (n = 3):
 // centred symmetric shapes, whose second support point is exactly minus the first.  nativeccd
 // starts EPA from such simplices (polytope2 / polytope3); here a support point off the simplex's
 // span per missing dimension completes a tetrahedron with the origin on its boundary (the
 // oracle's gjk_complete).  false: no extent off the span (touching).
-HDI bool gjk_complete(const MPair& P, MSup p[4], int n) {
+HDI bool gjk_complete(const MPair& P, GSup p[4], int n) {
   if (n == 2) {  // a direction normal to the segment: u x (the axis of u's smallest component)
-    float u[3], d[3];
-    sub(u, p[1].v, p[0].v);
-    const float ax = fabsf(u[0]), ay = fabsf(u[1]), az = fabsf(u[2]);
+    double u[3], d[3];
+    subd(u, p[1].v, p[0].v);
+    const double ax = fabs(u[0]), ay = fabs(u[1]), az = fabs(u[2]);
     const int k = ax <= ay && ax <= az ? 0 : ay <= az ? 1 : 2;
-    const float e[3] = {k == 0 ? 1.f : 0.f, k == 1 ? 1.f : 0.f, k == 2 ? 1.f : 0.f};
-    cross(d, u, e);
-    if (!(dot3(d, d) > 0.f)) return false;
-    nrm(d);
+    const double e[3] = {k == 0 ? 1.0 : 0.0, k == 1 ? 1.0 : 0.0, k == 2 ? 1.0 : 0.0};
+    crossd(d, u, e);
+    const double l = sqrt(dotd(d, d));
+    if (!(l > 0.0)) return false;
+    d[0] /= l, d[1] /= l, d[2] /= l;
     if (!ccd_extend(P, d, p[2])) return false;
   }
-  float ab[3], ac[3], nn[3];
-  sub(ab, p[1].v, p[0].v);
-  sub(ac, p[2].v, p[0].v);
-  cross(nn, ab, ac);
-  if (!(dot3(nn, nn) > 0.f)) return false;
-  nrm(nn);
+  double ab[3], ac[3], nn[3];
+  subd(ab, p[1].v, p[0].v);
+  subd(ac, p[2].v, p[0].v);
+  crossd(nn, ab, ac);
+  const double l = sqrt(dotd(nn, nn));
+  if (!(l > 0.0)) return false;
+  nn[0] /= l, nn[1] /= l, nn[2] /= l;
   return ccd_extend(P, nn, p[3]);
 }
 // GJK: true with p a tetrahedron enclosing the origin (possibly on its boundary: gjk_complete);
-// false apart (sep = a separating axis when a support plane proved it) or touching
-HDI bool gjk_enclose(const MPair& P, MSup p[4], float sep[3]) {
-  float c1[3], c2[3], x[3];
+// false apart (sep = a separating axis when a support plane proved it) or touching.  The
+// thresholds are the oracle's (oracle_collision.c gjk_enclose), both in fp64.
+HDI bool gjk_enclose(const MPair& P, MSup q[4], float sep[3]) {
+  float c1[3], c2[3];
   geom_center(P.m, P.g1, P.P1, c1);
   geom_center(P.m, P.g2, P.P2, c2);
-  sub(x, c1, c2);
-  if (dot3(x, x) == 0.f) x[0] = 1e-9f;
+  double x[3] = {(double)c1[0] - c2[0], (double)c1[1] - c2[1], (double)c1[2] - c2[2]};
+  if (dotd(x, x) == 0.0) x[0] = 1e-9;
+  GSup p[4];
   int n = 0;
-  float xx_prev = 3.0e38f;
+  double xx_prev = 1e300;
+  bool in = false;
   for (int it = 0; it < CCD_ITERS; it++) {
-    const float d[3] = {-x[0], -x[1], -x[2]};
-    MSup s;
-    P.sup(d, s);
-    const float xs = dot3(x, s.v);
-    if (xs > 0.f) {  // every point of A - B has x.p >= x.s > 0: -x separates
-      float a[3] = {-x[0], -x[1], -x[2]};
+    const double d[3] = {-x[0], -x[1], -x[2]};
+    GSup s;
+    gsup(P, d, s);
+    const double xs = dotd(x, s.v);
+    if (xs > 0.0) {  // every point of A - B has x.p >= x.s > 0: -x separates
+      float a[3] = {(float)-x[0], (float)-x[1], (float)-x[2]};
       nrm(a);
       setsep(sep, a);
       return false;
     }
-    if (dot3(x, x) - xs <= 1e-12f) return false;  // no progress: the origin is on the boundary
+    if (dotd(x, x) - xs <= 1e-12) return false;  // no progress: the origin is on the boundary
 #pragma unroll
-    for (int k = 0; k < 4; k++) sel(p[k], k == n, s);
+    for (int k = 0; k < 4; k++) gsel(p[k], k == n, s);
     n++;
     if (n == 4) {
-      const MSup q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
+      const GSup t0 = p[0], t1 = p[1], t2 = p[2], t3 = p[3];
       const int r = tet_contains(p, x, n);
-      if (r == 1) return true;
+      if (r == 1) {
+        in = true;
+        break;
+      }
       if (r < 0) {  // flat: the previous triangle p[0..2], completed if it carries the origin
         n = gjk_reduce(p, 3, x);
-        if (!(dot3(x, x) < 1e-12f * dot3(s.v, s.v))) return false;
-      } else if (!(dot3(x, x) < xx_prev)) {
-        // no progress: the origin is within rounding of this tetrahedron's face (a large flat
-        // Minkowski difference -- the table box -- whose closest-point direction fp32 resolves
-        // to ~1e-7 only, so the support along it returns the same vertex again): EPA from the
+        if (!(dotd(x, x) < 1e-12 * dotd(s.v, s.v))) return false;
+      } else if (!(dotd(x, x) < xx_prev)) {
+        // no progress (the support along x returns a vertex already held): EPA from this
         // tetrahedron decides (a face with d < 0 at the end: apart)
-        p[0] = q0, p[1] = q1, p[2] = q2, p[3] = q3;
-        return true;
+        p[0] = t0, p[1] = t1, p[2] = t2, p[3] = t3;
+        in = true;
+        break;
       }
     } else {
       n = gjk_reduce(p, n, x);
     }
-    xx_prev = dot3(x, x);
+    xx_prev = dotd(x, x);
     // the origin on the simplex up to rounding (|x| < 1e-6 of the support point's scale)
-    if (dot3(x, x) < 1e-12f * dot3(s.v, s.v)) return n >= 2 && gjk_complete(P, p, n);
+    if (dotd(x, x) < 1e-12 * dotd(s.v, s.v)) {
+      in = n >= 2 && gjk_complete(P, p, n);
+      break;
+    }
   }
-  return false;
+  if (!in) return false;
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+#pragma unroll
+    for (int c = 0; c < 3; c++)
+      q[k].v[c] = (float)p[k].v[c], q[k].v1[c] = p[k].v1[c], q[k].v2[c] = p[k].v1[c] - q[k].v[c];
+  return true;
 }
 struct EpaFace {
   uint32_t abc;  // vertex ids, 8 bits each
@@ -1117,6 +1162,52 @@ HDI void write_geom_poses(const Sim<NA, NF>& S, float* __restrict__ gpose, int n
         soa(gpose, g * GREC + 15 + k, n, e) = fabsf(R[3 * k]) * m.geom_half[g][0] + fabsf(R[3 * k + 1]) * m.geom_half[g][1] +
                                               fabsf(R[3 * k + 2]) * m.geom_half[g][2];
       }
+    }
+  }
+}
+
+// write_geom_poses with one geom per lane (lane g0 of gstep: geoms g0, g0 + gstep, ...): the env's
+// body frames go to LDS first (fr: this env's 12 * NB floats, free at this point), so each lane
+// reads its geom's body frame by index.  The per-body walk above runs its geom code once per body
+// with most lanes masked and pays the model loads' latency per body; here once (RS kernel: 16
+// lanes per env cover its 15 geoms in one pass).
+template <int NA, int NF>
+__device__ __forceinline__ void write_geom_poses_lds(const Sim<NA, NF>& S, float* __restrict__ gpose, int n, int e,
+                                                     int g0, int gstep, float* fr) {
+  const DModel& m = *S.mp;
+  constexpr int NB = Sim<NA, NF>::NB;
+  // (every lane of the env writes the same values: one store per float per env)
+#pragma unroll
+  for (int b = 0; b < NB; b++) {
+#pragma unroll
+    for (int c = 0; c < 3; c++) fr[b * 12 + c] = b > 0 ? S.xpos[b][c] : 0.f;
+#pragma unroll
+    for (int c = 0; c < 9; c++) fr[b * 12 + 3 + c] = b > 0 ? S.xmat[b][c] : (c % 4 == 0 ? 1.f : 0.f);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  for (int g = g0; g < m.ngeom; g += gstep) {
+    const float* f = fr + m.geom_bodyid[g] * 12;
+    float bp[3], bR[9];
+#pragma unroll
+    for (int c = 0; c < 3; c++) bp[c] = f[c];
+#pragma unroll
+    for (int c = 0; c < 9; c++) bR[c] = f[3 + c];
+    const float gp[3] = {m.geom_pos[g][0], m.geom_pos[g][1], m.geom_pos[g][2]};
+    float w[3], R[9];
+    mv(w, bR, gp);
+    mm(R, bR, m.geom_mat[g]);
+    GeomPose P;
+#pragma unroll
+    for (int c = 0; c < 3; c++) P.p[c] = bp[c] + w[c], soa(gpose, g * GREC + c, n, e) = P.p[c];
+#pragma unroll
+    for (int c = 0; c < 9; c++) P.R[c] = R[c], soa(gpose, g * GREC + 3 + c, n, e) = R[c];
+    float cc[3];
+    geom_center(m, g, P, cc);
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      soa(gpose, g * GREC + 12 + k, n, e) = cc[k];
+      soa(gpose, g * GREC + 15 + k, n, e) = fabsf(R[3 * k]) * m.geom_half[g][0] + fabsf(R[3 * k + 1]) * m.geom_half[g][1] +
+                                            fabsf(R[3 * k + 2]) * m.geom_half[g][2];
     }
   }
 }

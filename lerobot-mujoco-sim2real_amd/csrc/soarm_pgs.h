@@ -44,10 +44,12 @@ __device__ long long g_stamp[65536 * 16];
 // RS solve's split).  Lane 0 of each wave owns its row and launches are stream-ordered, so plain
 // read-modify-writes: shared-address atomics from every wave queued behind the profiled kernel's own
 // loads and inflated the phases after the solve ~15x (r05).  sim_phase_profile reduces the rows.
-// [82..84]: RS-kernel waves that took the v-form fallback -- count, max and summed wave cycles.
-constexpr int WPH = 85, WPH_MAXW = 16384;
+// [82..84]: RS-kernel waves that took the v-form fallback -- count, max and summed wave cycles;
+// [85..91] lanes of such waves by cause (rs_why bits).
+constexpr int WPH = 92, WPH_MAXW = 16384;
 __device__ unsigned long long g_wphase[WPH_MAXW * WPH];
 #define WPH_ID() (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6)
+__device__ int g_rs_force11;  // (set from SOARM_RS_FORCE11 by the launch code)
 #define WPH_ADD(k, v) g_wphase[WPH_ID() * WPH + (k)] += (unsigned long long)(v)
 #define WPH_MAX(k, v) \
   g_wphase[WPH_ID() * WPH + (k)] = max(g_wphase[WPH_ID() * WPH + (k)], (unsigned long long)(v))
@@ -164,8 +166,8 @@ enum { L_DOF = 0, L_SGN = 1, L_AREF = 2, L_R = 3, L_ARD = 4, L_IARD = 5, L_FRC =
 // kept broadcast in every lane of the env) take it: two dependent instructions per row.
 // The improvement of mj_solPGS's stopping test is the sweep's exact cost change: with
 // res = AR f + b, cost(f0) - cost(f1) = sum_r AR_rr / 2 (f1 - f0)_r (s0 + s1)_r, and each
-// row's force change over the sweep comes from a second accumulator beside s that takes
-// the off-diagonal steps only (u_r = sum_{q != r} C_rq d_q, so Delta f_r = u_r - Delta s_r).
+// row's force change over the sweep is its own step, which a second accumulator beside s takes
+// exactly (its coefficient is 1 at the row's own step, 0 elsewhere).
 constexpr int RS_MAXROW = 32;               // rows of one env (2 slots x 16 lanes)
 constexpr int RS_WROW = 12;                 // floats per row of W = M^-1 J' in LDS (NV <= 12)
 constexpr int RS_WENV = RS_MAXROW * RS_WROW + 4;  // per env (+4: the 4 envs of a wave on distinct banks)
@@ -235,7 +237,7 @@ struct RsLayout {
     return (sl == 0 ? upd_a(q) : upd_b(q)) ? ((upd_a(q) && upd_b(q)) ? 1 : 0) + 1 + (q < NA ? 1 : 0) : 2;
   }
 };
-// one sweep of the row-space PGS (see above): s = (residual, off-diagonal accumulator) per slot,
+// one sweep of the row-space PGS (see above): s = (residual, own-step accumulator) per slot,
 // C = (C, G) pairs per step, NF = lo - f of every row, NH = hi - f of the NA frictionloss rows (the
 // others have hi = +inf).  Instruction order is pinned (sched_barrier): a DPP op waits for every
 // VALU op in flight, so a step is its broadcast-max, the residual update of the slot the NEXT step
@@ -499,6 +501,9 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
   // Gram blocks / edge ARdiag nor the warm start below (rs_solve builds its own)
   bool rs_fast = false;
   int rs_nat = 0, rs_nct = 0, rs_nac = 0;  // contacts per category (RsLayout): arm-only, free body alone, both
+#ifdef SOARM_PHASE_PROF
+  int rs_why = 0;  // why a wave takes the fallback (bits: limit, overflow, order, CT>4, AT>1, AC>1, AT+AC)
+#endif
   // ---- dof frictionloss rows (MuJoCo row order: all of them first)
   float ff[NA], fa[NA], fR[NA], fhD[NA], fiD[NA];
 #pragma unroll
@@ -725,9 +730,18 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
           rs_nat += cat == 0, rs_nct += cat == 1, rs_nac += cat == 2;
         }
         // the layouts instantiated: (KAT, KAC) = (0, 0) the cube resting alone, (1, 0) plus one
-        // arm-only contact, (0, 1) plus one arm-cube contact; other waves take the v-form sweeps
+        // arm-only contact, (0, 1) plus one arm-cube contact, (1, 1) both, in one env or in two envs
+        // of the wave (without it those waves -- ~1 launch in 10 over steps 20-120 -- took the v-form
+        // sweeps at ~4x the wave time); other waves take the v-form sweeps
+#ifdef SOARM_PHASE_PROF
+        rs_why = (nlim > 0) | ((ncon > LDS_CON) << 1) | ((!ok && nlim == 0 && ncon <= LDS_CON) << 2) |
+                 ((rs_nct > 4) << 3) | ((rs_nat > 1) << 4) | ((rs_nac > 1) << 5);
+#endif
         ok = ok && rs_nct <= 4 && rs_nat <= 1 && rs_nac <= 1;
-        rs_fast = __all(ok) && !(__any(rs_nat >= 1) && __any(rs_nac >= 1));
+        rs_fast = __all(ok);
+#ifdef SOARM_PHASE_PROF
+        rs_why |= (!rs_fast && ok) << 6;  // an env that fits, in a wave with one that does not
+#endif
       }
       const int nlds = ncon < LDS_CON ? ncon : LDS_CON;
       constexpr int SPL = RS ? 16 : 4;  // the RS kernel: the env's 16 lanes split the build
@@ -2185,8 +2199,11 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
 #pragma unroll
       for (int i = 0; i < NV; i++) jvA = fmaf(JA[i], v[i], jvA), jvB = fmaf(JB[i], v[i], jvB);
       f2 sA = f2{-fmaf(RA, fA, jvA) * iA, 0.f}, sB = f2{-fmaf(RB, fB, jvB) * iB, 0.f};
-      // the scaled matrix: C[r][q] = -J_r W_q / AR_rr, C[r][r] = -1, as (C, G) pairs: G is C with a
-      // zero diagonal (the accumulator of the off-diagonal steps); only the blocks a step updates
+      // the scaled matrix: C[r][q] = -J_r W_q / AR_rr, C[r][r] = -1, as (C, G) pairs: G is the row's
+      // own-step indicator, so the second accumulator takes the row's force step exactly (the stop
+      // test's Delta f_r; it was u_r - Delta s_r from an off-diagonal accumulator, whose fp32
+      // cancellation stopped an ill-conditioned env 22 sweeps early, 3.3e-3 m/s off -- r05); only
+      // the blocks a step updates
       f2 CA[NS], CB[NS];
       sfor<NS>([&](auto qc) {
         constexpr int q = decltype(qc)::value;
@@ -2196,8 +2213,8 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
         for (int i = 0; i < NV; i++)
           a = fma2(f2{UA ? JA[i] : 0.f, UB ? JB[i] : 0.f}, splat2(Wl[q * RS_WROW + i]), a);
         const float ca = -a.x * iA, cb = -a.y * iB;
-        CA[q] = qA == q ? f2{-1.f, 0.f} : f2{ca, ca};
-        CB[q] = qB == q ? f2{-1.f, 0.f} : f2{cb, cb};
+        CA[q] = qA == q ? f2{-1.f, 1.f} : f2{ca, 0.f};
+        CB[q] = qB == q ? f2{-1.f, 1.f} : f2{cb, 0.f};
         // (the W rows of two steps in flight at a time: hoisting every step's 12 LDS loads to
         // the top would hold hundreds of values)
         if constexpr (q & 1) __builtin_amdgcn_sched_barrier(0);
@@ -2225,9 +2242,9 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
           const float s0A = sA.x, s0B = sB.x;
           sA.y = 0.f, sB.y = 0.f;
           rs_sweep<NA, LY>(sA, sB, CA, CB, NF_, NH_);
-          // Delta f_r = u_r - Delta s_r; improvement = sum_r AR_rr / 2 Delta f_r (s0 + s1)_r
-          float P = hdA * (sA.y - (sA.x - s0A)) * (s0A + sA.x);
-          P = fmaf(hdB * (sB.y - (sB.x - s0B)), s0B + sB.x, P);
+          // improvement = sum_r AR_rr / 2 Delta f_r (s0 + s1)_r, Delta f_r = the row's own step (y)
+          float P = hdA * sA.y * (s0A + sA.x);
+          P = fmaf(hdB * sB.y, s0B + sB.x, P);
           done = rowsum16(P) * scale < tol;
         }
         if (__all(done)) break;
@@ -2263,8 +2280,13 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
     if (rs_fast) {
       using Z = std::integral_constant<int, 0>;
       using O = std::integral_constant<int, 1>;
-      const int kat = __any(rs_nat >= 1) ? 1 : 0, kac = __any(rs_nac >= 1) ? 1 : 0;
-      if (kac == 1)
+      int kat = __any(rs_nat >= 1) ? 1 : 0, kac = __any(rs_nac >= 1) ? 1 : 0;
+#ifdef SOARM_PHASE_PROF
+      if (g_rs_force11) kat = kac = 1;  // (diagnostic: every RS wave in the (1, 1) layout)
+#endif
+      if (kac == 1 && kat == 1)
+        rs_solve(O{}, O{});
+      else if (kac == 1)
         rs_solve(Z{}, O{});
       else if (kat == 1)
         rs_solve(O{}, Z{});
@@ -2326,7 +2348,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
     g_pgs_prof[8 * e + 3] = (ypure ? 0 : yext ? 1 : block_first ? 2 : 3) | (npost > 0 && npost_free ? 16 : 0) |
                             (min(npost, 3) << 8) | (min(nfree_x, 3) << 12) | ((nl > 5) << 16) | ((nlim > 0) << 17) |
                             ((nl != ncon) << 18) | ((long long)min(armstop, 255) << 20) |
-                            ((long long)(yext ? 4 + 2 * yext2 + ycoupled : 0) << 28) | ((long long)(RS && !rs_fast) << 40),
+                            ((long long)(yext ? 4 + 2 * yext2 + ycoupled : 0) << 28) | ((long long)(RS && !rs_fast) << 40) | ((long long)rs_why << 41),
     g_pgs_prof[8 * e + 4] = nlim, g_pgs_prof[8 * e + 5] = ncon;
 #endif
 

@@ -1001,6 +1001,10 @@ int sim_step(sim_batch* b, const sim_state* s, const float* action, int frame_sk
         if (const char* v = getenv("SOARM_LDS_PAD")) lds_pad = (size_t)atol(v);
         // (SOARM_DIAG_NOGPOSE: the substep writes no geom records -- timing only, wrong contacts)
         const bool nogpose = getenv("SOARM_DIAG_NOGPOSE") != nullptr;
+        {
+          const int f11 = getenv("SOARM_RS_FORCE11") != nullptr;
+          (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_rs_force11), &f11, sizeof(f11), 0, hipMemcpyHostToDevice, q);
+        }
 #else
         constexpr bool nogpose = false;
 #endif
@@ -1138,6 +1142,7 @@ int sim_phase_profile(double* out, int reset) {
   out[77 + 8] = (double)h[77], out[77 + 9] = (double)h[78], out[77 + 10] = (double)h[79];
   out[77 + 11] = (double)h[80], out[77 + 16] = (double)h[81];
   out[77 + 17] = (double)h[82], out[77 + 18] = (double)h[83], out[77 + 19] = (double)h[84];  // RS fallback waves
+  for (int k = 0; k < 7; k++) out[101 + k] = (double)h[85 + k];  // (callers pass >= 108 doubles)
   if (reset) {
     void* a = nullptr;
     HIPCHECK(hipGetSymbolAddress(&a, HIP_SYMBOL(g_wphase)));

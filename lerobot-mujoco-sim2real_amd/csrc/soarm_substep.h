@@ -232,7 +232,10 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
   if (gpose) {
     S.kinematics();
     PSTAMP(14);
-    write_geom_poses(S, gpose, n, e, (int)threadIdx.x % LPE, LPE);
+    if constexpr (RS)  // (the W rows' LDS is free after the solve: the body frames go there)
+      write_geom_poses_lds(S, gpose, n, e, (int)threadIdx.x % LPE, LPE, s_rsw + L.col * RS_WENV);
+    else
+      write_geom_poses(S, gpose, n, e, (int)threadIdx.x % LPE, LPE);
   } else {
     PSTAMP(14);  // (the last substep writes no poses: both phases empty)
   }
@@ -264,6 +267,9 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
   census[7] = wsum(ny && ((cv >> 16) & 1)), census[8] = wsum(ny && ((cv >> 17) & 1)),
   census[9] = wsum(ny && ((cv >> 18) & 1));
   const int nsw_sum = wsum(nsw), lanes = wsum(1);
+  int why[7];
+#pragma unroll
+  for (int k = 0; k < 7; k++) why[k] = wsum((int)((cv >> (41 + k)) & 1));
   if ((threadIdx.x & 63) == 0 && WPH_ID() < WPH_MAXW) {
     WPH_MAX(15, cmax);
     WPH_ADD(6, nsw_sum);
@@ -294,7 +300,11 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
     WPH_MAX(10, p1 - p0);
     WPH_ADD(11, wmax);
     WPH_ADD(5, 1);
-    if (__any((g_pgs_prof[8 * e + 3] >> 40) & 1)) WPH_ADD(82, 1), WPH_MAX(83, t5 - t0), WPH_ADD(84, t5 - t0);
+    if ((cv >> 40) & 1) {
+      WPH_ADD(82, 1), WPH_MAX(83, t5 - t0), WPH_ADD(84, t5 - t0);
+#pragma unroll
+      for (int k = 0; k < 7; k++) WPH_ADD(85 + k, why[k]);
+    }
     const int ast = (int)((g_pgs_prof[8 * e + 3] >> 20) & 255);
     if (ast) WPH_ADD(57, 1), WPH_ADD(58, ast);
     WPH_MAX(ast ? 60 : 59, t5 - t0);

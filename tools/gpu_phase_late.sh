@@ -10,5 +10,5 @@ for l in open("gpurun_out/phase_rs1.log"):
     print(t, "mean", round(r["cycles_per_wave"]), "max", r["max_wave_cycles"], "maxpgs", r["max_wave_pgs_cycles"],
           "variants", {k: round(v, 4) for k, v in r["variant_waves"].items()}, "vmax", r["variant_max_cycles"],
           "nonblock", r["waves_with_nonblock_contact"], "maxncon", r["max_ncon"], "lim", r["waves_with_limit"])
-    print("   rs", {k: round(v, 2) for k, v in r.get("rs", {}).items()})
+    print("   rs", {k: (round(v, 2) if not isinstance(v, dict) else v) for k, v in r.get("rs", {}).items()})
 PY

@@ -44,7 +44,7 @@ q0 = W.initial_qpos(cm, ids, 0)
 sim.reset(init_qpos=q0[:, :5], extra_qpos=q0, seed=0)
 tab = {k: (torch.as_tensor(v, dtype=torch.float32, device="cuda") if isinstance(v, np.ndarray) else v)
        for k, v in W.chirp_tables(ids, 0).items()}
-out = (ctypes.c_double * 101)()
+out = (ctypes.c_double * 108)()
 res = {}
 every = int(os.environ.get("EVERY", 0))
 starts = set(range(0, T, every)) if every else {0, T // 2, T - 10}
@@ -94,7 +94,9 @@ for t in range(T):
                        "final_cycles_per_wave": v[77 + 10] / w, "sweeps_per_wave": v[77 + 16] / w,
                        "cycles_per_sweep": v[77 + 9] / max(v[77 + 16], 1),
                        "fallback_waves_per_launch": v[77 + 17] / max(v[5] / (n // 4), 1),
-                       "fallback_max_cycles": v[77 + 18], "fallback_mean_cycles": v[77 + 19] / max(v[77 + 17], 1)}
+                       "fallback_max_cycles": v[77 + 18], "fallback_mean_cycles": v[77 + 19] / max(v[77 + 17], 1),
+                       "fallback_lanes_by_cause": dict(zip(["limit", "overflow", "order", "ct>4", "at>1", "ac>1", "at+ac"],
+                                                           [v[101 + k] for k in range(7)]))}
         if v[77] > 0:
             r["newton"] = {"solves": v[77], "mean_iters": v[78] / v[77], "mean_ls_evals": v[79] / v[77],
                            "coupled_frac": v[80] / v[77], "mean_cycles": v[81] / v[77], "max_cycles": v[82],
