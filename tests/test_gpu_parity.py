@@ -359,10 +359,11 @@ def test_one_substep_extra_contact_sweeps(gpu_lib):
     orc.step(sub, None, nsub=1)
     np.testing.assert_allclose(to_np(S.qpos).T, sub["qpos"], atol=5e-6)
     dv = np.abs(to_np(S.qvel).T - sub["qvel"]).max(1)
-    # the waves of these lanes run the extra-slot sweep variants: every env here carries arm
-    # contacts, where fp32 and fp64 PGS stop a sweep apart more often (r03: p50 3.9e-6, p99
-    # 1.5e-5, max 3.3e-5 on this sample; arm-contact envs of the 4096 bench states: max 2.4e-4)
-    assert_pct(dv, 4e-5, 2.5e-3, 2.5e-3, what="qvel")
+    # every env here carries arm contacts; the RS kernel sweeps all their rows in mj_solPGS order
+    # (layouts (1, 0), (0, 1), (1, 1)) with no retirement (r05 tools/rs_cat.py on the 4096 bench
+    # states at t = 100: arm-only extra max 1.5e-5, arm-cube 6.6e-6, both 4.6e-6; VERDICT r4's
+    # p99 2e-4 / max 5e-4)
+    assert_pct(dv, 4e-5, 2e-4, 5e-4, what="qvel")
     assert to_np(S.ncon).sum() == sub["ncon"].sum()
 
 
@@ -927,9 +928,9 @@ def test_pgs_vs_reference_newton(gpu_lib):
     default Newton solver (SOARM101/SO101/scene_with_table_v.xml:1-32, SOARM101_Env.py:131-132).
     The device's PGS (north star) against the exact optimum of the same constraint problem (oracle
     Newton, tolerance 0), one substep from bench states at t = 20 and 120, 1024 envs.  Bars from
-    the 4096-env measurement (profiles/r03_newton_gap.json): block envs (cube resting) cube qvel
-    p50 1.9e-5 / 3.6e-5, p99 3.6e-5, max 3.7e-5; arm-contact envs cube qvel max 7.1e-3, arm qvel
-    max 2.4e-4; arm qvel elsewhere <= 1.6e-7."""
+    the 4096-env measurement (profiles/r05_rs_bars.json): block envs (cube resting) cube qvel
+    p50 1.9e-5 / 3.6e-5, p99 3.6e-5, max 3.7e-5; arm-contact envs cube qvel p99 6.5e-3 / max
+    7.1e-3, arm qvel p99 2.3e-4 / max 2.4e-4; arm qvel elsewhere <= 1.2e-7."""
     for t0 in (20, 120):
         cm, orc, st, _ = _bench_states("contact", 1024, t0, nthreads=16)
         ref = _exact_newton_substep(cm, st)
@@ -951,14 +952,19 @@ def test_pgs_vs_reference_newton(gpu_lib):
             # identical in the fp64 oracle PGS, which the device PGS must match within QVEL_BARS
             # (the p50 bars need a sample: with fewer than 8 such envs the median is one env's
             # gap and only the max bars apply)
+            # (r05, 4096 envs at t = 120, tools/rs_bars.py: cube qvel p99 6.5e-3 / max 7.1e-3, arm
+            # qvel p99 2.3e-4 / max 2.4e-4 -- the oracle's own PGS is 7.1e-3 / 1.9e-4 from the
+            # optimum; the bars are ~2x those p99)
             few = arm.sum() < 8
-            assert_pct(dv[arm, 6:].max(1), 1.5e-2 if few else 8e-5, 1.5e-2, 1.5e-2,
+            assert_pct(dv[arm, 6:].max(1), 1.3e-2 if few else 8e-5, 1.3e-2, 1.4e-2,
                        what=f"t{t0} arm-contact envs cube qvel")
             assert_pct(dv[arm, :6].max(1), 5e-4 if few else 1e-5, 5e-4, 5e-4, what=f"t{t0} arm-contact envs arm qvel")
             pgs = {k: v[arm].copy() for k, v in st.items()}
             orc.step(pgs, None, nsub=1)
-            dp = np.abs(to_np(S.qvel).T[arm] - pgs["qvel"])
-            assert dp.max() <= QVEL_BARS[2], ("device PGS vs oracle PGS on arm-contact envs", dp.max(0))
+            dp = np.abs(to_np(S.qvel).T[arm] - pgs["qvel"]).max(1)
+            # device PGS against the oracle's mj_solPGS on the same rows (r05 4096 envs: arm-contact
+            # envs p99 2.1e-4 / max 2.4e-4 at t = 120, 9.4e-5 / 9.6e-5 at t = 20)
+            assert_pct(dp, 1e-4, 3e-4, 5e-4, what=f"t{t0} device PGS vs oracle PGS, arm-contact envs")
 
 
 @pytest.mark.parametrize("t0", [20, 120])
