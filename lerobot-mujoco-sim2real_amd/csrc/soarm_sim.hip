@@ -139,6 +139,7 @@ struct sim_batch {
     }
   };
   bool use_graphs = true;
+  int rs_cap = 0;  // envs the RS substep runs in one round (4 per wave, one wave per SIMD)
   hipStream_t cap_stream = nullptr;
   std::vector<std::pair<GraphKey, hipGraphExec_t>> graphs;
   void drop_graphs() {
@@ -855,6 +856,13 @@ int sim_batch_create(const sim_model* m, int n_envs, int device, sim_batch** out
   B->n = n_envs;
   if (const char* ng = getenv("SOARM_NO_GRAPH")) B->use_graphs = ng[0] != '1';
   B->device = device;
+  {  // the RS kernel holds one wave per SIMD (256 VGPRs + AGPRs): past 4 envs per SIMD its waves
+     // run in a second round, where the quad kernel's 16-env waves still fit in one (r05: 8192
+     // envs 5.2 M env-steps/s RS against 7.9 M quad)
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess)
+      B->rs_cap = cus * 4 * RS_EPW;
+  }
   if (int rc = upload_model(m, device, &B->d_model)) {
     delete B;
     return rc;
@@ -931,8 +939,9 @@ int sim_reset(sim_batch* b, const sim_state* s, const float* init_qpos, const fl
   return SIM_OK;
 }
 
-// the row-space PGS substep (k_substep<..., RS>) for the scene with a free body; SOARM_RS=0 selects
-// the quad kernel (16 envs per wave), read when the env-step is enqueued
+// the row-space PGS substep (k_substep<..., RS>) for the scene with a free body, up to rs_cap envs
+// (one round of waves); SOARM_RS=0 selects the quad kernel (16 envs per wave), read when the
+// env-step is enqueued
 static bool rs_on() {
   const char* v = getenv("SOARM_RS");
   return !(v && v[0] == '0');
@@ -990,7 +999,7 @@ int sim_step(sim_batch* b, const sim_state* s, const float* action, int frame_sk
         auto kern = s->qfrc_applied ? k_substep<NA, NF, true, SOL> : k_substep<NA, NF, false, SOL>;
         int epb = 64 / lpe<NF>();  // envs per 64-thread workgroup
         if constexpr (NF == 1 && SOL == SIM_SOL_PGS) {
-          if (rs_on()) {
+          if (rs_on() && b->n <= b->rs_cap) {
             kern = s->qfrc_applied ? k_substep<NA, NF, true, SOL, true> : k_substep<NA, NF, false, SOL, true>;
             epb = RS_EPW;
           }
