@@ -76,8 +76,6 @@ struct DModel {
   const int32_t* hull_adj;   // local neighbour ids
   const uint16_t* hull_lut;  // per mesh geom: HULL_LUT_CELLS start vertices (cube-map of directions)
   int geom_lutadr[MAXG];     // first LUT entry of each mesh geom (-1: not a mesh)
-  // geoms grouped by body: geom_bybody[body_gadr[b] .. + body_gnum[b]) are body b's geoms
-  int body_gadr[MAXB], body_gnum[MAXB], geom_bybody[MAXG];
   // hill-climbing records, 32 B per vertex (two uint4): [0] x, y, z (float bits), degree |
   // overflow offset << 8; [1] the first 8 neighbour ids (local, uint16, padded with the
   // vertex itself).  Neighbours past 8 live in hull_ovf.  hull_lutrec holds, per LUT cell

@@ -50,22 +50,13 @@ struct GeomPose {
   float p[3], R[9];
 };
 
-// geom world records in global memory, SoA [geom*GREC + k][env]: position (3), rotation (9), then
-// what the midphase reads -- the world centre of the geom's collision box (3) and that box's
-// world-axis half-extents |R| h (3) -- so a pair the midphase rejects (~80 of the 86 candidate pairs
-// of an env) costs 12 loads instead of the 24 of two full poses; the values are the ones the
-// midphase computed from the poses before (same expressions), so its decisions are unchanged
-constexpr int GREC = 18;
-HDI void load_pose(const float* __restrict__ gpose, int n, int e, int g, GeomPose& o) {
-#pragma unroll
-  for (int k = 0; k < 3; k++) o.p[k] = soa(gpose, g * GREC + k, n, e);
-#pragma unroll
-  for (int k = 0; k < 9; k++) o.R[k] = soa(gpose, g * GREC + 3 + k, n, e);
-}
-HDI void load_bound(const float* __restrict__ gpose, int n, int e, int g, float c[3], float h[3]) {
-#pragma unroll
-  for (int k = 0; k < 3; k++) c[k] = soa(gpose, g * GREC + 12 + k, n, e), h[k] = soa(gpose, g * GREC + 15 + k, n, e);
-}
+// body world frames in global memory, SoA [body*BREC + k][env]: position (3), rotation (9) of every
+// body but the world (its slot stays unused).  The collide composes a geom's pose and midphase bound
+// from its body's frame (load_pose / geom_bound below, the expressions that wrote per-geom records
+// until round 5, so every value is the same): 12 floats per body instead of 18 per geom -- the 8
+// body frames of the pick scene are 96 floats per env against the 15 geom records' 270, written by
+// every substep and read by every collide.
+constexpr int BREC = 12;
 
 // contacts of one candidate pair (<= 4: box-box / plane-box corners; 1 otherwise), written
 // straight to the pair's slots of the contact buffer cbuf [slot*7 + f][env]: f = dist, pos(3),
@@ -1122,107 +1113,81 @@ HDI void box_box(const DModel& m, int g1, int g2, const GeomPose& P1, const Geom
   emit(o, -best / 1.05f, pos, bn);
 }
 
-// world records (pose + midphase bound, GREC floats) of every collidable geom of this env;
-// lane g0 of gstep writes geoms g0, g0 + gstep, ... of the body-grouped geom order (geom_bybody),
-// so the geoms spread evenly over an env's lanes whatever the bodies' geom counts
+// the env's body world frames (BREC floats each, bodies 1 .. NB-1); lane g0 of gstep writes the
+// floats f = g0, g0 + gstep, ... of the env's record (f = (b - 1) * BREC + k, compile-time body and
+// component: the frame is read with constant register indices)
 template <int NA, int NF>
-HDI void write_geom_poses(const Sim<NA, NF>& S, float* __restrict__ gpose, int n, int e, int g0 = 0,
+HDI void write_body_frames(const Sim<NA, NF>& S, float* __restrict__ gpose, int n, int e, int g0 = 0,
                            int gstep = 1) {
-  // bodies in compile-time order, each body's geoms from a wave-uniform list: the body frame
-  // is read with constant indices (a per-lane body id would select it with 12 v_cndmask per
-  // body)
-  const DModel& m = *S.mp;
   constexpr int NB = Sim<NA, NF>::NB;
 #pragma unroll
-  for (int b = 0; b < NB; b++) {
-    float bp[3] = {0, 0, 0}, bR[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
-    if (b > 0) {
+  for (int b = 1; b < NB; b++) {
 #pragma unroll
-      for (int c = 0; c < 3; c++) bp[c] = S.xpos[b][c];
-#pragma unroll
-      for (int c = 0; c < 9; c++) bR[c] = S.xmat[b][c];
-    }
-    const int adr = m.body_gadr[b], num = m.body_gnum[b];
-    for (int t = ((g0 - adr) % gstep + gstep) % gstep; t < num; t += gstep) {
-      const int g = m.geom_bybody[adr + t];
-      const float gp[3] = {m.geom_pos[g][0], m.geom_pos[g][1], m.geom_pos[g][2]};
-      float w[3], R[9];
-      mv(w, bR, gp);
-      mm(R, bR, m.geom_mat[g]);
-      GeomPose P;
-#pragma unroll
-      for (int c = 0; c < 3; c++) P.p[c] = bp[c] + w[c], soa(gpose, g * GREC + c, n, e) = P.p[c];
-#pragma unroll
-      for (int c = 0; c < 9; c++) P.R[c] = R[c], soa(gpose, g * GREC + 3 + c, n, e) = R[c];
-      float cc[3];
-      geom_center(m, g, P, cc);
-#pragma unroll
-      for (int k = 0; k < 3; k++) {
-        soa(gpose, g * GREC + 12 + k, n, e) = cc[k];
-        soa(gpose, g * GREC + 15 + k, n, e) = fabsf(R[3 * k]) * m.geom_half[g][0] + fabsf(R[3 * k + 1]) * m.geom_half[g][1] +
-                                              fabsf(R[3 * k + 2]) * m.geom_half[g][2];
-      }
+    for (int k = 0; k < BREC; k++) {
+      const int f = (b - 1) * BREC + k;
+      if (f % gstep == g0) soa(gpose, b * BREC + k, n, e) = k < 3 ? S.xpos[b][k] : S.xmat[b][k - 3];
     }
   }
 }
-
-// write_geom_poses with one geom per lane (lane g0 of gstep: geoms g0, g0 + gstep, ...): the env's
-// body frames go to LDS first (fr: this env's 12 * NB floats, free at this point), so each lane
-// reads its geom's body frame by index.  The per-body walk above runs its geom code once per body
-// with most lanes masked and pays the model loads' latency per body; here once (RS kernel: 16
-// lanes per env cover its 15 geoms in one pass).
+// the same from the env's 16 lanes via LDS (fr: 12 * NB floats of this env, free at this point): the
+// frames are staged once, then lane g0 of gstep stores floats g0, g0 + gstep, ... -- one store
+// instruction covers 16 consecutive floats of each of the wave's 4 envs
 template <int NA, int NF>
-__device__ __forceinline__ void write_geom_poses_lds(const Sim<NA, NF>& S, float* __restrict__ gpose, int n, int e,
-                                                     int g0, int gstep, float* fr) {
-  const DModel& m = *S.mp;
+__device__ __forceinline__ void write_body_frames_lds(const Sim<NA, NF>& S, float* __restrict__ gpose, int n,
+                                                      int e, int g0, int gstep, float* fr) {
   constexpr int NB = Sim<NA, NF>::NB;
-  // (every lane of the env writes the same values: one store per float per env)
+  // (every lane of the env writes the same values: one LDS store per float per env)
 #pragma unroll
-  for (int b = 0; b < NB; b++) {
+  for (int b = 1; b < NB; b++) {
 #pragma unroll
-    for (int c = 0; c < 3; c++) fr[b * 12 + c] = b > 0 ? S.xpos[b][c] : 0.f;
+    for (int c = 0; c < 3; c++) fr[b * BREC + c] = S.xpos[b][c];
 #pragma unroll
-    for (int c = 0; c < 9; c++) fr[b * 12 + 3 + c] = b > 0 ? S.xmat[b][c] : (c % 4 == 0 ? 1.f : 0.f);
+    for (int c = 0; c < 9; c++) fr[b * BREC + 3 + c] = S.xmat[b][c];
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-  for (int g = g0; g < m.ngeom; g += gstep) {
-    const float* f = fr + m.geom_bodyid[g] * 12;
-    float bp[3], bR[9];
-#pragma unroll
-    for (int c = 0; c < 3; c++) bp[c] = f[c];
-#pragma unroll
-    for (int c = 0; c < 9; c++) bR[c] = f[3 + c];
-    const float gp[3] = {m.geom_pos[g][0], m.geom_pos[g][1], m.geom_pos[g][2]};
-    float w[3], R[9];
-    mv(w, bR, gp);
-    mm(R, bR, m.geom_mat[g]);
-    GeomPose P;
-#pragma unroll
-    for (int c = 0; c < 3; c++) P.p[c] = bp[c] + w[c], soa(gpose, g * GREC + c, n, e) = P.p[c];
-#pragma unroll
-    for (int c = 0; c < 9; c++) P.R[c] = R[c], soa(gpose, g * GREC + 3 + c, n, e) = R[c];
-    float cc[3];
-    geom_center(m, g, P, cc);
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-      soa(gpose, g * GREC + 12 + k, n, e) = cc[k];
-      soa(gpose, g * GREC + 15 + k, n, e) = fabsf(R[3 * k]) * m.geom_half[g][0] + fabsf(R[3 * k + 1]) * m.geom_half[g][1] +
-                                            fabsf(R[3 * k + 2]) * m.geom_half[g][2];
-    }
-  }
+  for (int f = BREC + g0; f < NB * BREC; f += gstep) soa(gpose, f, n, e) = fr[f];
 }
 
-// midphase of candidate pair p from the geoms' records: bounding spheres and world-aligned boxes
-// (before the poses are loaded), and for a plane the other geom's bounding sphere above it.
-// false: no contact is possible.  P1 / P2 are loaded here when the pair survives.
+// geom g's world pose from its body's frame (the world body: the geom's own placement)
+HDI void load_pose(const DModel& m, const float* __restrict__ gpose, int n, int e, int g, GeomPose& o) {
+  const int b = m.geom_bodyid[g];
+  float bp[3] = {0.f, 0.f, 0.f}, bR[9] = {1.f, 0.f, 0.f, 0.f, 1.f, 0.f, 0.f, 0.f, 1.f};
+  if (b > 0) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) bp[k] = soa(gpose, b * BREC + k, n, e);
+#pragma unroll
+    for (int k = 0; k < 9; k++) bR[k] = soa(gpose, b * BREC + 3 + k, n, e);
+  }
+  const float gp[3] = {m.geom_pos[g][0], m.geom_pos[g][1], m.geom_pos[g][2]};
+  float w[3];
+  mv(w, bR, gp);
+  mm(o.R, bR, m.geom_mat[g]);
+#pragma unroll
+  for (int c = 0; c < 3; c++) o.p[c] = bp[c] + w[c];
+}
+// the midphase bound of geom g at pose P: the world centre of its collision box and that box's
+// world-axis half-extents |R| h
+HDI void geom_bound(const DModel& m, int g, const GeomPose& P, float c[3], float h[3]) {
+  geom_center(m, g, P, c);
+#pragma unroll
+  for (int k = 0; k < 3; k++)
+    h[k] = fabsf(P.R[3 * k]) * m.geom_half[g][0] + fabsf(P.R[3 * k + 1]) * m.geom_half[g][1] +
+           fabsf(P.R[3 * k + 2]) * m.geom_half[g][2];
+}
+
+// midphase of candidate pair p from the env's body frames: bounding spheres and world-aligned boxes,
+// and for a plane the other geom's bounding sphere above it.  false: no contact is possible.  P1 /
+// P2 are the geoms' poses either way.
 HDI bool midphase(const DModel& m, int p, const float* __restrict__ gpose, int n, int e, GeomPose& P1,
                    GeomPose& P2) {
   const int g1 = m.pair_geom1[p], g2 = m.pair_geom2[p];
+  load_pose(m, gpose, n, e, g1, P1);
+  load_pose(m, gpose, n, e, g2, P2);
   float c2[3], h2[3];
-  if (m.geom_rbound[g2] > 0.f) load_bound(gpose, n, e, g2, c2, h2);
+  if (m.geom_rbound[g2] > 0.f) geom_bound(m, g2, P2, c2, h2);
   if (m.geom_rbound[g1] > 0.f && m.geom_rbound[g2] > 0.f) {
     float c1[3], h1[3], r[3];
-    load_bound(gpose, n, e, g1, c1, h1);
+    geom_bound(m, g1, P1, c1, h1);
     sub(r, c1, c2);
     const float mg = m.pair_margin[p];
     const float rr = m.geom_rbound[g1] + m.geom_rbound[g2] + mg;
@@ -1232,13 +1197,11 @@ HDI bool midphase(const DModel& m, int p, const float* __restrict__ gpose, int n
     for (int k = 0; k < 3; k++) sep |= fabsf(r[k]) > h1[k] + h2[k] + mg;
     if (sep) return false;
   }
-  load_pose(gpose, n, e, g1, P1);
   if (m.geom_type[g1] == SIM_GEOM_PLANE && m.geom_rbound[g2] > 0.f) {
     // bounding sphere of geom2 entirely above the plane (beyond the margin): no contact
     const float h = (c2[0] - P1.p[0]) * P1.R[2] + (c2[1] - P1.p[1]) * P1.R[5] + (c2[2] - P1.p[2]) * P1.R[8];
     if (h > m.geom_rbound[g2] + m.pair_margin[p]) return false;
   }
-  load_pose(gpose, n, e, g2, P2);
   return true;
 }
 

@@ -81,9 +81,9 @@ struct CpuContact {
 template <int NA, int NF>
 int collide_env(const CpuBatch& B, Sim<NA, NF>& S, int e, CpuContact* con, int& status) {
   const DModel& m = B.dm;
-  float gpose[SIM_MAXGEOM * GREC];
+  float gpose[SIM_MAXBODY * BREC];
   float cbuf[PAIR_MAXCON * 7];
-  write_geom_poses(S, gpose, 1, 0, 0, 1);
+  write_body_frames(S, gpose, 1, 0, 0, 1);
   float* sep = const_cast<float*>(B.sepax.data());
   int nc = 0;
   for (int p = 0; p < m.npair; p++) {

@@ -116,7 +116,7 @@ struct sim_batch {
   DModel* d_model = nullptr;   // shared per (model, device): DevModel
   float* d_scratch = nullptr;  // contact rows, [slot][env]
   size_t scratch_floats = 0;
-  float* d_gpose = nullptr;    // geom world records [geom*GREC+k][env] (pose + midphase bound)
+  float* d_gpose = nullptr;    // body world frames [body*BREC+k][env] (soarm_collide.h load_pose)
   float* d_cbuf = nullptr;     // collide output [slot*7+f][env]
   int* d_ccount = nullptr;     // contacts per pair [pair][env]
   uint32_t* d_pmask = nullptr; // pairs with contacts, bit p%32 of word p/32: [word][env]
@@ -470,14 +470,6 @@ static int validate_and_build(const sim_model_desc& d, sim_model* M) {
     float KB[2];
     host_KB(d.dof_solref[i], d.dof_solimp[i], d.timestep, KB);
     m.dof_fricB[i] = KB[1];
-  }
-  {  // geoms grouped by body (write_geom_poses walks bodies with compile-time indices)
-    int k = 0;
-    for (int b = 0; b < SIM_MAXBODY; b++) {
-      m.body_gadr[b] = k, m.body_gnum[b] = 0;
-      for (int g = 0; g < d.ngeom; g++)
-        if (d.geom_bodyid[g] == b) m.geom_bybody[k++] = g, m.body_gnum[b]++;
-    }
   }
   for (int g = 0; g < d.ngeom; g++) {
     m.geom_type[g] = d.geom_type[g], m.geom_bodyid[g] = d.geom_bodyid[g];
@@ -873,7 +865,7 @@ int sim_batch_create(const sim_model* m, int n_envs, int device, sim_batch** out
     B->scratch_floats = ((size_t)4 * SIM_MAXCON * (2 * nv + 4) + 2) * n_envs;
     HIPCHECK(hipMalloc(&B->d_scratch, B->scratch_floats * sizeof(float)));
     HIPCHECK(hipMemset(B->d_scratch, 0, B->scratch_floats * sizeof(float)));
-    HIPCHECK(hipMalloc(&B->d_gpose, (size_t)m->desc.ngeom * GREC * n_envs * sizeof(float)));
+    HIPCHECK(hipMalloc(&B->d_gpose, (size_t)m->desc.nbody * BREC * n_envs * sizeof(float)));
     HIPCHECK(hipMalloc(&B->d_cbuf, (size_t)(m->dm.nslot > 0 ? m->dm.nslot : 1) * 7 * n_envs * sizeof(float)));
     HIPCHECK(hipMalloc(&B->d_ccount, (size_t)(m->desc.npair > 0 ? m->desc.npair : 1) * n_envs * sizeof(int)));
     const size_t nw = (size_t)std::max(pmask_words(m->dm), 1);

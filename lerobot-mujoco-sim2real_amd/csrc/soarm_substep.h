@@ -86,8 +86,8 @@ __global__ __launch_bounds__(64) void k_step(const DModel* __restrict__ dm, int 
   if (obs) write_obs(S, obs, e);
 }
 
-// geom world poses from the current qpos (collision input); GEOM_LPE lanes per env split
-// the geoms (the FK chain runs on each of them)
+// body world frames from the current qpos (collision input); GEOM_LPE lanes per env split the
+// stores (the FK chain runs on each of them)
 constexpr int GEOM_LPE = 4;
 // XCD-aware block index: workgroups are dealt round-robin over the 8 XCDs, so renumber them to give
 // each XCD a contiguous range of envs.  A 16-env workgroup touches half of each 128-B line of the
@@ -105,7 +105,7 @@ __global__ __launch_bounds__(64) void k_geom(const DModel* __restrict__ dm, int 
   Sim<NA, NF> S(dm, 1.f, -1.f, 1.f);
   load_state(S, st, n, e);
   S.kinematics();
-  write_geom_poses(S, gpose, n, e, (int)threadIdx.x % GEOM_LPE, GEOM_LPE);
+  write_body_frames(S, gpose, n, e, (int)threadIdx.x % GEOM_LPE, GEOM_LPE);
 }
 inline dim3 geom_grid(int n) { return dim3((n + 64 / GEOM_LPE - 1) / (64 / GEOM_LPE)); }
 
@@ -232,10 +232,10 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
   if (gpose) {
     S.kinematics();
     PSTAMP(14);
-    if constexpr (RS)  // (the W rows' LDS is free after the solve: the body frames go there)
-      write_geom_poses_lds(S, gpose, n, e, (int)threadIdx.x % LPE, LPE, s_rsw + L.col * RS_WENV);
+    if constexpr (RS)  // (the W rows' LDS is free after the solve: the body frames are staged there)
+      write_body_frames_lds(S, gpose, n, e, (int)threadIdx.x % LPE, LPE, s_rsw + L.col * RS_WENV);
     else
-      write_geom_poses(S, gpose, n, e, (int)threadIdx.x % LPE, LPE);
+      write_body_frames(S, gpose, n, e, (int)threadIdx.x % LPE, LPE);
   } else {
     PSTAMP(14);  // (the last substep writes no poses: both phases empty)
   }
