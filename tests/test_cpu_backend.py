@@ -245,9 +245,13 @@ def test_cpu_contacts_match_oracle(cpu_lib, ccd):
                     deep_bad += abs(out[e, k, 0] - rc[k, 0]) > 3e-2 * abs(rc[k, 0])
             checked += 1
         assert checked > 0.9 * n and total > n // 4 and skipped <= 0.03 * n, (checked, total, skipped)
-        assert deep_bad <= max(2, 0.05 * deep) and nrm_bad <= max(2, 0.06 * shallow)
-        assert geo_bad <= max(2, 0.06 * shallow), (geo_bad, shallow)
-        assert slide <= 0.15 * shallow, (slide, shallow)
+        # (as the device test: native GJK/EPA's depth / normal / deep depth must agree -- r05 here:
+        # 0 / <= 1 / 0 off; its point may slide within the patch: 7.2% and 5.3% of 207 / 227 here,
+        # 2.6% and 4.0% on the device's 512 envs)
+        frac = 0.0 if ccd == "native" else 1.0
+        assert deep_bad <= max(2, 0.05 * frac * deep) and nrm_bad <= max(2, 0.06 * frac * shallow)
+        assert geo_bad <= max(2, 0.06 * frac * shallow), (geo_bad, shallow)
+        assert slide <= 0.10 * shallow, (slide, shallow)
 
 
 def test_cpu_one_substep_with_contacts(cpu_lib, cube_model):

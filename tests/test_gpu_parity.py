@@ -236,16 +236,17 @@ def test_contacts_match_oracle(gpu_lib, arm_model, cube_model, ccd):
         # the envs left out of the pair-by-pair comparison: a grazing contact (|depth| < 20 um) on
         # the oracle side, or a count mismatch whose extra contact is grazing on the GPU side
         assert skipped_grazing + skipped_count <= 0.03 * n, (skipped_grazing, skipped_count)
-        # deep (>5 mm) penetrations: MPR's depth there depends on the portal path, which
-        # flips on near-tied support vertices; require agreement for the bulk only
-        assert deep_bad <= max(2, 0.05 * deep), (deep_bad, deep)
-        # normals of edge/vertex contacts come from MPR's final portal face, which fp32 can
-        # pick differently from fp64 when two faces nearly tie
-        assert nrm_bad <= max(2, 0.06 * shallow), ("normals", nrm_bad, shallow)
-        # depth / point: MPR is not a minimum-depth method; its portal refinement can end on
-        # a different face in fp32 than in fp64 for a few edge contacts
-        assert geo_bad <= max(2, 0.06 * shallow), ("depth/point", geo_bad, shallow)
-        assert slide <= 0.15 * shallow, ("EPA point slides", slide, shallow)
+        # MPR: deep (>5 mm) penetrations' depth depends on the portal path, which flips on near-tied
+        # support vertices, and its normals / points come from the final portal face, which fp32 can
+        # pick differently from fp64 when two faces nearly tie -- bars for the bulk only.  Native
+        # GJK/EPA is a minimum-depth method: depth, normal and deep depth must all agree (r05, 512
+        # envs per scene: 0 off in every class), its witness point may slide within a face contact's
+        # patch on <= 5% of the shallow contacts (r05: 2.6% and 4.0%; VERDICT r4 asked <= 5%)
+        frac = 0.0 if ccd == "native" else 1.0
+        assert deep_bad <= max(2, 0.05 * frac * deep), (deep_bad, deep)
+        assert nrm_bad <= max(2, 0.06 * frac * shallow), ("normals", nrm_bad, shallow)
+        assert geo_bad <= max(2, 0.06 * frac * shallow), ("depth/point", geo_bad, shallow)
+        assert slide <= 0.05 * shallow, ("EPA point slides", slide, shallow)
         print(f"contacts: {total} checked, shallow {shallow} (geometry off {geo_bad}, normal off {nrm_bad}), "
               f"deep {deep} (off {deep_bad}); envs skipped: grazing {skipped_grazing}, count {skipped_count}")
 
