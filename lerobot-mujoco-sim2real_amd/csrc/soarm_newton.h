@@ -118,10 +118,13 @@ struct NewtonRows {
   static constexpr int SIG_BITS = 4 * ((LDS_CON + QL - 1) / QL) + (4 * (SIM_MAXCON - LDS_CON) + QL - 1) / QL +
                                   2 * NA + 2 * NA;
   static_assert(!CON || SIG_BITS <= 64, "zone signature must fit its 64-bit word");
-  template <int LO, int HI, bool WANT_H>
-  DEVI float pass(const float a[NV], float jtf[NV], float H[], uint64_t& sig) const {
+  // C0: also the rows' cost at a0 (cost0; no derivatives there) in the same pass -- the warm
+  // start's two points (qacc_smooth and the warm start) share one read of the rows
+  template <int LO, int HI, bool WANT_H, bool C0 = false>
+  DEVI float pass(const float a[NV], float jtf[NV], float H[], uint64_t& sig, const float* a0 = nullptr,
+                  float* cost0 = nullptr) const {
     constexpr int NR = HI - LO, NH = NR * (NR + 1) / 2;
-    float cost = 0.f;
+    float cost = 0.f, c0 = 0.f;
     sig = 0ull;
 #pragma unroll
     for (int i = LO; i < HI; i++) jtf[i] = 0.f;
@@ -136,17 +139,24 @@ struct NewtonRows {
 #pragma unroll
           for (int i = CL; i < CH; i++) jc[q][i] = L.at(c, 12 * q + i);
         const float mu = L.at(c, F_MU), D = L.at(c, F_IARD);
-        float y[3] = {0.f, 0.f, 0.f};
+        float y[3] = {0.f, 0.f, 0.f}, y0[3] = {0.f, 0.f, 0.f};
 #pragma unroll
         for (int q = 0; q < 3; q++)
 #pragma unroll
-          for (int i = CL; i < CH; i++) y[q] = fmaf(jc[q][i], a[i], y[q]);
+          for (int i = CL; i < CH; i++) {
+            y[q] = fmaf(jc[q][i], a[i], y[q]);
+            if constexpr (C0) y0[q] = fmaf(jc[q][i], a0[i], y0[q]);
+          }
         float F[3] = {0.f, 0.f, 0.f}, K[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // K: nn n1 n2 11 12 22
 #pragma unroll
         for (int ed = 0; ed < 4; ed++) {
           const float s = (ed & 1) ? -mu : mu;
           const int t = 1 + (ed >> 1);
           const float x = y[0] + s * y[t] - L.at(c, F_AREF + ed);
+          if constexpr (C0) {
+            const float x0 = y0[0] + s * y0[t] - L.at(c, F_AREF + ed);
+            c0 += x0 < 0.f ? 0.5f * x0 * x0 * D : 0.f;
+          }
           const bool act = x < 0.f;
           sig = sig * 2ull + (act ? 1ull : 0ull);
           const float xa = act ? x : 0.f, Da = act ? D : 0.f;  // (branch-free)
@@ -193,9 +203,13 @@ struct NewtonRows {
         // contacts past the LDS records: per-edge rows in the global slab (rare; whole problem)
         for (int r = 4 * nl + ql(); r < 4 * ncon; r += QL) {
           mine = true;
-          float J[NV], x = -cr.S(r, 0);
+          float J[NV], x = -cr.S(r, 0), x0 = -cr.S(r, 0);
 #pragma unroll
-          for (int i = 0; i < NV; i++) J[i] = cr.J(r, i), x = fmaf(J[i], a[i], x);
+          for (int i = 0; i < NV; i++) {
+            J[i] = cr.J(r, i), x = fmaf(J[i], a[i], x);
+            if constexpr (C0) x0 = fmaf(J[i], a0[i], x0);
+          }
+          if constexpr (C0) c0 += x0 < 0.f ? 0.5f * x0 * x0 * cr.S(r, 2) : 0.f;
           sig = sig * 2ull + (x < 0.f ? 1ull : 0ull);
           if (x < 0.f) {
             const float D = cr.S(r, 2), f = -x * D;
@@ -215,6 +229,7 @@ struct NewtonRows {
       if constexpr (QL > 1) {
         if (__any(mine)) {
           cost = qred(cost);
+          if constexpr (C0) c0 = qred(c0);
 #pragma unroll
           for (int i = LO; i < HI; i++) jtf[i] = qred(jtf[i]);
           if constexpr (WANT_H)
@@ -235,6 +250,10 @@ struct NewtonRows {
         const float flx = x < 0.f ? fl : -fl;
         jtf[i] += lin ? flx : -x * iR;
         cost += lin ? fmaf(fl, fabsf(x), -0.5f * Rfl * fl) : 0.5f * x * x * iR;
+        if constexpr (C0) {
+          const float x0 = a0[i] - fa[i];
+          c0 += fabsf(x0) >= Rfl ? fmaf(fl, fabsf(x0), -0.5f * Rfl * fl) : 0.5f * x0 * x0 * iR;
+        }
         sig = sig * 3ull + (q ? 1ull : (x < 0.f ? 2ull : 0ull));
         if constexpr (WANT_H) H[hidx(i, i)] += q ? iR : 0.f;
       }
@@ -242,10 +261,17 @@ struct NewtonRows {
       for (int l = 0; l < nlim; l++) {
         const int d = (int)L.lm(l, L_DOF);
         const float sg = L.lm(l, L_SGN), iR = L.lm(l, L_IARD);
-        float ad = 0.f;
+        float ad = 0.f, ad0 = 0.f;
 #pragma unroll
-        for (int i = 0; i < NA; i++) ad = i == d ? a[i] : ad;
+        for (int i = 0; i < NA; i++) {
+          ad = i == d ? a[i] : ad;
+          if constexpr (C0) ad0 = i == d ? a0[i] : ad0;
+        }
         const float x = sg * ad - L.lm(l, L_AREF);
+        if constexpr (C0) {
+          const float x0 = sg * ad0 - L.lm(l, L_AREF);
+          c0 += x0 < 0.f ? 0.5f * x0 * x0 * iR : 0.f;
+        }
         sig = sig * 2ull + (x < 0.f ? 1ull : 0ull);
         if (x < 0.f) {
           cost += 0.5f * x * x * iR;
@@ -258,6 +284,7 @@ struct NewtonRows {
         }
       }
     }
+    if constexpr (C0) *cost0 = c0;
     return cost;
   }
 
@@ -432,13 +459,14 @@ DEVI int newton_range(const Sim<NA, NF>& S, const NewtonRows<NA, NF, CON>& R, fl
   // Hessian pass runs at the warm point, and again at qacc_smooth only in lanes where it wins
   float cost;
   {
-    float js[NV];
-    const float cs = R.template pass<LO, HI, false>(a0, js, H, sig);
+    // (one pass over the rows for both points: the cost at qacc_smooth (its Gauss term is 0) and
+    // cost, gradient and Hessian at the warm start)
 #pragma unroll
     for (int i = 0; i < NV; i++) a[i] = (i >= LO && i < HI) ? S.warm[i] : a[i];
 #pragma unroll
     for (int i = 0; i < NH; i++) H[i] = 0.f;
-    cost = gauss(a, Ma) + R.template pass<LO, HI, true>(a, jtf, H, sig);
+    float cs;
+    cost = gauss(a, Ma) + R.template pass<LO, HI, true, true>(a, jtf, H, sig, a0, &cs);
     if (cs < cost) {
 #pragma unroll
       for (int i = LO; i < HI; i++) a[i] = a0[i], Ma[i] = 0.f;
