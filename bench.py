@@ -499,11 +499,17 @@ def main():
         tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(tpath):
             tr = json.load(open(tpath))
-            traffic = tr.get(name if args.solver == "pgs" else f"{name}_newton", {}).get(kind)
-        # 64-lane waves, one lane per env (four per env in k_substep: quad mode, soarm_pgs.h
-        # lpe()): the kernel can occupy at most that many of the chip's 1024 SIMDs; the VALU
-        # peak those SIMDs can issue bounds it first
-        lanes = 4 if kind == "substep" else 1
+            key = name if args.solver == "pgs" else f"{name}_newton"
+            key = f"{name}_native" if args.ccd == "native" and args.solver == "pgs" else key
+            traffic = tr.get(key, {}).get(kind)
+        # 64-lane waves, one lane per env (k_substep: four per env in quad mode, soarm_pgs.h lpe();
+        # sixteen in the row-space PGS kernel, which the library runs for PGS on the free-body scene
+        # up to 4 envs per SIMD, soarm_sim.hip rs_cap): the kernel can occupy at most that many of
+        # the chip's 1024 SIMDs; the VALU peak those SIMDs can issue bounds it first
+        rs = (kind == "substep" and args.solver == "pgs" and sim.nv == 12 and  # (arm + one free body)
+              os.environ.get("SOARM_RS", "1") != "0" and
+              n <= 16 * torch.cuda.get_device_properties(dev).multi_processor_count)
+        lanes = (16 if rs else 4) if kind == "substep" else 1
         waves = -(-n * lanes // 64)
         capped = PEAK_FP32_TFLOPS * min(1.0, waves / 1024)
         roof = {"bound": "valu", "achieved": achieved, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
