@@ -43,6 +43,7 @@ struct DModel {
   int geom_type[MAXG], geom_bodyid[MAXG], geom_hulladr[MAXG], geom_hullnum[MAXG];
   float geom_pos[MAXG][3], geom_mat[MAXG][9], geom_size[MAXG][3];
   float geom_center[MAXG][3], geom_half[MAXG][3], geom_rbound[MAXG];
+  float geom_cbody[MAXG][3];  // the collision-box centre in the body frame: pos + mat centre (midphase)
   float geom_friction[MAXG];
 
   // candidate pairs (mixed per-pair contact parameters)

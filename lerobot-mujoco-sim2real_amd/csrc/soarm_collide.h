@@ -1148,6 +1148,20 @@ __device__ __forceinline__ void write_body_frames_lds(const Sim<NA, NF>& S, floa
   for (int f = BREC + g0; f < NB * BREC; f += gstep) soa(gpose, f, n, e) = fr[f];
 }
 
+// a body-frame point x in world coordinates from the env's frame of body b (b = 0: the world)
+HDI void body_point(const DModel& m, const float* __restrict__ gpose, int n, int e, int b, const float x[3],
+                    float w[3]) {
+  if (b == 0) {
+    w[0] = x[0], w[1] = x[1], w[2] = x[2];
+    return;
+  }
+  float bR[9];
+#pragma unroll
+  for (int k = 0; k < 9; k++) bR[k] = soa(gpose, b * BREC + 3 + k, n, e);
+  mv(w, bR, x);
+#pragma unroll
+  for (int k = 0; k < 3; k++) w[k] += soa(gpose, b * BREC + k, n, e);
+}
 // geom g's world pose from its body's frame (the world body: the geom's own placement)
 HDI void load_pose(const DModel& m, const float* __restrict__ gpose, int n, int e, int g, GeomPose& o) {
   const int b = m.geom_bodyid[g];
@@ -1175,32 +1189,42 @@ HDI void geom_bound(const DModel& m, int g, const GeomPose& P, float c[3], float
            fabsf(P.R[3 * k + 2]) * m.geom_half[g][2];
 }
 
-// midphase of candidate pair p from the env's body frames: bounding spheres and world-aligned boxes,
-// and for a plane the other geom's bounding sphere above it.  false: no contact is possible.  P1 /
-// P2 are the geoms' poses either way.
+// midphase of candidate pair p from the env's body frames: bounding spheres and, for a plane, the
+// other geom's bounding sphere above it (from the body frames alone), then world-aligned boxes of
+// the composed poses.  false: no contact is possible; P1 / P2 are set when it returns true.
 HDI bool midphase(const DModel& m, int p, const float* __restrict__ gpose, int n, int e, GeomPose& P1,
                    GeomPose& P2) {
   const int g1 = m.pair_geom1[p], g2 = m.pair_geom2[p];
+  if (m.geom_rbound[g1] > 0.f && m.geom_rbound[g2] > 0.f) {
+    // bounding spheres first, from the body frames and the centres' body-frame offsets (no geom
+    // pose composed for the ~80 of 86 pairs this rejects)
+    float c1[3], c2[3], r[3];
+    body_point(m, gpose, n, e, m.geom_bodyid[g1], m.geom_cbody[g1], c1);
+    body_point(m, gpose, n, e, m.geom_bodyid[g2], m.geom_cbody[g2], c2);
+    sub(r, c1, c2);
+    const float rr = m.geom_rbound[g1] + m.geom_rbound[g2] + m.pair_margin[p];
+    if (dot3(r, r) > rr * rr) return false;
+  }
+  if (m.geom_type[g1] == SIM_GEOM_PLANE && m.geom_rbound[g2] > 0.f) {
+    // bounding sphere of geom2 entirely above the plane (beyond the margin): no contact
+    float c2[3];
+    body_point(m, gpose, n, e, m.geom_bodyid[g2], m.geom_cbody[g2], c2);
+    load_pose(m, gpose, n, e, g1, P1);
+    const float h = (c2[0] - P1.p[0]) * P1.R[2] + (c2[1] - P1.p[1]) * P1.R[5] + (c2[2] - P1.p[2]) * P1.R[8];
+    if (h > m.geom_rbound[g2] + m.pair_margin[p]) return false;
+  }
   load_pose(m, gpose, n, e, g1, P1);
   load_pose(m, gpose, n, e, g2, P2);
-  float c2[3], h2[3];
-  if (m.geom_rbound[g2] > 0.f) geom_bound(m, g2, P2, c2, h2);
-  if (m.geom_rbound[g1] > 0.f && m.geom_rbound[g2] > 0.f) {
-    float c1[3], h1[3], r[3];
+  if (m.geom_rbound[g1] > 0.f && m.geom_rbound[g2] > 0.f) {  // world-aligned boxes
+    float c1[3], h1[3], c2[3], h2[3], r[3];
     geom_bound(m, g1, P1, c1, h1);
+    geom_bound(m, g2, P2, c2, h2);
     sub(r, c1, c2);
     const float mg = m.pair_margin[p];
-    const float rr = m.geom_rbound[g1] + m.geom_rbound[g2] + mg;
-    if (dot3(r, r) > rr * rr) return false;
     bool sep = false;
 #pragma unroll
     for (int k = 0; k < 3; k++) sep |= fabsf(r[k]) > h1[k] + h2[k] + mg;
     if (sep) return false;
-  }
-  if (m.geom_type[g1] == SIM_GEOM_PLANE && m.geom_rbound[g2] > 0.f) {
-    // bounding sphere of geom2 entirely above the plane (beyond the margin): no contact
-    const float h = (c2[0] - P1.p[0]) * P1.R[2] + (c2[1] - P1.p[1]) * P1.R[5] + (c2[2] - P1.p[2]) * P1.R[8];
-    if (h > m.geom_rbound[g2] + m.pair_margin[p]) return false;
   }
   return true;
 }

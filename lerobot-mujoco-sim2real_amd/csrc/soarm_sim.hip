@@ -481,6 +481,11 @@ static int validate_and_build(const sim_model_desc& d, sim_model* M) {
       m.geom_half[g][k] = (float)d.geom_aabb[g][3 + k];
     }
     quat2mat_h(m.geom_mat[g], d.geom_quat[g]);
+    for (int k = 0; k < 3; k++) {
+      double c = d.geom_pos[g][k];
+      for (int j = 0; j < 3; j++) c += (double)m.geom_mat[g][3 * k + j] * d.geom_aabb[g][j];
+      m.geom_cbody[g][k] = (float)c;
+    }
     m.geom_rbound[g] = (float)d.geom_rbound[g];
     m.geom_friction[g] = (float)d.geom_friction[g][0];
   }
