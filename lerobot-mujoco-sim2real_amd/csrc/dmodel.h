@@ -57,6 +57,9 @@ struct DModel {
   // which holds (contacts - 1) in bits 2q, 2q+1 (-1: single-contact pair, a set mask bit is
   // its one contact); the count word follows the presence words in pmask
   int pair_cq[MAXP];
+  // k_collide's dispatch order (blockIdx.y -> pair): the pairs whose narrowphase is a convex-convex
+  // solver or box-box clipping first (the launch's longest waves), plane pairs last
+  int pair_order[MAXP];
   int ncq;
   int nslot;            // total contact slots (sum of per-pair capacities)
   int free_diag;        // every free body has ipos = 0 and iquat = 1: its 6x6 M block is diagonal

@@ -157,6 +157,7 @@ struct sim_batch {
 #endif
 // CCD: one instantiation per narrowphase, so the MPR kernel carries none of EPA's private-memory
 // polytope (2.2 KB of scratch per lane)
+__device__ __forceinline__ int m_pair_order(const DModel* dm, int y) { return dm->pair_order[y]; }
 template <int CCD>
 __global__ __launch_bounds__(256, SOARM_COLLIDE_WAVES) void k_collide(const DModel* __restrict__ dm, int n,
                                                  const float* __restrict__ gpose,
@@ -167,7 +168,7 @@ __global__ __launch_bounds__(256, SOARM_COLLIDE_WAVES) void k_collide(const DMod
   // (env chunks numbered per XCD as in k_geom / k_substep: the geom records this reads and the
   // contact buffer it writes stay in the L2 of the XCD whose substep waves own those envs)
   const int e = xcd_block() * blockDim.x + threadIdx.x;
-  const int p = gridDim.y - 1 - blockIdx.y;  // later pairs (self / cube-arm: MPR-heavy) dispatch first
+  const int p = m_pair_order(dm, blockIdx.y);  // (DModel::pair_order: the heavy pairs dispatch first)
   if (e >= n) return;
   const long long t0 = pcyc ? clock64() : 0;
   const DModel& m = *dm;
@@ -512,6 +513,21 @@ static int validate_and_build(const sim_model_desc& d, sim_model* M) {
     m.nslot += cap;
   }
   if (m.ncq > 16) return fail(SIM_E_MODEL, "more than 16 box-box / plane-box pairs");
+  {  // collide dispatch order: by class (convex-convex and box-box with the free body or the world's
+     // boxes, then the arm's own mesh pairs, then plane pairs), later pairs first within a class
+     // (round 4's order): a class-0 pair dispatched among the last workgroups started after the
+     // grid had filled and set the launch's tail
+    auto cls = [&](int p) {
+      const int t1 = d.geom_type[d.pair_geom1[p]], t2 = d.geom_type[d.pair_geom2[p]];
+      if (t1 == SIM_GEOM_PLANE || t2 == SIM_GEOM_PLANE) return 2;
+      const int b1 = d.geom_bodyid[d.pair_geom1[p]], b2 = d.geom_bodyid[d.pair_geom2[p]];
+      return (b1 == 0 || b2 == 0 || b1 >= 2 + na || b2 >= 2 + na) ? 0 : 1;
+    };
+    int k = 0;
+    for (int c = 0; c < 3; c++)
+      for (int p = d.npair - 1; p >= 0; p--)
+        if (cls(p) == c) m.pair_order[k++] = p;
+  }
   // free bodies: the kernels use a diagonal 6x6 mass block, which needs the inertia frame at
   // the body frame (ipos = 0, iquat = identity) — true for the build-defined cube
   m.free_diag = 1;
