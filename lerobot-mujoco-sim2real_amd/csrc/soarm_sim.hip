@@ -158,6 +158,9 @@ struct sim_batch {
 // CCD: one instantiation per narrowphase, so the MPR kernel carries none of EPA's private-memory
 // polytope (2.2 KB of scratch per lane)
 __device__ __forceinline__ int m_pair_order(const DModel* dm, int y) { return dm->pair_order[y]; }
+#ifdef SOARM_DIAG_SKIPP
+__device__ uint32_t g_diag_skip[4];
+#endif
 template <int CCD>
 __global__ __launch_bounds__(256, SOARM_COLLIDE_WAVES) void k_collide(const DModel* __restrict__ dm, int n,
                                                  const float* __restrict__ gpose,
@@ -170,6 +173,9 @@ __global__ __launch_bounds__(256, SOARM_COLLIDE_WAVES) void k_collide(const DMod
   const int e = xcd_block() * blockDim.x + threadIdx.x;
   const int p = m_pair_order(dm, blockIdx.y);  // (DModel::pair_order: the heavy pairs dispatch first)
   if (e >= n) return;
+#ifdef SOARM_DIAG_SKIPP
+  if ((g_diag_skip[p >> 5] >> (p & 31)) & 1u) return;  // (diagnostic: the pairs SOARM_DIAG_SKIP names cost nothing)
+#endif
   const long long t0 = pcyc ? clock64() : 0;
   const DModel& m = *dm;
   PairOut o{cbuf, n, e, m.pair_slot[p], m.pair_cap[p], 0};
@@ -875,6 +881,23 @@ int sim_batch_create(const sim_model* m, int n_envs, int device, sim_batch** out
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess)
       B->rs_cap = cus * 4 * RS_EPW;
+#ifdef SOARM_DIAG_SKIPP
+  {  // SOARM_DIAG_SKIP: "p,p,..." pairs to skip; a leading '~' skips every pair but those
+    static uint32_t w[4] = {0u, 0u, 0u, 0u};
+    if (const char* v = getenv("SOARM_DIAG_SKIP")) {
+      const bool inv = *v == '~';
+      for (const char* c = v + inv; *c;) {
+        const int p = atoi(c);
+        if (p >= 0 && p < 128) w[p >> 5] |= 1u << (p & 31);
+        while (*c && *c != ',') c++;
+        if (*c) c++;
+      }
+      if (inv)
+        for (auto& x : w) x = ~x;
+    }
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_diag_skip), w, sizeof(w), 0, hipMemcpyHostToDevice);
+  }
+#endif
   }
   if (int rc = upload_model(m, device, &B->d_model)) {
     delete B;
