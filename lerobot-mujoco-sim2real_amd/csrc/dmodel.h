@@ -57,6 +57,12 @@ struct DModel {
   // which holds (contacts - 1) in bits 2q, 2q+1 (-1: single-contact pair, a set mask bit is
   // its one contact); the count word follows the presence words in pmask
   int pair_cq[MAXP];
+  // the same per 32-pair word of the contact mask, for the contact list walk (wave-uniform words:
+  // scalar loads, where pair_cq[p] / pair_body[p] of a lane's own pair p are per-lane gathers):
+  // multi-contact pairs (cq = pair_cqbase[w] + the multi-contact pairs below p in word w, since cq
+  // is assigned in pair order), pairs touching an arm body, pairs touching a free body
+  uint32_t pair_mw_multi[(MAXP + 31) / 32], pair_mw_arm[(MAXP + 31) / 32], pair_mw_free[(MAXP + 31) / 32];
+  int pair_cqbase[(MAXP + 31) / 32];
   // k_collide's dispatch order (blockIdx.y -> pair): the pairs whose narrowphase is a convex-convex
   // solver or box-box clipping first (the launch's longest waves), plane pairs last
   int pair_order[MAXP];

@@ -313,6 +313,13 @@ struct PairMask {
     const int cq = m.pair_cq[p];
     return cq < 0 ? 1 : (int)((cw >> (2 * cq)) & 3u) + 1;
   }
+  // the same for pair 32 w + b from the word's tables (w compile-time: no per-lane load)
+  DEVI int count_w(const DModel& m, int w, int b) const {
+    const uint32_t mu = m.pair_mw_multi[w], bit = 1u << b;
+    if (!(mu & bit)) return 1;
+    const int cq = m.pair_cqbase[w] + __popc(mu & (bit - 1u));
+    return (int)((cw >> (2 * cq)) & 3u) + 1;
+  }
 };
 
 // first row past the contact rows of the scratch slab (sim_batch d_scratch): Newton's zone history
@@ -687,13 +694,20 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       // and writes each into the quad's 4 columns; overflow contacts (rare) are built by
       // every lane (identical values in the env's slab)
       const int nw = (m.npair + 31) >> 5;
+      // (RS) the contact categories of the RS layout (RsLayout) in list order: AT* CT* AC*, from the
+      // pair words' body tables as the list is made (no per-contact pass over the list)
+      bool rs_ok = true;
+      int rs_stage = 0;
 #pragma unroll
       for (int w = 0; w < PairMask::MAXW; w++) {  // unrolled: pm->w[] stays in registers
         uint32_t bits = w >= nw ? 0u : pm.w[w];
+        const uint32_t warm = RS && w < nw ? m.pair_mw_arm[w] : 0u, wfree = RS && w < nw ? m.pair_mw_free[w] : 0u;
         while (bits) {
-          const int p = 32 * w + __builtin_ctz(bits);
+          const int b = __builtin_ctz(bits);
+          const int p = 32 * w + b;
           bits &= bits - 1;
-          const int cnt = pm.count(m, p);
+          const int cnt = pm.count_w(m, w, b);
+          const int cat = (wfree >> b) & 1u ? ((warm >> b) & 1u ? 2 : 1) : 0;
           for (int k = 0; k < cnt; k++) {
             if (ncon >= SIM_MAXCON) {
               S.status |= SIM_ST_CONOVERFLOW;
@@ -701,6 +715,11 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
             }
             L.ex(ncon) = __int_as_float(p << 3 | k);
             ncon++;
+            if constexpr (RS) {
+              rs_ok = rs_ok && cat >= rs_stage;
+              rs_stage = cat;
+              rs_nat += cat == 0, rs_nct += cat == 1, rs_nac += cat == 2;
+            }
           }
         }
       }
@@ -718,17 +737,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
                   m.pair_tran[p], m.pair_margin[p], m.pair_KB[p][0], m.pair_KB[p][1], si, split);
       };
       if constexpr (RS) {  // the contact categories of the RS layout (RsLayout): AT* CT* AC* in list order
-        bool ok = nlim == 0 && ncon <= LDS_CON;
-        int stage = 0;
-        for (int c = 0; c < ncon; c++) {
-          const int p = __float_as_int(L.ex(c)) >> 3;
-          const int b1 = m.pair_body1[p], b2 = m.pair_body2[p];
-          const bool ta = (b1 >= 2 && b1 < 2 + NA) || (b2 >= 2 && b2 < 2 + NA), tf = b1 >= 2 + NA || b2 >= 2 + NA;
-          const int cat = tf ? (ta ? 2 : 1) : 0;
-          ok = ok && cat >= stage;
-          stage = cat;
-          rs_nat += cat == 0, rs_nct += cat == 1, rs_nac += cat == 2;
-        }
+        bool ok = nlim == 0 && ncon <= LDS_CON && rs_ok;
         // the layouts instantiated: (KAT, KAC) = (0, 0) the cube resting alone, (1, 0) plus one
         // arm-only contact, (0, 1) plus one arm-cube contact, (1, 1) both, in one env or in two envs
         // of the wave (without it those waves -- ~1 launch in 10 over steps 20-120 -- took the v-form

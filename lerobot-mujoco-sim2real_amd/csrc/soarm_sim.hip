@@ -519,6 +519,17 @@ static int validate_and_build(const sim_model_desc& d, sim_model* M) {
     m.nslot += cap;
   }
   if (m.ncq > 16) return fail(SIM_E_MODEL, "more than 16 box-box / plane-box pairs");
+  for (int w = 0; w < (MAXP + 31) / 32; w++)
+    m.pair_mw_multi[w] = m.pair_mw_arm[w] = m.pair_mw_free[w] = 0u, m.pair_cqbase[w] = 0;
+  for (int p = 0, q = 0; p < d.npair; p++) {
+    const int w = p >> 5;
+    const uint32_t bit = 1u << (p & 31);
+    if ((p & 31) == 0) m.pair_cqbase[w] = q;
+    if (m.pair_cq[p] >= 0) m.pair_mw_multi[w] |= bit, q++;
+    const int b1 = m.pair_body1[p], b2 = m.pair_body2[p];
+    if ((b1 >= 2 && b1 < 2 + na) || (b2 >= 2 && b2 < 2 + na)) m.pair_mw_arm[w] |= bit;
+    if (b1 >= 2 + na || b2 >= 2 + na) m.pair_mw_free[w] |= bit;
+  }
   {  // collide dispatch order: by class (convex-convex and box-box with the free body or the world's
      // boxes, then the arm's own mesh pairs, then plane pairs), later pairs first within a class
      // (round 4's order): a class-0 pair dispatched among the last workgroups started after the

@@ -3,7 +3,7 @@
 # usage: A=path B=path bash tools/gpu_ab2.sh tag
 set -o pipefail
 t=$1
-for i in 1 2; do
+for i in 1 2 3; do
   for v in A B; do
     lib=${!v}
     echo "== $v $lib $(date +%T)"
