@@ -833,9 +833,11 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
 #endif
 
   // ---- warm start from qacc_warmstart (forces implied by the primal), keep if it beats f = 0
+  // (a wave on the RS solve makes its warm start in row space instead, rs_solve)
   float v[NV];
 #pragma unroll
   for (int i = 0; i < NV; i++) v[i] = S.qacc_s[i];
+  if (!(RS && rs_fast)) {
 #pragma unroll
   for (int i = 0; i < NA; i++) {
     const float fl = m.dof_frictionloss[i];
@@ -954,6 +956,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
     for (int r = 4 * nl; r < 4 * ncon; r++) cr.S(r, 3) = 0.f;
 #pragma unroll
     for (int i = 0; i < NV; i++) v[i] = S.qacc_s[i];
+  }
   }
 
 #ifdef SOARM_PHASE_PROF
@@ -2164,13 +2167,23 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
         if (kind == 0) {  // dof frictionloss row ed: J = e_ed
 #pragma unroll
           for (int i = 0; i < NA; i++)
-            if (ed == i) J[i] = 1.f, ar = fa[i], R = fR[i], f = ff[i];
+            if (ed == i) {
+              J[i] = 1.f, ar = fa[i], R = fR[i];
+              // warm-start force (the Gram-form warm start's frictionloss branch)
+              const float fl = m.dof_frictionloss[i], jar = S.warm[i] - fa[i];
+              const float fs = (jar <= -fl * R) ? fl : (jar >= fl * R) ? -fl : -jar / R;
+              f = fl > 0.f ? fs : 0.f;
+            }
         } else if (kind == 1) {  // pyramid edge J_n +- mu J_t of contact c
           const float mu = L.at(c, F_MU), s = (ed & 1) ? -mu : mu;
           const int t = 12 * (1 + (ed >> 1));
 #pragma unroll
           for (int i = 0; i < NV; i++) J[i] = fmaf(s, L.at(c, t + i), L.at(c, i));
-          ar = L.at(c, F_AREF + ed), R = L.at(c, F_R), f = L.at(c, F_FRC + ed);
+          ar = L.at(c, F_AREF + ed), R = L.at(c, F_R);
+          float jar = -ar;  // warm-start force: the edge's J qacc_warmstart - aref, if negative
+#pragma unroll
+          for (int i = 0; i < NV; i++) jar = fmaf(J[i], S.warm[i], jar);
+          f = jar < 0.f ? -jar / R : 0.f;
         }
       };
       float JA[NV], JB[NV], WA[NV], WB[NV], arA, arB, RA, RB, fA, fB;
@@ -2194,19 +2207,52 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       // the bound registers, broadcast over the env's row: -f_q (edges) and the frictionloss
       // rows' lo - f, hi - f
       float NF_[NS], NH_[NA];
-      sfor<NS>([&](auto qc) {
-        constexpr int q = decltype(qc)::value;
-        const float fq = -rowbcast<LY::lane(q)>(LY::slot(q) == 0 ? fA : fB);
-        if constexpr (q < NA) {
-          const float fl = m.dof_frictionloss[q];
-          NF_[q] = fq - fl, NH_[q] = fq + fl;
-        } else {
-          NF_[q] = fq;
-        }
-      });
-      float jvA = -arA, jvB = -arB;
+      auto bounds = [&]() {
+        sfor<NS>([&](auto qc) {
+          constexpr int q = decltype(qc)::value;
+          const float fq = -rowbcast<LY::lane(q)>(LY::slot(q) == 0 ? fA : fB);
+          if constexpr (q < NA) {
+            const float fl = m.dof_frictionloss[q];
+            NF_[q] = fq - fl, NH_[q] = fq + fl;
+          } else {
+            NF_[q] = fq;
+          }
+        });
+      };
+      // v = qacc_smooth + sum_q W_q f_q (lane i < NV sums dof i, the row broadcasts it); f_q from the
+      // bound registers (NH_ = fl - f on the frictionloss rows, NF_ = -f on the others)
+      auto vel = [&]() {
+        float acc = 0.f;
+        const int di = r16 < NV ? r16 : 0;
 #pragma unroll
-      for (int i = 0; i < NV; i++) jvA = fmaf(JA[i], v[i], jvA), jvB = fmaf(JB[i], v[i], jvB);
+        for (int q = 0; q < NS; q++)
+          acc = fmaf(Wl[q * RS_WROW + di], q < NA ? m.dof_frictionloss[q] - NH_[q] : -NF_[q], acc);
+        sfor<NV>([&](auto ic) {
+          constexpr int i = decltype(ic)::value;
+          v[i] = S.qacc_s[i] + rowbcast<i>(acc);
+        });
+      };
+      // the warm start in row space (the Gram-form block above is skipped on these waves): every
+      // row's warm force (row_of), v, and the dual cost against f = 0, summed over the env's rows
+      bounds();
+      vel();
+      float jvA = -arA, jvB = -arB, jqA = -arA, jqB = -arB;
+#pragma unroll
+      for (int i = 0; i < NV; i++) {
+        jvA = fmaf(JA[i], v[i], jvA), jvB = fmaf(JB[i], v[i], jvB);
+        jqA = fmaf(JA[i], S.qacc_s[i], jqA), jqB = fmaf(JB[i], S.qacc_s[i], jqB);
+      }
+      // dual cost: sum_r 0.5 f_r (J_r v - aref_r + R_r f_r) + 0.5 f_r (J_r qacc_smooth - aref_r)
+      const float wcost = rowsum16(0.5f * fA * (jvA + RA * fA) + 0.5f * fA * jqA +
+                                   (0.5f * fB * (jvB + RB * fB) + 0.5f * fB * jqB));
+      const bool rej = wcost > 0.f;  // worse than no warm start: f = 0, v = qacc_smooth
+      if (__any(rej)) {              // (wave-uniform: the broadcasts run on every row)
+        fA = rej ? 0.f : fA, fB = rej ? 0.f : fB;
+        bounds();
+#pragma unroll
+        for (int i = 0; i < NV; i++) v[i] = rej ? S.qacc_s[i] : v[i];
+        jvA = rej ? jqA : jvA, jvB = rej ? jqB : jvB;
+      }
       f2 sA = f2{-fmaf(RA, fA, jvA) * iA, 0.f}, sB = f2{-fmaf(RB, fB, jvB) * iB, 0.f};
       // the scaled matrix: C[r][q] = -J_r W_q / AR_rr, C[r][r] = -1, as (C, G) pairs: G is the row's
       // own-step indicator, so the second accumulator takes the row's force step exactly (the stop
@@ -2263,15 +2309,7 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
 #endif
       // qacc = qacc_smooth + sum_q W_q f_q (NH_ = fl - f on the frictionloss rows, NF_ = -f on the
       // others): lane i < NV sums dof i, then the row broadcasts it
-      float acc = 0.f;
-      const int di = r16 < NV ? r16 : 0;
-#pragma unroll
-      for (int q = 0; q < NS; q++)
-        acc = fmaf(Wl[q * RS_WROW + di], q < NA ? m.dof_frictionloss[q] - NH_[q] : -NF_[q], acc);
-      sfor<NV>([&](auto ic) {
-        constexpr int i = decltype(ic)::value;
-        v[i] = S.qacc_s[i] + rowbcast<i>(acc);
-      });
+      vel();
 #ifdef SOARM_PHASE_PROF
       if ((threadIdx.x & 63) == 0 && WPH_ID() < WPH_MAXW) {
         const long long rp2 = clock64();
