@@ -152,6 +152,9 @@ struct sim_batch {
 
 
 // mj_collision, one lane per (env, candidate pair); blockIdx.y = pair
+#ifndef SOARM_COLLIDE_BLOCK
+#define SOARM_COLLIDE_BLOCK 256  // envs (lanes) per collide workgroup
+#endif
 #ifndef SOARM_COLLIDE_WAVES
 #define SOARM_COLLIDE_WAVES 3  // min waves per SIMD (VGPR cap 512 / 3 = 168)
 #endif
@@ -162,7 +165,7 @@ __device__ __forceinline__ int m_pair_order(const DModel* dm, int y) { return dm
 __device__ uint32_t g_diag_skip[4];
 #endif
 template <int CCD>
-__global__ __launch_bounds__(256, SOARM_COLLIDE_WAVES) void k_collide(const DModel* __restrict__ dm, int n,
+__global__ __launch_bounds__(SOARM_COLLIDE_BLOCK, SOARM_COLLIDE_WAVES) void k_collide(const DModel* __restrict__ dm, int n,
                                                  const float* __restrict__ gpose,
                                                  float* __restrict__ cbuf, int* __restrict__ ccount,
                                                  uint32_t* __restrict__ pmask,
@@ -201,10 +204,11 @@ __global__ __launch_bounds__(256, SOARM_COLLIDE_WAVES) void k_collide(const DMod
 #endif
 }
 
-// the collide launch: (env, pair) lanes, 256-env blocks x npair
+// the collide launch: (env, pair) lanes, SOARM_COLLIDE_BLOCK-env blocks x npair
 static void launch_collide(const sim_batch* b, hipStream_t q, unsigned long long* pcyc) {
   auto kern = b->model->desc.ccd == SIM_CCD_NATIVE ? k_collide<SIM_CCD_NATIVE> : k_collide<SIM_CCD_MPR>;
-  hipLaunchKernelGGL(kern, dim3((b->n + 255) / 256, b->model->desc.npair), dim3(256), 0, q, b->d_model, b->n,
+  hipLaunchKernelGGL(kern, dim3((b->n + SOARM_COLLIDE_BLOCK - 1) / SOARM_COLLIDE_BLOCK, b->model->desc.npair),
+                     dim3(SOARM_COLLIDE_BLOCK), 0, q, b->d_model, b->n,
                      b->d_gpose, b->d_cbuf, b->d_ccount, b->d_pmask, b->d_sepax, pcyc);
 }
 
