@@ -69,6 +69,15 @@ struct DModel {
   int ncq;
   int nslot;            // total contact slots (sum of per-pair capacities)
   int free_diag;        // every free body has ipos = 0 and iquat = 1: its 6x6 M block is diagonal
+  // the contacts at qpos0, mj_resetData's pose: a soft reset (mj_checkPos/Vel/Acc) re-runs
+  // mj_forward there, collision included, so k_substep hands a reset env these instead of the
+  // collide output of the state it discarded.  Made once on the host with the kernels' own collide
+  // code (soarm_cpu.hip cpu_qpos0_contacts): the pair-mask words then the count word, and per
+  // contact its slot and 7-float record (dist, pos, normal), in pair order
+  uint32_t c0_w[(MAXP + 31) / 32 + 1];
+  int c0_n;
+  int c0_slot[SIM_MAXCON];
+  float c0_rec[SIM_MAXCON][7];
 
   // sites
   int site_bodyid[SIM_MAXSITE];

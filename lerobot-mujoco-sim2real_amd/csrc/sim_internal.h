@@ -37,6 +37,8 @@ int soarm_set_error(int code, const std::string& msg);
 // are host memory; calls are synchronous.
 struct CpuBatch;
 int cpu_batch_create(const sim_model* m, int n, CpuBatch** out);
+// the model's contacts at qpos0 (DModel c0_*: what a soft reset's mj_forward collides), at model creation
+int cpu_qpos0_contacts(sim_model* m);
 void cpu_batch_free(CpuBatch* c);
 int cpu_reset(CpuBatch* c, const sim_state* s, const float* init_qpos, const float* init_qvel,
               const float* extra_qpos, uint64_t seed, int64_t env_offset, const uint8_t* mask, float* obs);

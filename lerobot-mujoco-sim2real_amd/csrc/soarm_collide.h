@@ -326,51 +326,55 @@ HDI int discover(const MPair& P, MSup p[4], float sep[3]) {
   }
   return -1;
 }
-HDI void closest_tri(const float a[3], const float b[3], const float c[3], float o[3]) {
-  float ab[3], ac[3];
-  sub(ab, b, a);
-  sub(ac, c, a);
-  const float ap[3] = {-a[0], -a[1], -a[2]};
-  const float d1 = dot3(ab, ap), d2 = dot3(ac, ap);
-  if (d1 <= 0.f && d2 <= 0.f) {
+template <class T>
+HDI T dot3t(const T a[3], const T b[3]) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+// closest point of triangle abc to the origin (T = double: MPR's final depth and normal, below)
+template <class T>
+HDI void closest_tri(const T a[3], const T b[3], const T c[3], T o[3]) {
+  T ab[3], ac[3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) ab[k] = b[k] - a[k], ac[k] = c[k] - a[k];
+  const T ap[3] = {-a[0], -a[1], -a[2]};
+  const T d1 = dot3t(ab, ap), d2 = dot3t(ac, ap);
+  if (d1 <= T(0) && d2 <= T(0)) {
     o[0] = a[0], o[1] = a[1], o[2] = a[2];
     return;
   }
-  const float bp[3] = {-b[0], -b[1], -b[2]};
-  const float d3 = dot3(ab, bp), d4 = dot3(ac, bp);
-  if (d3 >= 0.f && d4 <= d3) {
+  const T bp[3] = {-b[0], -b[1], -b[2]};
+  const T d3 = dot3t(ab, bp), d4 = dot3t(ac, bp);
+  if (d3 >= T(0) && d4 <= d3) {
     o[0] = b[0], o[1] = b[1], o[2] = b[2];
     return;
   }
-  const float vc = d1 * d4 - d3 * d2;
-  if (vc <= 0.f && d1 >= 0.f && d3 <= 0.f) {
-    const float v = d1 / (d1 - d3);
+  const T vc = d1 * d4 - d3 * d2;
+  if (vc <= T(0) && d1 >= T(0) && d3 <= T(0)) {
+    const T v = d1 / (d1 - d3);
 #pragma unroll
     for (int k = 0; k < 3; k++) o[k] = a[k] + v * ab[k];
     return;
   }
-  const float cp[3] = {-c[0], -c[1], -c[2]};
-  const float d5 = dot3(ab, cp), d6 = dot3(ac, cp);
-  if (d6 >= 0.f && d5 <= d6) {
+  const T cp[3] = {-c[0], -c[1], -c[2]};
+  const T d5 = dot3t(ab, cp), d6 = dot3t(ac, cp);
+  if (d6 >= T(0) && d5 <= d6) {
     o[0] = c[0], o[1] = c[1], o[2] = c[2];
     return;
   }
-  const float vb = d5 * d2 - d1 * d6;
-  if (vb <= 0.f && d2 >= 0.f && d6 <= 0.f) {
-    const float w = d2 / (d2 - d6);
+  const T vb = d5 * d2 - d1 * d6;
+  if (vb <= T(0) && d2 >= T(0) && d6 <= T(0)) {
+    const T w = d2 / (d2 - d6);
 #pragma unroll
     for (int k = 0; k < 3; k++) o[k] = a[k] + w * ac[k];
     return;
   }
-  const float va = d3 * d6 - d5 * d4;
-  if (va <= 0.f && (d4 - d3) >= 0.f && (d5 - d6) >= 0.f) {
-    const float w = (d4 - d3) / ((d4 - d3) + (d5 - d6));
+  const T va = d3 * d6 - d5 * d4;
+  if (va <= T(0) && (d4 - d3) >= T(0) && (d5 - d6) >= T(0)) {
+    const T w = (d4 - d3) / ((d4 - d3) + (d5 - d6));
 #pragma unroll
     for (int k = 0; k < 3; k++) o[k] = b[k] + w * (c[k] - b[k]);
     return;
   }
-  const float den = 1.f / (va + vb + vc);
-  const float v = vb * den, w = vc * den;
+  const T den = T(1) / (va + vb + vc);
+  const T v = vb * den, w = vc * den;
 #pragma unroll
   for (int k = 0; k < 3; k++) o[k] = a[k] + ab[k] * v + ac[k] * w;
 }
@@ -442,12 +446,25 @@ HDI int mpr(const MPair& P, float& depth, float dir[3], float pos[3], float sep[
     MSup v4;
     P.sup(d, v4);
     if (reach_tol(p, v4, d) || it > MPR_ITERS) {
-      float w[3];
-      closest_tri(p[1].v, p[2].v, p[3].v, w);
-      depth = sqrtf(dot3(w, w));
+      // depth and normal = the portal's closest point to the origin, in fp64 on the exact Minkowski
+      // points s1 - s2 of the fp32 support points: a grazing contact's depth (~1e-6 m) is a
+      // cancellation of coordinates ~1 m (the table box), where fp32 leaves ~6e-8 m of noise in
+      // each component -- a normal tilted by up to ~5 degrees (tools/env_diverge.py: env 2624 of
+      // the headline's t = 100 states, an arm link on the table, 0.077 of tilt and 1e-2 rad/s of
+      // arm velocity per substep against the fp64 oracle's vertical normal)
+      double pa[3], pb[3], pc[3], w[3];
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        pa[k] = (double)p[1].v1[k] - (double)p[1].v2[k];
+        pb[k] = (double)p[2].v1[k] - (double)p[2].v2[k];
+        pc[k] = (double)p[3].v1[k] - (double)p[3].v2[k];
+      }
+      closest_tri(pa, pb, pc, w);
+      const double dd = sqrt(dot3t(w, w));
+      depth = (float)dd;
       if (fz(depth)) return 0;
-      const float inv = 1.f / depth;
-      dir[0] = w[0] * inv, dir[1] = w[1] * inv, dir[2] = w[2] * inv;
+      const double inv = 1.0 / dd;
+      dir[0] = (float)(w[0] * inv), dir[1] = (float)(w[1] * inv), dir[2] = (float)(w[2] * inv);
       portal_pos(p, pos);
       return 1;
     }

@@ -525,7 +525,11 @@ void step_env(const CpuBatch& B, const sim_state& st, const sim_params& pp, cons
       S.soft_reset(SIM_ST_BADQACC);
       if (applied) zero_applied(applied, NV, n, e);
       nc = 0;
-      forward_env(S, sol, cl, 0, nullptr, n, e);
+      if (con) {  // mj_forward at qpos0, collision included
+        S.kinematics();
+        nc = collide_env(B, S, e, cl, S.status);
+      }
+      forward_env(S, sol, cl, nc, nullptr, n, e);
     }
     nsum += (float)nc;
     const float ee[3] = {S.ee[0], S.ee[1], S.ee[2]};
@@ -570,6 +574,41 @@ int cpu_batch_create(const sim_model* m, int n, CpuBatch** out) {
 }
 
 void cpu_batch_free(CpuBatch* c) { delete c; }
+
+// the contacts at qpos0 into m->dm.c0_* (dmodel.h): kinematics at qpos0, then every candidate pair
+// through the kernels' collide code, as k_collide writes them (mask bit per pair with contacts,
+// count word for multi-contact pairs, records in the pair's slots)
+int cpu_qpos0_contacts(sim_model* m) {
+  DModel& d = m->dm;
+  memset(d.c0_w, 0, sizeof(d.c0_w));
+  d.c0_n = 0;
+  if (m->desc.disable_contact || d.npair == 0) return SIM_OK;
+  CpuBatch* c = nullptr;
+  cpu_batch_create(m, 1, &c);
+  const int nw = (d.npair + 31) >> 5;
+  dispatch_nf(m->nf, [&](auto nfc) {
+    constexpr int NF = decltype(nfc)::value;
+    Sim<6, NF> S(&c->dm, 1.f, -1.f, 1.f);
+    S.soft_reset(0);
+    S.kinematics();
+    float gpose[SIM_MAXBODY * BREC];
+    write_body_frames(S, gpose, 1, 0, 0, 1);
+    float cb[PAIR_MAXCON * 7];
+    for (int p = 0; p < d.npair; p++) {
+      PairOut o{cb, 1, 0, 0, d.pair_cap[p], 0};
+      collide_pair(c->dm, p, gpose, 1, 0, o, SepCache{c->sepax.data(), 1, 0});
+      if (o.n == 0) continue;
+      d.c0_w[p >> 5] |= 1u << (p & 31);
+      if (d.pair_cq[p] >= 0) d.c0_w[nw] |= (uint32_t)(o.n - 1) << (2 * d.pair_cq[p]);
+      for (int k = 0; k < o.n && d.c0_n < SIM_MAXCON; k++, d.c0_n++) {
+        d.c0_slot[d.c0_n] = d.pair_slot[p] + k;
+        for (int f = 0; f < 7; f++) d.c0_rec[d.c0_n][f] = cb[7 * k + f];
+      }
+    }
+  });
+  cpu_batch_free(c);
+  return SIM_OK;
+}
 
 int cpu_reset(CpuBatch* c, const sim_state* s, const float* init_qpos, const float* init_qvel,
               const float* extra_qpos, uint64_t seed, int64_t env_offset, const uint8_t* mask, float* obs) {

@@ -688,7 +688,12 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
 
   constexpr bool QUADR = lpe<NF>() == 4 && CON;
   if constexpr (CON && QUADR) {
-    if (ccount != nullptr) {
+    // per env (a soft reset's re-forward and the acc_bad retry list no contacts), so divergent
+    const bool listed = ccount != nullptr;
+    // (RS) whether this env's rows fit a row-space layout; without a contact list the layouts hold
+    // the NA frictionloss rows only, so an active limit row sends the wave to the v-form sweeps
+    bool rs_lane = nlim == 0;
+    if (listed) {
       // lane-split build (quad mode): every lane lists the env's contacts (pair, slot) in
       // pair order, then lane k of the quad builds contacts k, k+4, ... of the LDS records
       // and writes each into the quad's 4 columns; overflow contacts (rare) are built by
@@ -723,6 +728,28 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
           }
         }
       }
+      if constexpr (RS) {  // the contact categories of the RS layout (RsLayout): AT* CT* AC* in list order
+        const bool ok = nlim == 0 && ncon <= LDS_CON && rs_ok;
+        // the layouts instantiated: (KAT, KAC) = (0, 0) the cube resting alone, (1, 0) plus one
+        // arm-only contact, (0, 1) plus one arm-cube contact, (1, 1) both, in one env or in two envs
+        // of the wave (without it those waves -- ~1 launch in 10 over steps 20-120 -- took the v-form
+        // sweeps at ~4x the wave time); other waves take the v-form sweeps
+#ifdef SOARM_PHASE_PROF
+        rs_why = (nlim > 0) | ((ncon > LDS_CON) << 1) | ((!ok && nlim == 0 && ncon <= LDS_CON) << 2) |
+                 ((rs_nct > 4) << 3) | ((rs_nat > 1) << 4) | ((rs_nac > 1) << 5);
+#endif
+        rs_lane = ok && rs_nct <= 4 && rs_nat <= 1 && rs_nac <= 1;
+      }
+    }
+    if constexpr (RS) {
+      // one vote of the whole wave, taken with every lane active (outside the per-env branch): the
+      // solve's dispatch on rs_fast is wave-uniform
+      rs_fast = __all(rs_lane);
+#ifdef SOARM_PHASE_PROF
+      if (listed) rs_why |= (!rs_fast && rs_lane) << 6;  // an env that fits, in a wave with one that does not
+#endif
+    }
+    if (listed) {
       auto build_listed = [&](int c, bool split) {
         const int pk = __float_as_int(L.ex(c));
         const int p = pk >> 3, k = pk & 7;
@@ -736,22 +763,6 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
         build_row(c, rw, m.pair_body1[p], m.pair_body2[p], S.fric >= 0.f ? S.fric : m.pair_friction[p],
                   m.pair_tran[p], m.pair_margin[p], m.pair_KB[p][0], m.pair_KB[p][1], si, split);
       };
-      if constexpr (RS) {  // the contact categories of the RS layout (RsLayout): AT* CT* AC* in list order
-        bool ok = nlim == 0 && ncon <= LDS_CON && rs_ok;
-        // the layouts instantiated: (KAT, KAC) = (0, 0) the cube resting alone, (1, 0) plus one
-        // arm-only contact, (0, 1) plus one arm-cube contact, (1, 1) both, in one env or in two envs
-        // of the wave (without it those waves -- ~1 launch in 10 over steps 20-120 -- took the v-form
-        // sweeps at ~4x the wave time); other waves take the v-form sweeps
-#ifdef SOARM_PHASE_PROF
-        rs_why = (nlim > 0) | ((ncon > LDS_CON) << 1) | ((!ok && nlim == 0 && ncon <= LDS_CON) << 2) |
-                 ((rs_nct > 4) << 3) | ((rs_nat > 1) << 4) | ((rs_nac > 1) << 5);
-#endif
-        ok = ok && rs_nct <= 4 && rs_nat <= 1 && rs_nac <= 1;
-        rs_fast = __all(ok);
-#ifdef SOARM_PHASE_PROF
-        rs_why |= (!rs_fast && ok) << 6;  // an env that fits, in a wave with one that does not
-#endif
-      }
       const int nlds = ncon < LDS_CON ? ncon : LDS_CON;
       constexpr int SPL = RS ? 16 : 4;  // the RS kernel: the env's 16 lanes split the build
       for (int c0 = 0; c0 < nlds; c0 += SPL) {
@@ -760,8 +771,6 @@ DEVI int solve_constraints(Sim<NA, NF>& S, const float* __restrict__ cbuf, const
       }
       wave_sync();  // the quad's records, written by its 4 lanes
       for (int c = LDS_CON; c < ncon; c++) build_listed(c, false);
-    } else if constexpr (RS) {
-      rs_fast = true;  // no contacts: the NA frictionloss rows and the active limits
     }
   } else if constexpr (CON) {
     if (ccount != nullptr) {

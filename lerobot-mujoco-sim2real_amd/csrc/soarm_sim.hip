@@ -134,8 +134,10 @@ struct sim_batch {
     const float* action;
     float* obs;
     int frame_skip;
+    bool rs;  // the RS substep chosen (SOARM_RS, read per call): part of what the graph captured
     bool operator==(const GraphKey& o) const {
-      return !memcmp(&s, &o.s, sizeof(s)) && action == o.action && obs == o.obs && frame_skip == o.frame_skip;
+      return !memcmp(&s, &o.s, sizeof(s)) && action == o.action && obs == o.obs && frame_skip == o.frame_skip &&
+             rs == o.rs;
     }
   };
   bool use_graphs = true;
@@ -417,6 +419,11 @@ static int validate_and_build(const sim_model_desc& d, sim_model* M) {
     if (d.actuator_trnid[a] != a) return fail(SIM_E_MODEL, "actuator a must drive joint a");
   for (int i = na; i < d.nv; i++)
     if (d.dof_frictionloss[i] > 0) return fail(SIM_E_MODEL, "frictionloss on free dofs unsupported");
+  // one limit row per joint at a time (the kernels' LDS holds NA): both sides active at once needs
+  // range width < 2 margin
+  for (int j = 0; j < na; j++)
+    if (d.jnt_limited[j] && d.jnt_range[j][1] - d.jnt_range[j][0] < 2.0 * d.jnt_margin[j])
+      return fail(SIM_E_MODEL, "joint margin wider than half its range (both limit rows active) unsupported");
   if (d.nact > na || d.obs_nq > na) return fail(SIM_E_MODEL, "obs/act larger than the arm");
   for (int k = 0; k < d.obs_nq; k++)
     if (d.obs_qadr[k] >= na) return fail(SIM_E_MODEL, "observed joints must be arm hinges");
@@ -802,6 +809,7 @@ int sim_model_create(const sim_model_desc* desc, const float* hull_vert, const i
       }
     }
   }
+  cpu_qpos0_contacts(M);  // (the hull tables above are its input)
   *out = M;
   return SIM_OK;
 }
@@ -991,8 +999,8 @@ int sim_reset(sim_batch* b, const sim_state* s, const float* init_qpos, const fl
 }
 
 // the row-space PGS substep (k_substep<..., RS>) for the scene with a free body, up to rs_cap envs
-// (one round of waves); SOARM_RS=0 selects the quad kernel (16 envs per wave), read when the
-// env-step is enqueued
+// (one round of waves); SOARM_RS=0 selects the quad kernel (16 envs per wave), read per env-step call
+// (and part of the graph cache's key)
 static bool rs_on() {
   const char* v = getenv("SOARM_RS");
   return !(v && v[0] == '0');
@@ -1026,6 +1034,7 @@ int sim_step(sim_batch* b, const sim_state* s, const float* action, int frame_sk
   }
   // contacts: geom poses, then per substep (env, pair)-parallel collide + per-env dynamics
   const int np = b->model->desc.npair;
+  const bool rs = rs_on() && b->n <= b->rs_cap;
   auto enqueue = [&](hipStream_t q) {
     dispatch_nf(b->model->nf, [&](auto nfc) {
      dispatch_sol(sol, [&](auto solc) {
@@ -1050,7 +1059,7 @@ int sim_step(sim_batch* b, const sim_state* s, const float* action, int frame_sk
         auto kern = s->qfrc_applied ? k_substep<NA, NF, true, SOL> : k_substep<NA, NF, false, SOL>;
         int epb = 64 / lpe<NF>();  // envs per 64-thread workgroup
         if constexpr (NF == 1 && SOL == SIM_SOL_PGS) {
-          if (rs_on() && b->n <= b->rs_cap) {
+          if (rs) {
             kern = s->qfrc_applied ? k_substep<NA, NF, true, SOL, true> : k_substep<NA, NF, false, SOL, true>;
             epb = RS_EPW;
           }
@@ -1061,8 +1070,9 @@ int sim_step(sim_batch* b, const sim_state* s, const float* action, int frame_sk
         if (const char* v = getenv("SOARM_LDS_PAD")) lds_pad = (size_t)atol(v);
         // (SOARM_DIAG_NOGPOSE: the substep writes no geom records -- timing only, wrong contacts)
         const bool nogpose = getenv("SOARM_DIAG_NOGPOSE") != nullptr;
-        {
-          const int f11 = getenv("SOARM_RS_FORCE11") != nullptr;
+        {  // (static: a captured graph's memcpy node reads this address at every replay)
+          static int f11;
+          f11 = getenv("SOARM_RS_FORCE11") != nullptr;
           (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_rs_force11), &f11, sizeof(f11), 0, hipMemcpyHostToDevice, q);
         }
 #else
@@ -1084,7 +1094,7 @@ int sim_step(sim_batch* b, const sim_state* s, const float* action, int frame_sk
     return SIM_OK;
   }
   // replay a captured graph of the whole env-step (one launch instead of 1 + 2 x frame_skip)
-  const sim_batch::GraphKey key{*s, action, obs, frame_skip};
+  const sim_batch::GraphKey key{*s, action, obs, frame_skip, rs};
   hipGraphExec_t exec = nullptr;
   for (auto& g : b->graphs)
     if (g.first == key) exec = g.second;

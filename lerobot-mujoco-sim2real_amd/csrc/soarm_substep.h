@@ -109,6 +109,19 @@ __global__ __launch_bounds__(64) void k_geom(const DModel* __restrict__ dm, int 
 }
 inline dim3 geom_grid(int n) { return dim3((n + 64 / GEOM_LPE - 1) / (64 / GEOM_LPE)); }
 
+// a soft-reset env's contact input: the model's contacts at qpos0 (DModel c0_*) into its own slots of
+// the collide output and its pair mask.  Every lane of the env writes the same records, so each lane
+// reads back its own stores in the build that follows.  Cold: taken only by envs that soft-reset.
+DEVI void qpos0_contacts(const DModel& m, float* cbuf, int n, int e, PairMask& pm) {
+  const int nw = (m.npair + 31) >> 5;
+#pragma unroll
+  for (int k = 0; k < PairMask::MAXW; k++) pm.w[k] = k < nw ? m.c0_w[k] : 0u;
+  pm.cw = m.c0_w[nw];
+  for (int c = 0; c < m.c0_n; c++)
+#pragma unroll
+    for (int f = 0; f < 7; f++) soa(cbuf, m.c0_slot[c] * 7 + f, n, e) = m.c0_rec[c][f];
+}
+
 // one substep with contacts: gather -> forward -> Euler -> next substep's geom poses
 // (AP: st.qfrc_applied is set, as in k_step)
 // RS (PGS, free-body scene): the row-space kernel -- 16 lanes per env, 4 envs per wave.  The
@@ -160,8 +173,9 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
     store_state(S, st, n, e);
     if (AP) zero_applied(st.qfrc_applied, Sim<NA, NF>::NV, n, e);
   }
-  // a soft reset moved the env: the collide output no longer applies
-  const bool use = S.status == st0 && ccount != nullptr;
+  // a soft reset moved the env to qpos0: the collide output no longer applies, the contacts at
+  // qpos0 do (mj_resetData then mj_forward, collision included)
+  const bool use = ccount != nullptr;
   // Newton's frictionloss-zone history (two substeps, past the contact rows of the scratch slab):
   // a period-2 pattern predicts this substep's zones (soarm_newton.h)
   uint32_t zh1 = 0u, zh2 = 0u;
@@ -172,6 +186,7 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
   }
   PairMask pm;
   if (use) pm.load(pmask, m, n, e);  // (stays zero otherwise: no contact list)
+  if (use && S.status != st0) qpos0_contacts(m, const_cast<float*>(cbuf), n, e, pm);
 #ifdef SOARM_PHASE_PROF
   PHASE_T(t1);
   PSTAMP(0);
@@ -196,7 +211,10 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
     S.soft_reset(SIM_ST_BADQACC);
     store_state(S, st, n, e);
     if (AP) zero_applied(st.qfrc_applied, Sim<NA, NF>::NV, n, e);
-    ncon = forward<NA, NF, true, SOL, RS>(S, nullptr, nullptr, nullptr, n, e, L, cr);
+    PairMask p0;
+    if (use) qpos0_contacts(m, const_cast<float*>(cbuf), n, e, p0);
+    ncon = forward<NA, NF, true, SOL, RS>(S, use ? cbuf : nullptr, use ? ccount : nullptr, pmask, n, e, L, cr,
+                                          nullptr, p0);
   }
   PSTAMP(10);
   if constexpr (SOL == SIM_SOL_NEWTON) {

@@ -10,7 +10,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import cube_qpos
+from conftest import cube_qpos, fp32_noise_envelope
 from oracle import Oracle
 
 RNG = np.random.default_rng(17)
@@ -289,6 +289,7 @@ def test_cpu_env_step_bench_states(cpu_lib, solver):
     st["ncon"][:] = 0
     load_state(S, st)
     og = to_np(S.step(a))
+    env = fp32_noise_envelope(orc, st, a.astype(np.float64))
     oc = orc.step(st, a.astype(np.float64), nthreads=8)
     arm = st["ncon"] > 40  # more than the cube's 4 resting contacts in some substep
     blk = ~arm
@@ -299,13 +300,25 @@ def test_cpu_env_step_bench_states(cpu_lib, solver):
     # PGS / 2.5e-6 Newton; arm qvel max 2.3e-5)
     assert_pct(e[blk], 1e-6, 2e-6, 2e-6, what="block envs obs")
     assert_pct(dv[blk, 6:].max(1), 5e-6, 5e-4, 5e-4, what="block envs cube qvel")
-    assert_pct(dv[blk, :6].max(1), 5e-6, 5e-5, 2e-4, what="block envs arm qvel")
-    # envs whose arm touches the table or pushes the cube: over 10 substeps the chattering wrist
-    # servo amplifies rounding (the device test's tail; measured obs max 9.2e-5, cube qvel max
-    # 7.3e-3 PGS / 1.3e-2 Newton, arm qvel p50 4.5e-5 max 9.7e-2)
-    assert_pct(e[arm], 1e-6, 2e-4, 2e-4, what="arm-contact envs obs")
-    assert_pct(dv[arm, 6:].max(1), 5e-5, 2e-2, 2e-2, what="arm-contact envs cube qvel")
-    assert_pct(dv[arm, :6].max(1), 2e-4, 0.1, 0.1, what="arm-contact envs arm qvel")
+    assert_pct(dv[blk, :6].max(1), 5e-6, 5e-5, 1e-4, what="block envs arm qvel")
+    # envs whose arm touches the table or pushes the cube (r06: MPR's normal in fp64, soarm_collide.h
+    # mpr; before it, a grazing arm-link contact's fp32 normal tilted up to 5 degrees and the arm qvel
+    # max was 9.7e-2; measured now: arm qvel max 5.3e-6, cube 8.2e-5 PGS)
+    assert_pct(e[arm], 1e-6, 2e-5, 2e-5, what="arm-contact envs obs")
+    # (Newton's path meets a deep jaw-cube contact, env 2023 at substep 5, where MPR's portal -- and
+    # with it the normal -- is decided by near-tied support vertices: fp32 (0.452, -0.229, 0.862)
+    # against fp64 (0.445, -0.249, 0.860), 5.6e-3 m/s of cube velocity; tools/env_diverge.py)
+    assert_pct(dv[arm, 6:].max(1), 5e-5, 1e-3 if solver == "PGS" else 2e-2, 1e-3 if solver == "PGS" else 2e-2,
+               what="arm-contact envs cube qvel")
+    am = 1e-4 if solver == "PGS" else 2e-3  # (Newton: the same env, arm qvel 1.1e-3)
+    assert_pct(dv[arm, :6].max(1), 2e-5, am, am, what="arm-contact envs arm qvel")
+    # every env's arm qvel within 10x the oracle's own fp32-noise envelope (conftest.fp32_noise_envelope;
+    # PGS -- Newton's path crosses the MPR portal flip above, which no fp32-sized noise reproduces)
+    if solver == "PGS":
+        ratio = dv[:, :6].max(1) / (10 * env[:, :6].max(1) + 1e-6)
+        k = int(ratio.argmax())
+        assert ratio.max() <= 1.0, ("arm qvel vs fp32-noise envelope", ratio.max(), int(ids[k]), dv[k, :6].max(),
+                                    env[k, :6].max())
     # (a grazing contact, |depth| ~ fp32 resolution, can exist on one side only)
     assert abs(float(to_np(S.ncon).sum()) - float(st["ncon"].sum())) <= max(2.0, 1e-3 * float(st["ncon"].sum()))
 
@@ -441,3 +454,25 @@ def check_probe_contacts(cm, S, qs):
         r, k = rc[0], got[0]
         assert abs(out[e, k, 0] - r[0]) <= 2e-6, (e, out[e, k, 0], r[0])
         assert abs(abs(out[e, k, 4:7] @ r[4:7]) - 1) <= 1e-5, (e, out[e, k, 4:7], r[4:7])
+
+
+def test_cpu_soft_reset_contact_scene_limit_at_qpos0(cpu_lib):
+    """mj_checkVel soft reset in the pick scene on a model whose qpos0 sits inside a joint-limit
+    margin (conftest.limit_qpos0_model): the reset env's substep runs mj_forward at qpos0 with the
+    cube's resting contacts and the active limit row, as the oracle does."""
+    from conftest import limit_qpos0_model, soft_reset_states
+    from lerobot_mujoco_sim2real_amd import abi
+    cm = limit_qpos0_model()
+    orc = Oracle(cm)
+    n, bad = 64, [1, 6, 17, 30, 63]
+    st = soft_reset_states(cm, orc, n, bad)
+    S = make_sim(cm, n)
+    load_state(S, st)
+    S.substeps(1)
+    orc.step(st, None, nsub=1)
+    stat = to_np(S.status).astype(int)
+    assert all(stat[b] & abi.ST_BADQVEL for b in bad) and (stat == st["status"]).all()
+    np.testing.assert_allclose(to_np(S.qpos).T, st["qpos"], atol=5e-6)
+    dv = np.abs(to_np(S.qvel).T - st["qvel"]).max(1)
+    assert_pct(dv, *QVEL_BARS, what="qvel")
+    assert dv[bad].max() < 1e-5, dv[bad]

@@ -11,7 +11,7 @@ Tolerances (fp32 kernel vs fp64 oracle):
 import numpy as np
 import pytest
 
-from conftest import cube_qpos
+from conftest import cube_qpos, fp32_noise_envelope, limit_qpos0_model, soft_reset_states
 from oracle import Oracle
 from test_cpu_backend import contact_point_split
 
@@ -310,9 +310,10 @@ def test_one_substep_bench_state_mixed_contacts(gpu_lib, rs, monkeypatch):
     assert_pct(dv[:, 6:].max(1), *QVEL_BARS, what="cube qvel")
     assert_pct(dv.max(1), *QVEL_BARS, what="qvel")
     assert to_np(S.ncon).sum() == st["ncon"].sum()
-    # the arm's velocities (its rows retire from the sweeps early, soarm_pgs.h ysweeps): the
-    # bulk stays at fp32 resolution, as with the full sweep schedule (measured p99 8e-8,
-    # max 2e-5 on 1024 envs, identical to a build without retirement)
+    # the arm's velocities: rs = "1" sweeps every row in mj_solPGS order (no retirement); rs = "0"
+    # (the quad kernel) retires the arm's rows once a sweep moves them by <= 1e-6 (soarm_pgs.h
+    # ysweeps).  Either way the bulk stays at fp32 resolution (quad, measured: p99 8e-8, max 2e-5
+    # on 1024 envs, identical to a build without retirement)
     err = np.abs(to_np(S.qvel).T[:, :6] - st["qvel"][:, :6]).max(1)
     assert np.percentile(err, 99) < 1e-6 and err.max() < 2e-4, (np.percentile(err, 99), err.max())
 
@@ -383,33 +384,19 @@ def test_one_substep_domain_randomised(gpu_lib):
     assert to_np(S.ncon).sum() == st["ncon"].sum()
 
 
-def _fp32_envelope(cm, orc, st, a, params=None, nthreads=16):
-    """Per-env qvel envelope of one env-step, the larger of two fp32 spreads around the fp64 oracle
-    stepped from st (the test's reference): (i) the same oracle re-rounded to fp32 after every
-    substep -- what fp32 state rounding alone does over the 10 substeps -- and (ii) the library's
-    fp32 CPU backend (sim_batch_create(..., device = -1): the kernels' per-env code on the host,
-    PGS in mj_solPGS's row order), an independent fp32 arithmetic of the same step.  A chattering
-    wrist servo amplifies fp32 arithmetic far beyond state rounding (r05: one env of 4096 at 3e-2
-    rad/s on the device against a 5e-4 rounding envelope), which (ii) measures per env."""
-    import torch
-    from lerobot_mujoco_sim2real_amd.sim import BatchSim
-    b = {k: v.copy() for k, v in st.items()}
-    for sub in range(10):
-        orc.step(b, a if sub == 0 else None, nsub=1, params=params, nthreads=nthreads)
-        for k in ("qpos", "qvel", "warm"):
-            b[k][:] = b[k].astype(np.float32)
-    ref = {k: v.copy() for k, v in st.items()}
-    orc.step(ref, a, params=params, nthreads=nthreads)
-    n = st["qpos"].shape[0]
-    C = BatchSim(cm, n, -1)
-    if params is not None:
-        C.set_params(mass_scale=params[:, 0], friction=params[:, 1], damping_scale=params[:, 2])
-    C.qpos.copy_(torch.as_tensor(st["qpos"].T, dtype=torch.float32))
-    C.qvel.copy_(torch.as_tensor(st["qvel"].T, dtype=torch.float32))
-    C.qacc_warmstart.copy_(torch.as_tensor(st["warm"].T, dtype=torch.float32))
-    C.ctrl.copy_(torch.as_tensor(st["ctrl"].T, dtype=torch.float32))
-    C.step(torch.as_tensor(a, dtype=torch.float32))
-    return np.maximum(np.abs(b["qvel"] - ref["qvel"]), np.abs(to_np(C.qvel).T - ref["qvel"]))
+# arm qvel max over one full-size env-step (4096 / 8192 envs) against the fp64 oracle (r06, after
+# the MPR normal fix; r05: 5e-2)
+ARM_QVEL_MAX = 2e-3
+
+
+def _within_noise_envelope(dv, env):
+    """Every env's arm qvel within 10x the fp64 oracle's own fp32-noise envelope (conftest.
+    fp32_noise_envelope: the oracle with +-8 fp32 ulps of state noise injected after every substep,
+    no library code; VERDICT r5 next #1).  1e-6: qvel's fp32 resolution at ~10 rad/s."""
+    ratio = dv[:, :6].max(1) / (10 * env[:, :6].max(1) + 1e-6)
+    k = int(ratio.argmax())
+    assert ratio.max() <= 1.0, ("arm qvel vs fp32-noise envelope", ratio.max(), k, dv[k, :6].max(), env[k, :6].max(),
+                                "envs over 1/10 of it", int((ratio > 0.1).sum()))
 
 
 def test_dr_env_step_full_size(gpu_lib):
@@ -427,16 +414,13 @@ def test_dr_env_step_full_size(gpu_lib):
     st["ncon"][:] = 0
     load_state(S, st)
     og = to_np(S.step(a))
-    env = _fp32_envelope(cm, orc, st, a.astype(np.float64), params=prm)
+    env = fp32_noise_envelope(orc, st, a.astype(np.float64), params=prm, nthreads=16)
     oc = orc.step(st, a.astype(np.float64), params=prm, nthreads=16)
     assert_pct(np.abs(og - oc).max(1), 1e-6, 2e-6, 2e-4, what="obs")
     dv = np.abs(to_np(S.qvel).T - st["qvel"])
     assert_pct(dv[:, 6:].max(1), 5e-6, 5e-4, 2e-2, what="cube qvel")
-    assert_pct(dv[:, :6].max(1), 5e-6, 5e-4, 5e-2, what="arm qvel")
-    # every env's arm qvel within 10x its own fp32 envelope + 5e-4
-    ratio = dv[:, :6].max(1) / (10 * env[:, :6].max(1) + 5e-4)
-    k = int(ratio.argmax())
-    assert ratio.max() <= 1.0, ("arm qvel vs fp32 envelope", ratio.max(), k, dv[k, :6].max(), env[k, :6].max())
+    assert_pct(dv[:, :6].max(1), 5e-6, 5e-5, ARM_QVEL_MAX, what="arm qvel")
+    _within_noise_envelope(dv, env)
     np.testing.assert_allclose(to_np(S.qpos).T[:, 6:9], st["qpos"][:, 6:9], atol=5e-6)
     assert int((to_np(S.status) != 0).sum()) == int((st["status"] != 0).sum())
 
@@ -652,6 +636,33 @@ def test_bad_state_soft_reset(gpu_lib, arm_model_nocontact):
     assert np.isfinite(to_np(S.qpos)).all() and (st[[0, 1, 2, 3]] == 0).all()
 
 
+@pytest.mark.parametrize("rs", ["1", "0"])
+def test_soft_reset_contact_scene_limit_at_qpos0(gpu_lib, rs, monkeypatch):
+    """mj_checkVel soft resets in the pick scene, on a model whose qpos0 sits inside a joint-limit
+    margin (conftest.limit_qpos0_model): the reset envs run mj_forward at qpos0 with the
+    cube's 4 resting contacts (DModel c0_*, made at model creation) and the active limit row, in
+    waves shared with envs that keep their own contacts; rs = "1" the RS kernel (a reset env's
+    limit row sends its wave to the v-form sweeps by a wave-wide vote), "0" the quad kernel."""
+    from lerobot_mujoco_sim2real_amd import abi
+    monkeypatch.setenv("SOARM_RS", rs)
+    cm = limit_qpos0_model()
+    orc = Oracle(cm)
+    n, bad = 64, [1, 6, 17, 30, 63]
+    st = soft_reset_states(cm, orc, n, bad)
+    S = make_sim(cm, n)
+    st["ncon"][:] = 0
+    load_state(S, st)
+    S.substeps(1)
+    orc.step(st, None, nsub=1)
+    stat = to_np(S.status).astype(int)
+    assert all(stat[b] & abi.ST_BADQVEL for b in bad) and (stat == st["status"]).all()
+    np.testing.assert_allclose(to_np(S.qpos).T, st["qpos"], atol=5e-6)
+    dv = np.abs(to_np(S.qvel).T - st["qvel"]).max(1)
+    assert_pct(dv, *QVEL_BARS, what="qvel")
+    assert dv[bad].max() < 1e-5, dv[bad]
+    assert to_np(S.ncon).sum() == st["ncon"].sum()
+
+
 def test_golden_fixture_gpu(gpu_lib, arm_model_nocontact):
     import os
     z = np.load(os.path.join(os.path.dirname(__file__), "golden", "oracle_arm_random.npz"))
@@ -858,22 +869,19 @@ def test_contact_env_step_late_states_full_size(gpu_lib):
     st["ncon"][:] = 0
     load_state(S, st)
     og = to_np(S.step(a))  # graph replay of geom + 10 x (collide, substep)
-    env = _fp32_envelope(cm, orc, st, a.astype(np.float64))
+    env = fp32_noise_envelope(orc, st, a.astype(np.float64), nthreads=16)
     oc = orc.step(st, a.astype(np.float64), nthreads=16)
     assert st["ncon"].sum() > 4 * 10 * n, "no arm contacts in the sample"
     assert_pct(np.abs(og - oc).max(1), 1e-6, 2e-6, 2e-4, what="obs")
     # over 10 substeps an env whose arm pushes the cube can see fp32 / fp64 PGS stop a sweep apart
     # in several substeps (r03 on 4096 envs at t = 100: cube qvel p50 5e-7, p99 4.2e-5, max 2.3e-3)
     dv = np.abs(to_np(S.qvel).T - st["qvel"])
-    # (the arm's: a chattering wrist servo amplifies fp32 rounding over the 10 substeps, as in the
-    # shadowing tests; r03: one env of 4096 at 3.2e-2)
     assert_pct(dv[:, 6:].max(1), 5e-6, 5e-4, 2e-2, what="cube qvel")
-    assert_pct(dv[:, :6].max(1), 5e-6, 5e-4, 5e-2, what="arm qvel")
-    # every env's arm qvel within 10x its own fp32 envelope + 5e-4 (the 0.1 max let
-    # any single env off; the envelope covers the chattering wrist that needed it)
-    ratio = dv[:, :6].max(1) / (10 * env[:, :6].max(1) + 5e-4)
-    k = int(ratio.argmax())
-    assert ratio.max() <= 1.0, ("arm qvel vs fp32 envelope", ratio.max(), k, dv[k, :6].max(), env[k, :6].max())
+    # the arm's: r03-r05 one env of 4096 (2624) at 3.2e-2 -- a grazing arm-link contact on the table
+    # whose fp32 MPR normal tilted by up to 5 degrees; fixed in r06 (soarm_collide.h mpr: the final
+    # depth and normal in fp64; tools/env_diverge.py)
+    assert_pct(dv[:, :6].max(1), 5e-6, 5e-5, ARM_QVEL_MAX, what="arm qvel")
+    _within_noise_envelope(dv, env)
     np.testing.assert_allclose(to_np(S.qpos).T[:, 6:9], st["qpos"][:, 6:9], atol=5e-6)
     assert int((to_np(S.status) != 0).sum()) == int((st["status"] != 0).sum())
     assert abs(float(to_np(S.ncon).sum()) - float(st["ncon"].sum())) <= 1e-4 * float(st["ncon"].sum())
@@ -928,44 +936,47 @@ def test_pgs_vs_reference_newton(gpu_lib):
     """Fidelity to what the reference computes: its scene has no <option>, so mj_step runs MuJoCo's
     default Newton solver (SOARM101/SO101/scene_with_table_v.xml:1-32, SOARM101_Env.py:131-132).
     The device's PGS (north star) against the exact optimum of the same constraint problem (oracle
-    Newton, tolerance 0), one substep from bench states at t = 20 and 120, 1024 envs.  Bars from
+    Newton, tolerance 0), one substep from bench states at t = 20 and 120: every arm-contact env of
+    the 4096 bench envs (oracle census; 3 at t = 20, 13 at t = 120) plus 1024 block envs.  Bars from
     the 4096-env measurement (profiles/r05_rs_bars.json): block envs (cube resting) cube qvel
     p50 1.9e-5 / 3.6e-5, p99 3.6e-5, max 3.7e-5; arm-contact envs cube qvel p99 6.5e-3 / max
     7.1e-3, arm qvel p99 2.3e-4 / max 2.4e-4; arm qvel elsewhere <= 1.2e-7."""
     for t0 in (20, 120):
-        cm, orc, st, _ = _bench_states("contact", 1024, t0, nthreads=16)
+        cm, orc, st4, _ = _bench_states("contact", 4096, t0, nthreads=16)
+        names = cm.geom_names
+        table, cube = names.index("table"), names.index("cube")
+        arm4 = np.array([any({int(c[7]), int(c[8])} != {table, cube} for c in
+                             orc.forward(st4["qpos"][i], st4["qvel"][i], st4["ctrl"][i], st4["warm"][i])["contacts"])
+                         for i in range(4096)])
+        pick = np.r_[np.flatnonzero(arm4), np.flatnonzero(~arm4)[:1024]]
+        st = {k: v[pick].copy() for k, v in st4.items()}
+        arm = arm4[pick]
+        n = len(pick)
         ref = _exact_newton_substep(cm, st)
-        S = make_sim(cm, 1024)
+        S = make_sim(cm, n)
         load_state(S, st)
         S.substeps(1)
         dv = np.abs(to_np(S.qvel).T - ref["qvel"])
-        names = cm.geom_names
-        table, cube = names.index("table"), names.index("cube")
-        arm = np.array([any({int(c[7]), int(c[8])} != {table, cube} for c in
-                            orc.forward(st["qpos"][i], st["qvel"][i], st["ctrl"][i], st["warm"][i])["contacts"])
-                        for i in range(1024)])
         assert_pct(dv[~arm, 6:].max(1), 4e-5, 5e-5, 1e-4, what=f"t{t0} block envs cube qvel")
         assert_pct(dv[~arm, :6].max(1), 1e-6, 1e-6, 2e-6, what=f"t{t0} block envs arm qvel")
-        if arm.any():
-            # arm-contact envs (3 at t = 20, 13 at t = 120 in 4096): bars at ~2x the measured
-            # PGS-vs-exact-optimum gap (r03_newton_gap.json, device PGS: cube qvel p50 3.6e-5 /
-            # max 7.1e-3, arm qvel p50 4.5e-6 / max 2.4e-4) -- the PGS algorithm's own distance,
-            # identical in the fp64 oracle PGS, which the device PGS must match within QVEL_BARS
-            # (the p50 bars need a sample: with fewer than 8 such envs the median is one env's
-            # gap and only the max bars apply)
-            # (r05, 4096 envs at t = 120, tools/rs_bars.py: cube qvel p99 6.5e-3 / max 7.1e-3, arm
-            # qvel p99 2.3e-4 / max 2.4e-4 -- the oracle's own PGS is 7.1e-3 / 1.9e-4 from the
-            # optimum; the bars are ~2x those p99)
-            few = arm.sum() < 8
-            assert_pct(dv[arm, 6:].max(1), 1.3e-2 if few else 8e-5, 1.3e-2, 1.4e-2,
-                       what=f"t{t0} arm-contact envs cube qvel")
-            assert_pct(dv[arm, :6].max(1), 5e-4 if few else 1e-5, 5e-4, 5e-4, what=f"t{t0} arm-contact envs arm qvel")
-            pgs = {k: v[arm].copy() for k, v in st.items()}
-            orc.step(pgs, None, nsub=1)
-            dp = np.abs(to_np(S.qvel).T[arm] - pgs["qvel"]).max(1)
-            # device PGS against the oracle's mj_solPGS on the same rows (r05 4096 envs: arm-contact
-            # envs p99 2.1e-4 / max 2.4e-4 at t = 120, 9.4e-5 / 9.6e-5 at t = 20)
-            assert_pct(dp, 1e-4, 3e-4, 5e-4, what=f"t{t0} device PGS vs oracle PGS, arm-contact envs")
+        assert arm.any(), "arm contacts in the 4096 bench states"
+        # arm-contact envs: bars at ~2x the measured PGS-vs-exact-optimum gap (r03_newton_gap.json,
+        # device PGS: cube qvel p50 3.6e-5 / max 7.1e-3, arm qvel p50 4.5e-6 / max 2.4e-4) -- the PGS
+        # algorithm's own distance, identical in the fp64 oracle PGS, which the device PGS must match
+        # within QVEL_BARS (with fewer than 8 such envs -- t = 20 -- the median is one env's gap and
+        # only the max bars apply).  r05, 4096 envs at t = 120 (tools/rs_bars.py): cube qvel p99
+        # 6.5e-3 / max 7.1e-3, arm qvel p99 2.3e-4 / max 2.4e-4 -- the oracle's own PGS is 7.1e-3 /
+        # 1.9e-4 from the optimum
+        few = arm.sum() < 8
+        assert_pct(dv[arm, 6:].max(1), 1.3e-2 if few else 8e-5, 1.3e-2, 1.4e-2,
+                   what=f"t{t0} arm-contact envs cube qvel")
+        assert_pct(dv[arm, :6].max(1), 5e-4 if few else 1e-5, 5e-4, 5e-4, what=f"t{t0} arm-contact envs arm qvel")
+        pgs = {k: v[arm].copy() for k, v in st.items()}
+        orc.step(pgs, None, nsub=1)
+        dp = np.abs(to_np(S.qvel).T[arm] - pgs["qvel"]).max(1)
+        # device PGS against the oracle's mj_solPGS on the same rows (r05 4096 envs: arm-contact
+        # envs p99 2.1e-4 / max 2.4e-4 at t = 120, 9.4e-5 / 9.6e-5 at t = 20)
+        assert_pct(dp, 1e-4, 3e-4, 5e-4, what=f"t{t0} device PGS vs oracle PGS, arm-contact envs")
 
 
 @pytest.mark.parametrize("t0", [20, 120])
