@@ -455,10 +455,12 @@ def main():
             got = shard.gather_rollouts(rows if backend == "nccl" else rows.cpu(), dst=0)
             torch.cuda.synchronize()
             gather_s = time.perf_counter() - tg
-            if world == 1:  # one rank: the gathered rows are this rank's, bit for bit
-                gather_exact = bool(torch.equal(got.to(rows.device), rows))
     sync()
     dt = time.perf_counter() - t0
+    if rollout and use_pg and world == 1:
+        # one rank: the gathered rows are this rank's, bit for bit (checked after the clock stops: the
+        # first torch.equal of a run loads its kernels, ~20 ms, which r05 timed as "RCCL overhead")
+        gather_exact = bool(torch.equal(got.to(rows.device), rows))
     (dt,) = max_over_ranks(dt)
     if gather_s is not None:
         (gather_s,) = max_over_ranks(gather_s)

@@ -205,6 +205,13 @@ HDI void geom_center(const DModel& m, int g, const GeomPose& P, float c[3]) {
 }
 
 // ---------------------------------------------------------------------- MPR
+HDI double dotd(const double a[3], const double b[3]) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+HDI void subd(double r[3], const double a[3], const double b[3]) {
+  r[0] = a[0] - b[0], r[1] = a[1] - b[1], r[2] = a[2] - b[2];
+}
+HDI void crossd(double r[3], const double a[3], const double b[3]) {
+  r[0] = a[1] * b[2] - a[2] * b[1], r[1] = a[2] * b[0] - a[0] * b[2], r[2] = a[0] * b[1] - a[1] * b[0];
+}
 struct MSup {
   float v[3], v1[3], v2[3];
 };
@@ -378,36 +385,43 @@ HDI void closest_tri(const T a[3], const T b[3], const T c[3], T o[3]) {
 #pragma unroll
   for (int k = 0; k < 3; k++) o[k] = a[k] + ab[k] * v + ac[k] * w;
 }
-HDI void portal_pos(const MSup p[4], float pos[3]) {
-  float d[3], x[3], b[4];
-  portal_dir(p, d);
-  cross(x, p[1].v, p[2].v);
-  b[0] = dot3(x, p[3].v);
-  cross(x, p[3].v, p[2].v);
-  b[1] = dot3(x, p[0].v);
-  cross(x, p[0].v, p[1].v);
-  b[2] = dot3(x, p[3].v);
-  cross(x, p[2].v, p[1].v);
-  b[3] = dot3(x, p[0].v);
-  float sum = b[0] + b[1] + b[2] + b[3];
-  if (fz(sum) || sum < 0.f) {
-    b[0] = 0.f;
-    cross(x, p[2].v, p[3].v);
-    b[1] = dot3(x, d);
-    cross(x, p[3].v, p[1].v);
-    b[2] = dot3(x, d);
-    cross(x, p[1].v, p[2].v);
-    b[3] = dot3(x, d);
-    sum = b[1] + b[2] + b[3];
-  }
-  const float inv = 1.f / sum;
-  float s1[3] = {0, 0, 0}, s2[3] = {0, 0, 0};
+// contact position: the origin's barycentric weights on the portal tetrahedron (or its face),
+// applied to both geoms' support points -- in fp64 on the exact Minkowski points (the weights are
+// triple products of coordinates ~1 m whose result is ~depth x area: the same cancellation as the
+// normal's, mpr below).  pd: the portal direction.
+HDI void portal_pos(const MSup p[4], const double pd[3], float pos[3]) {
+  double v[4][3], x[3], b[4];
 #pragma unroll
   for (int i = 0; i < 4; i++)
 #pragma unroll
-    for (int k = 0; k < 3; k++) s1[k] += b[i] * p[i].v1[k], s2[k] += b[i] * p[i].v2[k];
+    for (int k = 0; k < 3; k++) v[i][k] = (double)p[i].v1[k] - (double)p[i].v2[k];
+  crossd(x, v[1], v[2]);
+  b[0] = dotd(x, v[3]);
+  crossd(x, v[3], v[2]);
+  b[1] = dotd(x, v[0]);
+  crossd(x, v[0], v[1]);
+  b[2] = dotd(x, v[3]);
+  crossd(x, v[2], v[1]);
+  b[3] = dotd(x, v[0]);
+  double sum = b[0] + b[1] + b[2] + b[3];
+  if (fabs(sum) < 2.220446049250313e-16 || sum < 0.0) {  // (libccd's zero test in double)
+    b[0] = 0.0;
+    crossd(x, v[2], v[3]);
+    b[1] = dotd(x, pd);
+    crossd(x, v[3], v[1]);
+    b[2] = dotd(x, pd);
+    crossd(x, v[1], v[2]);
+    b[3] = dotd(x, pd);
+    sum = b[1] + b[2] + b[3];
+  }
+  const double inv = 1.0 / sum;
+  double s1[3] = {0, 0, 0}, s2[3] = {0, 0, 0};
 #pragma unroll
-  for (int k = 0; k < 3; k++) pos[k] = 0.5f * (s1[k] + s2[k]) * inv;
+  for (int i = 0; i < 4; i++)
+#pragma unroll
+    for (int k = 0; k < 3; k++) s1[k] += b[i] * (double)p[i].v1[k], s2[k] += b[i] * (double)p[i].v2[k];
+#pragma unroll
+  for (int k = 0; k < 3; k++) pos[k] = (float)(0.5 * (s1[k] + s2[k]) * inv);
 }
 // returns 1 with depth/dir(geom1->geom2)/pos when penetrating; sep = a separating axis
 // when it proved the pair apart by a support query (else unchanged)
@@ -465,7 +479,13 @@ HDI int mpr(const MPair& P, float& depth, float dir[3], float pos[3], float sep[
       if (fz(depth)) return 0;
       const double inv = 1.0 / dd;
       dir[0] = (float)(w[0] * inv), dir[1] = (float)(w[1] * inv), dir[2] = (float)(w[2] * inv);
-      portal_pos(p, pos);
+      double ab[3], ac[3], pd[3];  // the portal's direction (its face normal), for the face fallback
+#pragma unroll
+      for (int k = 0; k < 3; k++) ab[k] = pb[k] - pa[k], ac[k] = pc[k] - pa[k];
+      crossd(pd, ab, ac);
+      const double pn = sqrt(dotd(pd, pd));
+      if (pn > 0.0) pd[0] /= pn, pd[1] /= pn, pd[2] /= pn;
+      portal_pos(p, pd, pos);
       return 1;
     }
     expand(p, v4);
@@ -500,13 +520,6 @@ struct GSup {
   double v[3];
   float v1[3];
 };
-HDI double dotd(const double a[3], const double b[3]) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
-HDI void subd(double r[3], const double a[3], const double b[3]) {
-  r[0] = a[0] - b[0], r[1] = a[1] - b[1], r[2] = a[2] - b[2];
-}
-HDI void crossd(double r[3], const double a[3], const double b[3]) {
-  r[0] = a[1] * b[2] - a[2] * b[1], r[1] = a[2] * b[0] - a[0] * b[2], r[2] = a[0] * b[1] - a[1] * b[0];
-}
 HDI void copyd(double d[3], const double s[3]) { d[0] = s[0], d[1] = s[1], d[2] = s[2]; }
 HDI void gsel(GSup& dst, bool c, const GSup& src) {  // (value selects: see sel)
 #pragma unroll

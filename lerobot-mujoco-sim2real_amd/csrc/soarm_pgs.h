@@ -168,6 +168,9 @@ enum { L_DOF = 0, L_SGN = 1, L_AREF = 2, L_R = 3, L_ARD = 4, L_IARD = 5, L_FRC =
 // res = AR f + b, cost(f0) - cost(f1) = sum_r AR_rr / 2 (f1 - f0)_r (s0 + s1)_r, and each
 // row's force change over the sweep is its own step, which a second accumulator beside s takes
 // exactly (its coefficient is 1 at the row's own step, 0 elsewhere).
+#ifndef SOARM_RS_SEQ
+#define SOARM_RS_SEQ 0  // 1: the decoupled layouts' steps one at a time (A/B of the paired sweep)
+#endif
 constexpr int RS_MAXROW = 32;               // rows of one env (2 slots x 16 lanes)
 constexpr int RS_WROW = 12;                 // floats per row of W = M^-1 J' in LDS (NV <= 12)
 constexpr int RS_WENV = RS_MAXROW * RS_WROW + 4;  // per env (+4: the 4 envs of a wave on distinct banks)
@@ -228,6 +231,7 @@ template <int NA, int KAT, int KAC>
 struct RsLayout {
   static_assert(NA + 4 * (KAT + KAC) <= 16, "slot B holds the F, AT and AC rows");
   static constexpr int CT0 = NA + 4 * KAT, AC0 = CT0 + 16, NS = AC0 + 4 * KAC;
+  static constexpr bool decoupled = KAC == 0;  // no AC rows: the slot-B (arm) and slot-A (cube) steps never meet
   static constexpr int slot(int q) { return (q >= CT0 && q < AC0) ? 0 : 1; }
   static constexpr int lane(int q) { return q < CT0 ? q : q < AC0 ? q - CT0 : q - 16; }
   static constexpr bool upd_a(int q) { return q >= CT0; }                 // CT, AC
@@ -243,9 +247,46 @@ struct RsLayout {
 // VALU op in flight, so a step is its broadcast-max, the residual update of the slot the NEXT step
 // broadcasts from, then the other slot's update and the bound updates -- which are also the 2 wait
 // states the next broadcast needs after that write (padded with s_nop where a step has fewer)
+//
+// Layouts without AC rows (KAC = 0: no arm-cube contact in the wave, ~99.6% of the headline's waves)
+// are two systems that never meet: the F / AT steps read and move slot B alone, the CT steps slot A
+// alone (M is block diagonal).  Their steps then run paired -- B step i beside A step i, two
+// independent chains in one instruction stream, each hiding the other's latency and DPP drain --
+// and each slot still takes its own steps in mj_solPGS order, so every residual, force and
+// accumulator is bit-identical to the sequential sweep.
 template <int NA, class LY>
 DEVI void rs_sweep(f2& sA, f2& sB, const f2 (&CA)[LY::NS], const f2 (&CB)[LY::NS], float (&NF)[LY::NS],
                    float (&NH)[NA]) {
+  if constexpr (LY::decoupled && !SOARM_RS_SEQ) {
+    constexpr int NB = LY::CT0, NAS = LY::NS - LY::CT0;  // slot-B steps (F, AT), slot-A steps (CT)
+    static_assert(NB <= NAS, "slot A has at least as many steps as slot B");
+    sfor<NAS>([&](auto ic) {
+      constexpr int I = decltype(ic)::value;
+      constexpr bool HB = I < NB;
+      constexpr int QA = LY::CT0 + I;
+      // wait states before this step's broadcasts (2 needed after the VALU write of the source):
+      // B reads sB, written by step I-1's first update, with the sA update and >= 2 bound updates
+      // after it; A reads sA, written by step I-1's second update, with step I-1's bound updates
+      // (2 when it had a B step, else 1) and this step's B broadcast after it
+      constexpr int waitA = I == 0 ? 0 : ((I - 1) < NB ? 2 + (HB ? 1 : 0) : 1 + (HB ? 1 : 0));
+      float dB = 0.f, dA;
+      if constexpr (HB) dB = max_bcast<LY::lane(I), (I == 0 ? 2 : 0)>(sB.x, NF[I]);
+      dA = max_bcast<LY::lane(QA), (waitA >= 2 ? 0 : 2 - waitA)>(sA.x, NF[QA]);
+      if constexpr (HB && I < NA) dB = vmin(dB, NH[I]);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (HB) sB = __builtin_elementwise_fma(CB[I], f2{dB, dB}, sB);
+      __builtin_amdgcn_sched_barrier(0);
+      sA = __builtin_elementwise_fma(CA[QA], f2{dA, dA}, sA);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (HB) {
+        NF[I] -= dB;
+        if constexpr (I < NA) NH[I] -= dB;
+      }
+      NF[QA] -= dA;
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    return;
+  }
   sfor<LY::NS>([&](auto qc) {
     constexpr int Q = decltype(qc)::value;
     constexpr int SL = LY::slot(Q), LN = LY::lane(Q);

@@ -152,18 +152,18 @@ def test_trajectory_shadowing(gpu_lib, arm_model_nocontact):
         assert np.quantile(e, 0.9) <= 10 * np.quantile(env, 0.9) + 2e-4
 
 
-def _contact_poses(cm, n):
+def _contact_poses(cm, n, rng=RNG):
     """Poses that drive the gripper into the table / fold the arm (self contacts)."""
     q = np.zeros((n, 6))
-    q[:, 0] = RNG.uniform(-1.0, 1.0, n)
-    q[:, 1] = RNG.uniform(0.6, 1.6, n)
-    q[:, 2] = RNG.uniform(-0.5, 1.0, n)
-    q[:, 3] = RNG.uniform(0.3, 1.6, n)
-    q[:, 4] = RNG.uniform(-2.0, 2.0, n)
-    q[:, 5] = RNG.uniform(0.0, 1.5, n)
+    q[:, 0] = rng.uniform(-1.0, 1.0, n)
+    q[:, 1] = rng.uniform(0.6, 1.6, n)
+    q[:, 2] = rng.uniform(-0.5, 1.0, n)
+    q[:, 3] = rng.uniform(0.3, 1.6, n)
+    q[:, 4] = rng.uniform(-2.0, 2.0, n)
+    q[:, 5] = rng.uniform(0.0, 1.5, n)
     half = n // 2
-    q[half:, 1] = RNG.uniform(-1.7, -1.3, n - half)    # home-like fold: shoulder servo vs lower arm
-    q[half:, 2] = RNG.uniform(1.3, 1.69, n - half)
+    q[half:, 1] = rng.uniform(-1.7, -1.3, n - half)    # home-like fold: shoulder servo vs lower arm
+    q[half:, 2] = rng.uniform(1.3, 1.69, n - half)
     return q.astype(np.float32).astype(np.float64)
 
 
@@ -178,8 +178,9 @@ def test_contacts_match_oracle(gpu_lib, arm_model, cube_model, ccd):
         assert cm.desc.ccd == (1 if ccd == "native" else 0)
         n = 512
         S, orc = make_sim(cm, n), Oracle(cm)
-        q = _contact_poses(cm, n)
-        full = cube_qpos(cm, n, RNG, q) if cm.nq > 6 else q
+        rng = np.random.default_rng(31 + cm.nq)  # (the poses do not depend on which tests ran before)
+        q = _contact_poses(cm, n, rng)
+        full = cube_qpos(cm, n, rng, q) if cm.nq > 6 else q
         full = full.astype(np.float32).astype(np.float64)
         S.qpos.copy_(torch.as_tensor(full.T, dtype=torch.float32, device=S.device))
         out, nc = S.contacts()
@@ -384,9 +385,10 @@ def test_one_substep_domain_randomised(gpu_lib):
     assert to_np(S.ncon).sum() == st["ncon"].sum()
 
 
-# arm qvel max over one full-size env-step (4096 / 8192 envs) against the fp64 oracle (r06, after
-# the MPR normal fix; r05: 5e-2)
-ARM_QVEL_MAX = 2e-3
+# qvel max over one full-size env-step (4096 / 8192 envs) against the fp64 oracle, ~3x the r06
+# measurement after the MPR normal fix (arm 6.7e-5 / 3.1e-4, cube 6.8e-5 / 6.1e-4 at t = 100 / DR
+# t = 40; r05 bars: arm 5e-2, cube 2e-2)
+ARM_QVEL_MAX, CUBE_QVEL_MAX = 1e-3, 2e-3
 
 
 def _within_noise_envelope(dv, env):
@@ -395,6 +397,10 @@ def _within_noise_envelope(dv, env):
     no library code; VERDICT r5 next #1).  1e-6: qvel's fp32 resolution at ~10 rad/s."""
     ratio = dv[:, :6].max(1) / (10 * env[:, :6].max(1) + 1e-6)
     k = int(ratio.argmax())
+    a, c = dv[:, :6].max(1), dv[:, 6:].max(1)
+    print(f"env-step vs oracle: arm qvel p50 {np.median(a):.3g} p99 {np.percentile(a, 99):.3g} max {a.max():.3g}; "
+          f"cube qvel p50 {np.median(c):.3g} p99 {np.percentile(c, 99):.3g} max {c.max():.3g}; "
+          f"envelope ratio max {ratio.max():.3g} (env {k})")
     assert ratio.max() <= 1.0, ("arm qvel vs fp32-noise envelope", ratio.max(), k, dv[k, :6].max(), env[k, :6].max(),
                                 "envs over 1/10 of it", int((ratio > 0.1).sum()))
 
@@ -418,7 +424,7 @@ def test_dr_env_step_full_size(gpu_lib):
     oc = orc.step(st, a.astype(np.float64), params=prm, nthreads=16)
     assert_pct(np.abs(og - oc).max(1), 1e-6, 2e-6, 2e-4, what="obs")
     dv = np.abs(to_np(S.qvel).T - st["qvel"])
-    assert_pct(dv[:, 6:].max(1), 5e-6, 5e-4, 2e-2, what="cube qvel")
+    assert_pct(dv[:, 6:].max(1), 5e-6, 5e-4, CUBE_QVEL_MAX, what="cube qvel")
     assert_pct(dv[:, :6].max(1), 5e-6, 5e-5, ARM_QVEL_MAX, what="arm qvel")
     _within_noise_envelope(dv, env)
     np.testing.assert_allclose(to_np(S.qpos).T[:, 6:9], st["qpos"][:, 6:9], atol=5e-6)
@@ -823,6 +829,40 @@ def test_full_size_shard_invariance_and_determinism(gpu_lib):
     assert float(a["ncon"].sum()) / (n * T * 10) > 3.5
 
 
+def test_shard_invariance_quad_kernel(gpu_lib, monkeypatch):
+    """Config 4's partition (8192 envs per GPU) with the PGS kernel held fixed: the quad kernel
+    (SOARM_RS=0) on 8192 envs as one batch and as two shards of 4096 (global env ids), DR scene,
+    10 env-steps -- bit-identical.  (The default kernel depends on the per-GPU batch: the row-space
+    kernel up to rs_cap = 4096 envs on MI355X, the quad kernel above.  Their fp32 summation orders
+    differ, so a batch split across rs_cap -- 8192 as 2 x 4096 -- agrees with the unsplit one to the
+    parity bars only, not bit for bit)"""
+    import torch
+    from lerobot_mujoco_sim2real_amd import workloads as W
+    from lerobot_mujoco_sim2real_amd.sim import BatchSim
+    monkeypatch.setenv("SOARM_RS", "0")
+    cm = W.model("dr")
+    n, T = 8192, 10
+
+    def run(lo, hi):
+        ids = np.arange(lo, hi)
+        S = BatchSim(cm, hi - lo)
+        q0 = W.initial_qpos(cm, ids, 0)
+        S.reset(init_qpos=q0[:, :5], extra_qpos=q0, seed=0, env_offset=lo)
+        S.set_params(**W.dr_params(ids, 0))
+        tab = {k: (torch.as_tensor(v, dtype=torch.float32, device=S.device) if isinstance(v, np.ndarray) else v)
+               for k, v in W.chirp_tables(ids, 0).items()}
+        for t in range(T):
+            S.step(W.chirp_action(tab, float(t), lib=torch))
+        torch.cuda.synchronize()
+        return {"obs": S.obs.clone(), "qpos": S.qpos.clone(), "qvel": S.qvel.clone()}
+
+    a = run(0, n)
+    h0, h1 = run(0, n // 2), run(n // 2, n)
+    assert torch.equal(a["obs"], torch.cat([h0["obs"], h1["obs"]]))
+    for k in ("qpos", "qvel"):
+        assert torch.equal(a[k], torch.cat([h0[k], h1[k]], 1)), k
+
+
 def test_separating_axis_cache_is_exact(gpu_lib):
     """k_collide's separating-axis cache (soarm_collide.h SepCache) only lets a pair skip an MPR
     run whose answer would be "apart": a batch whose cache was warmed over 80 env-steps of the
@@ -876,7 +916,7 @@ def test_contact_env_step_late_states_full_size(gpu_lib):
     # over 10 substeps an env whose arm pushes the cube can see fp32 / fp64 PGS stop a sweep apart
     # in several substeps (r03 on 4096 envs at t = 100: cube qvel p50 5e-7, p99 4.2e-5, max 2.3e-3)
     dv = np.abs(to_np(S.qvel).T - st["qvel"])
-    assert_pct(dv[:, 6:].max(1), 5e-6, 5e-4, 2e-2, what="cube qvel")
+    assert_pct(dv[:, 6:].max(1), 5e-6, 5e-4, CUBE_QVEL_MAX, what="cube qvel")
     # the arm's: r03-r05 one env of 4096 (2624) at 3.2e-2 -- a grazing arm-link contact on the table
     # whose fp32 MPR normal tilted by up to 5 degrees; fixed in r06 (soarm_collide.h mpr: the final
     # depth and normal in fp64; tools/env_diverge.py)

@@ -41,6 +41,8 @@ def main():
     p.add_argument("--lazy", action="store_true", help="nccl group without device_id (communicator made at first use)")
     p.add_argument("--pin", action="store_true", help="pin this (launching) thread to its first allowed core")
     p.add_argument("--phases", default="none,gloo,nccl,nccl_used,destroyed")
+    p.add_argument("--pg-first", action="store_true",
+                   help="init the nccl group (eager, device_id) before the sim and its tensors exist, as bench.py does")
     a = p.parse_args()
     import numpy as np
     import torch
@@ -55,6 +57,12 @@ def main():
         os.sched_setaffinity(0, {cores[0]})
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(0)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 1000))
+    os.environ.setdefault("RANK", "0")
+    os.environ.setdefault("WORLD_SIZE", "1")
+    if a.pg_first:
+        dist.init_process_group("nccl", init_method="env://", device_id=dev)
     cfg = W.CONFIGS[a.config]
     n = cfg.get("envs", 4096)
     ids = np.arange(n)
@@ -82,14 +90,12 @@ def main():
     for _ in range(10):
         step()
     torch.cuda.synchronize()
-    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 1000))
-    os.environ.setdefault("RANK", "0")
-    os.environ.setdefault("WORLD_SIZE", "1")
     res = {"config": a.config, "lazy": a.lazy, "pin": a.pin, "phases": {}}
     for ph in a.phases.split(","):
         if ph == "gloo":
             dist.init_process_group("gloo", init_method="env://")
+        elif ph == "nccl" and a.pg_first:
+            pass
         elif ph == "nccl":
             if dist.is_initialized():
                 dist.destroy_process_group()
