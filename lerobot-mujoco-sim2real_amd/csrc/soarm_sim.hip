@@ -209,7 +209,12 @@ __global__ __launch_bounds__(SOARM_COLLIDE_BLOCK, SOARM_COLLIDE_WAVES) void k_co
 // the collide launch: (env, pair) lanes, SOARM_COLLIDE_BLOCK-env blocks x npair
 static void launch_collide(const sim_batch* b, hipStream_t q, unsigned long long* pcyc) {
   auto kern = b->model->desc.ccd == SIM_CCD_NATIVE ? k_collide<SIM_CCD_NATIVE> : k_collide<SIM_CCD_MPR>;
-  hipLaunchKernelGGL(kern, dim3((b->n + SOARM_COLLIDE_BLOCK - 1) / SOARM_COLLIDE_BLOCK, b->model->desc.npair),
+  int rows = b->model->desc.npair;
+#ifdef SOARM_DIAG_SKIPP
+  // (diagnostic: SOARM_DIAG_ROWS=k launches only the first k rows of the dispatch order -- timings only)
+  if (const char* v = getenv("SOARM_DIAG_ROWS")) rows = std::min(rows, std::max(1, atoi(v)));
+#endif
+  hipLaunchKernelGGL(kern, dim3((b->n + SOARM_COLLIDE_BLOCK - 1) / SOARM_COLLIDE_BLOCK, rows),
                      dim3(SOARM_COLLIDE_BLOCK), 0, q, b->d_model, b->n,
                      b->d_gpose, b->d_cbuf, b->d_ccount, b->d_pmask, b->d_sepax, pcyc);
 }
