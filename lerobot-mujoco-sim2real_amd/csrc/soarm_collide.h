@@ -757,11 +757,35 @@ HDI void epa_face(EpaFace& f, const float (*V)[6], int a, int b, int c) {
   f.abc = (uint32_t)a | ((uint32_t)b << 8) | ((uint32_t)c << 16);
   f.d = dot3(f.n, V[a]);
 }
-// EPA from the enclosing tetrahedron p: 1 with depth / dir / pos
-HDI int epa(const MPair& P, const MSup p[4], float& depth, float dir[3], float pos[3]) {
+// the polytope of one EPA run (2.1 KB)
+struct EpaPoly {
   float V[EPA_KV][6];  // v (3), geom1 support point (3)
   EpaFace F[EPA_KF];
   uint8_t E[EPA_KE][2];
+};
+// k_collide<native>'s per-workgroup LDS slots for EPA polytopes (null on the host): an EPA run takes
+// the next free slot and keeps its polytope in LDS instead of private (scratch) memory, whose every
+// access is a round trip to the memory hierarchy; runs beyond the slots use private memory
+struct EpaPool {
+  EpaPoly* slot;
+  int* used;
+  int nslot;
+};
+// EPA from the enclosing tetrahedron p: 1 with depth / dir / pos
+HDI int epa(const MPair& P, const MSup p[4], float& depth, float dir[3], float pos[3], const EpaPool* pool = nullptr) {
+  EpaPoly own;
+  EpaPoly* Q = &own;
+#if SOARM_DEVICE_PASS
+  if (pool) {
+    const int k = atomicAdd(pool->used, 1);
+    if (k < pool->nslot) Q = pool->slot + k;
+  }
+#else
+  (void)pool;
+#endif
+  float (*V)[6] = Q->V;
+  EpaFace* F = Q->F;
+  uint8_t (*E)[2] = Q->E;
 #pragma unroll
   for (int k = 0; k < 4; k++) copy3(V[k], p[k].v), copy3(V[k] + 3, p[k].v1);
   int nv = 4, nf = 0;
@@ -848,10 +872,10 @@ HDI int epa(const MPair& P, const MSup p[4], float& depth, float dir[3], float p
   depth = f.d;
   return f.d > 0.f;
 }
-HDI int ccd_native(const MPair& P, float& depth, float dir[3], float pos[3], float sep[3]) {
+HDI int ccd_native(const MPair& P, float& depth, float dir[3], float pos[3], float sep[3], const EpaPool* pool = nullptr) {
   MSup p[4];
   if (!gjk_enclose(P, p, sep)) return 0;
-  return epa(P, p, depth, dir, pos);
+  return epa(P, p, depth, dir, pos, pool);
 }
 
 // ------------------------------------------------------------- primitives
@@ -1306,7 +1330,7 @@ HDI bool cached_apart(const DModel& m, int p, int g1, int g2, const GeomPose& P1
 // convex-convex narrowphase fixed at compile time (SIM_CCD_*), or -1 to read it from the model
 template <int CCD = -1>
 HDI void narrowphase(const DModel& m, int p, const GeomPose& P1, const GeomPose& P2, PairOut& o,
-                      const SepCache& sc) {
+                      const SepCache& sc, const EpaPool* pool = nullptr) {
   o.n = 0;
   o.xc = 6;
   const int g1 = m.pair_geom1[p], g2 = m.pair_geom2[p];
@@ -1385,7 +1409,7 @@ HDI void narrowphase(const DModel& m, int p, const GeomPose& P1, const GeomPose&
   MPair mp{m, g1, g2, P1, P2};
   float depth, dir[3], pos[3], sep[3] = {0.f, 0.f, 0.f};
   const bool native = CCD < 0 ? m.ccd == SIM_CCD_NATIVE : CCD == SIM_CCD_NATIVE;
-  if (native ? ccd_native(mp, depth, dir, pos, sep) : mpr(mp, depth, dir, pos, sep)) {
+  if (native ? ccd_native(mp, depth, dir, pos, sep, pool) : mpr(mp, depth, dir, pos, sep)) {
     emit(o, -depth, pos, dir);
     o.xc = 5;
   } else {
@@ -1400,9 +1424,9 @@ namespace soarm {
 // midphase + narrowphase of candidate pair p of env e (geom records in gpose)
 template <int CCD = -1>
 HDI void collide_pair(const DModel& m, int p, const float* __restrict__ gpose, int n, int e, PairOut& o,
-                       const SepCache& sc = SepCache{nullptr, 0, 0}) {
+                       const SepCache& sc = SepCache{nullptr, 0, 0}, const EpaPool* pool = nullptr) {
   o.n = 0;
   GeomPose P1, P2;
-  if (midphase(m, p, gpose, n, e, P1, P2)) narrowphase<CCD>(m, p, P1, P2, o, sc);
+  if (midphase(m, p, gpose, n, e, P1, P2)) narrowphase<CCD>(m, p, P1, P2, o, sc, pool);
 }
 }  // namespace soarm

@@ -157,6 +157,9 @@ struct sim_batch {
 #ifndef SOARM_COLLIDE_BLOCK
 #define SOARM_COLLIDE_BLOCK 256  // envs (lanes) per collide workgroup
 #endif
+#ifndef SOARM_EPA_SLOTS
+#define SOARM_EPA_SLOTS 8  // EPA polytopes per native-collide workgroup in LDS (2.1 KB each)
+#endif
 #ifndef SOARM_COLLIDE_WAVES
 #define SOARM_COLLIDE_WAVES 3  // min waves per SIMD (VGPR cap 512 / 3 = 168)
 #endif
@@ -175,6 +178,15 @@ __global__ __launch_bounds__(SOARM_COLLIDE_BLOCK, SOARM_COLLIDE_WAVES) void k_co
                                                  unsigned long long* __restrict__ pcyc) {
   // (env chunks numbered per XCD as in k_geom / k_substep: the geom records this reads and the
   // contact buffer it writes stay in the L2 of the XCD whose substep waves own those envs)
+  // native: LDS slots for the EPA polytopes of this workgroup's penetrating lanes (EpaPool)
+  constexpr int NSLOT = CCD == SIM_CCD_NATIVE ? SOARM_EPA_SLOTS : 0;
+  __shared__ EpaPoly s_epa[NSLOT > 0 ? NSLOT : 1];
+  __shared__ int s_epa_used;
+  if constexpr (NSLOT > 0) {
+    if (threadIdx.x == 0) s_epa_used = 0;
+    __syncthreads();
+  }
+  const EpaPool pool{s_epa, &s_epa_used, NSLOT};
   const int e = xcd_block() * blockDim.x + threadIdx.x;
   const int p = m_pair_order(dm, blockIdx.y);  // (DModel::pair_order: the heavy pairs dispatch first)
   if (e >= n) return;
@@ -184,7 +196,7 @@ __global__ __launch_bounds__(SOARM_COLLIDE_BLOCK, SOARM_COLLIDE_WAVES) void k_co
   const long long t0 = pcyc ? clock64() : 0;
   const DModel& m = *dm;
   PairOut o{cbuf, n, e, m.pair_slot[p], m.pair_cap[p], 0};
-  collide_pair<CCD>(m, p, gpose, n, e, o, SepCache{sepax, n, e});
+  collide_pair<CCD>(m, p, gpose, n, e, o, SepCache{sepax, n, e}, NSLOT > 0 ? &pool : nullptr);
   // (no per-pair count is stored: the pair mask bit and, for multi-contact pairs, its 2-bit
   // count word carry it -- an empty pair costs no store)
   (void)ccount;

@@ -19,7 +19,7 @@ tag = sys.argv[1]
 T = int(sys.argv[2]) if len(sys.argv) > 2 else 120
 solver = sys.argv[3] if len(sys.argv) > 3 else "PGS"
 n = 4096
-cm = W.model("contact", solver=solver)
+cm = W.model("contact", solver=solver, ccd=os.environ.get("CCD", W.BENCH_CCD))
 ids = np.arange(n)
 sim = BatchSim(cm, n, 0)
 q0 = W.initial_qpos(cm, ids, 0)
