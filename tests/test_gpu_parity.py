@@ -863,6 +863,48 @@ def test_shard_invariance_quad_kernel(gpu_lib, monkeypatch):
         assert torch.equal(a[k], torch.cat([h0[k], h1[k]], 1)), k
 
 
+def test_rs_choice_switches_on_a_live_batch(gpu_lib, monkeypatch):
+    """SOARM_RS is read per env-step call and is part of the step graph's cache key: a
+    batch whose graph was captured with the row-space kernel runs the quad kernel once SOARM_RS=0 --
+    bit-identical to a fresh batch stepped with the quad kernel from the same state, and not to the
+    row-space step (the two kernels' fp32 summation orders differ)."""
+    import torch
+    from lerobot_mujoco_sim2real_amd import workloads as W
+    from lerobot_mujoco_sim2real_amd.sim import BatchSim
+    cm = W.model("contact")
+    n = 1024
+    ids = np.arange(n)
+    q0 = W.initial_qpos(cm, ids, 0)
+    tab = W.chirp_tables(ids, 0)
+
+    def fresh():
+        S = BatchSim(cm, n)
+        S.reset(init_qpos=q0[:, :5], extra_qpos=q0, seed=0)
+        return S
+
+    def copy(dst, src):
+        for k in ("qpos", "qvel", "qacc_warmstart", "ctrl", "status"):
+            getattr(dst, k).copy_(getattr(src, k))
+
+    a0, a1 = (torch.as_tensor(W.chirp_action(tab, t), dtype=torch.float32) for t in (0, 1))
+    monkeypatch.setenv("SOARM_RS", "1")
+    A = fresh()
+    for _ in range(3):
+        A.step(a0.to(A.device))
+    B = fresh()
+    copy(B, A)
+    D = fresh()
+    copy(D, A)
+    monkeypatch.setenv("SOARM_RS", "0")
+    A.step(a1.to(A.device))  # (its cached graph was captured with the RS kernel)
+    B.step(a1.to(B.device))
+    monkeypatch.setenv("SOARM_RS", "1")
+    D.step(a1.to(D.device))
+    torch.cuda.synchronize()
+    assert torch.equal(A.qvel, B.qvel) and torch.equal(A.qpos, B.qpos)
+    assert not torch.equal(A.qvel, D.qvel)
+
+
 def test_separating_axis_cache_is_exact(gpu_lib):
     """k_collide's separating-axis cache (soarm_collide.h SepCache) only lets a pair skip an MPR
     run whose answer would be "apart": a batch whose cache was warmed over 80 env-steps of the
