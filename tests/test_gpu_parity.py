@@ -863,6 +863,43 @@ def test_shard_invariance_quad_kernel(gpu_lib, monkeypatch):
         assert torch.equal(a[k], torch.cat([h0[k], h1[k]], 1)), k
 
 
+def test_whole_node_batch_on_one_gpu(gpu_lib):
+    """The largest size BASELINE.json names -- config 4's 65536 envs, the whole node's count -- as ONE
+    batch on one GPU (the [row][env] offsets, the contact buffer and the scratch slab at their largest):
+    3 DR env-steps finite, no soft reset, the cube's resting contacts present, and bit-identical to
+    the same envs as two batches of 32768 (global env ids; both above rs_cap: the quad kernel)."""
+    import torch
+    from lerobot_mujoco_sim2real_amd import workloads as W
+    from lerobot_mujoco_sim2real_amd.sim import BatchSim
+    cm = W.model("dr")
+    n, T = 65536, 3
+
+    def run(lo, hi):
+        ids = np.arange(lo, hi)
+        S = BatchSim(cm, hi - lo)
+        q0 = W.initial_qpos(cm, ids, 0)
+        S.reset(init_qpos=q0[:, :5], extra_qpos=q0, seed=0, env_offset=lo)
+        S.set_params(**W.dr_params(ids, 0))
+        tab = {k: (torch.as_tensor(v, dtype=torch.float32, device=S.device) if isinstance(v, np.ndarray) else v)
+               for k, v in W.chirp_tables(ids, 0).items()}
+        for t in range(T):
+            S.step(W.chirp_action(tab, float(t), lib=torch))
+        torch.cuda.synchronize()
+        out = {"obs": S.obs.clone(), "qpos": S.qpos.clone(), "qvel": S.qvel.clone(), "status": S.status.clone(),
+               "ncon": S.ncon.clone()}
+        S.close()
+        return out
+
+    a = run(0, n)
+    assert bool(torch.isfinite(a["qpos"]).all()) and bool(torch.isfinite(a["qvel"]).all())
+    assert int((a["status"] != 0).sum()) == 0
+    assert float(a["ncon"].sum()) / (n * T * 10) > 3.5
+    h0, h1 = run(0, n // 2), run(n // 2, n)
+    assert torch.equal(a["obs"], torch.cat([h0["obs"], h1["obs"]]))
+    for k in ("qpos", "qvel"):
+        assert torch.equal(a[k], torch.cat([h0[k], h1[k]], 1)), k
+
+
 def test_rs_choice_switches_on_a_live_batch(gpu_lib, monkeypatch):
     """SOARM_RS is read per env-step call and is part of the step graph's cache key: a
     batch whose graph was captured with the row-space kernel runs the quad kernel once SOARM_RS=0 --
