@@ -974,23 +974,24 @@ def test_separating_axis_cache_is_exact(gpu_lib):
         assert torch.equal(getattr(A, k), getattr(B, k)), k
 
 
-def test_contact_env_step_late_states_full_size(gpu_lib):
+@pytest.mark.parametrize("t0", [20, 60, 100])
+def test_contact_env_step_late_states_full_size(gpu_lib, t0):
     """The graph-captured 10-substep contact sim_step (the headline's launch sequence) against one
-    oracle env-step, from late bench states (t = 100: the cube resting, arm-table and arm-cube
-    contacts in some envs) at the headline's 4096 envs.  Bars ~10x the measured fp32 / fp64 spread
+    oracle env-step, from bench states at t0 = 20 (the driver's window), 60 and 100 (the cube
+    resting, arm-table and arm-cube contacts in some envs) at the headline's 4096 envs.  Bars ~10x the measured fp32 / fp64 spread
     (profiles/r03_newton_gap.json env_step pgs_device_vs_pgs_fp64: obs p50 6e-8, p99 1.3e-7, max
     1.2e-5; cube qvel p50 5e-7, p99 4e-5, max 1.4e-4)."""
     from lerobot_mujoco_sim2real_amd import workloads as W
     n = 4096
-    cm, orc, st, _ = _bench_states("contact", n, 100, nthreads=16)
-    a = W.chirp_action(W.chirp_tables(np.arange(n)), 100).astype(np.float32)
+    cm, orc, st, _ = _bench_states("contact", n, t0, nthreads=16)
+    a = W.chirp_action(W.chirp_tables(np.arange(n)), t0).astype(np.float32)
     S = make_sim(cm, n)
     st["ncon"][:] = 0
     load_state(S, st)
     og = to_np(S.step(a))  # graph replay of geom + 10 x (collide, substep)
     env = fp32_noise_envelope(orc, st, a.astype(np.float64), nthreads=16)
     oc = orc.step(st, a.astype(np.float64), nthreads=16)
-    assert st["ncon"].sum() > 4 * 10 * n, "no arm contacts in the sample"
+    assert st["ncon"].sum() > (4 * 10 * n if t0 >= 60 else 3.5 * 10 * n), "contacts in the sample"
     assert_pct(np.abs(og - oc).max(1), 1e-6, 2e-6, 2e-4, what="obs")
     # over 10 substeps an env whose arm pushes the cube can see fp32 / fp64 PGS stop a sweep apart
     # in several substeps (r03 on 4096 envs at t = 100: cube qvel p50 5e-7, p99 4.2e-5, max 2.3e-3)
