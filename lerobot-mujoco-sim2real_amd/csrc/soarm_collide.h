@@ -800,9 +800,14 @@ HDI int epa(const MPair& P, const MSup p[4], float& depth, float dir[3], float p
   int best = 0;
   float upper = 3.0e38f;
   for (int it = 0; it < CCD_ITERS; it++) {
+    // (the running minimum in a register: the loads of F[i].d are independent and pipeline, where
+    // re-reading F[best].d made every step wait for the previous one)
     best = 0;
-    for (int i = 1; i < nf; i++)
-      if (F[i].d < F[best].d) best = i;
+    float bd = F[0].d;
+    for (int i = 1; i < nf; i++) {
+      const float di = F[i].d;
+      if (di < bd) bd = di, best = i;
+    }
     MSup w;
     P.sup(F[best].n, w);
     upper = fminf(upper, dot3(F[best].n, w.v));
@@ -849,8 +854,11 @@ HDI int epa(const MPair& P, const MSup p[4], float& depth, float dir[3], float p
   }
   if (best < 0) {  // (a horizon pass compacted the faces: find the closest again)
     best = 0;
-    for (int i = 1; i < nf; i++)
-      if (F[i].d < F[best].d) best = i;
+    float bd = F[0].d;
+    for (int i = 1; i < nf; i++) {
+      const float di = F[i].d;
+      if (di < bd) bd = di, best = i;
+    }
   }
   const EpaFace f = F[best];
   const int a = f.abc & 255, b = (f.abc >> 8) & 255, c = (f.abc >> 16) & 255;
