@@ -168,6 +168,7 @@ struct sim_batch {
 __device__ __forceinline__ int m_pair_order(const DModel* dm, int y) { return dm->pair_order[y]; }
 #ifdef SOARM_DIAG_SKIPP
 __device__ uint32_t g_diag_skip[4];
+__device__ int g_diag_stage;  // (SOARM_DIAG_STAGE: 1 midphase only, 2 no mask atomics, else everything)
 #endif
 template <int CCD>
 __global__ __launch_bounds__(SOARM_COLLIDE_BLOCK, SOARM_COLLIDE_WAVES) void k_collide(const DModel* __restrict__ dm, int n,
@@ -196,7 +197,17 @@ __global__ __launch_bounds__(SOARM_COLLIDE_BLOCK, SOARM_COLLIDE_WAVES) void k_co
   const long long t0 = pcyc ? clock64() : 0;
   const DModel& m = *dm;
   PairOut o{cbuf, n, e, m.pair_slot[p], m.pair_cap[p], 0};
+#ifdef SOARM_DIAG_SKIPP
+  if (g_diag_stage == 1) {
+    GeomPose P1, P2;
+    if (midphase(m, p, gpose, n, e, P1, P2)) soa(cbuf, 0, n, e) = P1.p[0] + P2.p[0];
+    return;
+  }
+#endif
   collide_pair<CCD>(m, p, gpose, n, e, o, SepCache{sepax, n, e}, NSLOT > 0 ? &pool : nullptr);
+#ifdef SOARM_DIAG_SKIPP
+  if (g_diag_stage == 2) return;
+#endif
   // (no per-pair count is stored: the pair mask bit and, for multi-contact pairs, its 2-bit
   // count word carry it -- an empty pair costs no store)
   (void)ccount;
@@ -936,6 +947,8 @@ int sim_batch_create(const sim_model* m, int n_envs, int device, sim_batch** out
         for (auto& x : w) x = ~x;
     }
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_diag_skip), w, sizeof(w), 0, hipMemcpyHostToDevice);
+    const int stage = getenv("SOARM_DIAG_STAGE") ? atoi(getenv("SOARM_DIAG_STAGE")) : 0;
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_diag_stage), &stage, sizeof(stage), 0, hipMemcpyHostToDevice);
   }
 #endif
   }
