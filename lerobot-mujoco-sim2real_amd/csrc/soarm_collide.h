@@ -88,8 +88,27 @@ HDI uint4 ldg(gptr<uint4> p, int i) {  // (dword loads, merged into one 16-B loa
   const gptr<uint32_t> q = (gptr<uint32_t>)(p + i);
   return make_uint4(q[0], q[1], q[2], q[3]);
 }
+#if defined(SOARM_DIAG_SUPPORT) && SOARM_DEVICE_PASS
+// (diagnostic build: per geom, support queries, queries whose cube-map cell / answer repeats the
+// lane's previous query on that geom, and climbing round trips)
+// (g_diag_sup, g_diag_prev: soarm_sim.hip)
+DEVI void diag_support(int g, int cell, uint4 r0, int steps) {
+  const int t = (blockIdx.y * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= 128 * 8192) return;
+  const uint32_t key = ((uint32_t)g << 20) | (uint32_t)cell, ans = r0.x ^ (r0.y * 3u) ^ (r0.z * 7u);
+  atomicAdd(&g_diag_sup[g][0], 1ull);
+  if (g_diag_prev[0][t] == key) atomicAdd(&g_diag_sup[g][1], 1ull);
+  if (g_diag_prev[1][t] == ans && (g_diag_prev[0][t] >> 20) == (uint32_t)g) atomicAdd(&g_diag_sup[g][2], 1ull);
+  atomicAdd(&g_diag_sup[g][3], (unsigned long long)steps);
+  g_diag_prev[0][t] = key, g_diag_prev[1][t] = ans;
+}
+#endif
 HDI float3 hull_support(const DModel& m, int g, const float l[3]) {
   const gptr<uint4> rec = (gptr<uint4>)m.hull_rec + 2 * m.geom_hulladr[g];
+#if defined(SOARM_DIAG_SUPPORT) && SOARM_DEVICE_PASS
+  const int dcell = lut_cell(l[0], l[1], l[2]);
+  int dsteps = 0;
+#endif
   const gptr<uint4> lr = (gptr<uint4>)m.hull_lutrec + HULL_LUTREC * (m.geom_lutadr[g] + lut_cell(l[0], l[1], l[2]));
   uint4 r0 = ldg(lr, 0), r1 = ldg(lr, 1), nb[8];
 #pragma unroll
@@ -107,14 +126,25 @@ HDI float3 hull_support(const DModel& m, int g, const float l[3]) {
       const float s = dotr(nb[k]);
       if (s > nd) nd = s, best = k;
     }
-    if (best < 0) return make_float3(fbits(r0.x), fbits(r0.y), fbits(r0.z));
+    if (best < 0) {
+#if defined(SOARM_DIAG_SUPPORT) && SOARM_DEVICE_PASS
+      diag_support(g, dcell, r0, 0);
+#endif
+      return make_float3(fbits(r0.x), fbits(r0.y), fbits(r0.z));
+    }
     uint32_t u = 0;
 #pragma unroll
     for (int k = 0; k < 8; k++)
       if (k == best) u = nb[k].w;
     r0 = ldg(rec, 2 * u), r1 = ldg(rec, 2 * u + 1), cd = nd;
+#if defined(SOARM_DIAG_SUPPORT) && SOARM_DEVICE_PASS
+    dsteps++;
+#endif
   }
   for (int guard = 0; guard < nvert; guard++) {
+#if defined(SOARM_DIAG_SUPPORT) && SOARM_DEVICE_PASS
+    dsteps++;
+#endif
     const uint32_t ids[4] = {r1.x, r1.y, r1.z, r1.w};
     uint4 c0[8], c1[8];
 #pragma unroll
@@ -152,6 +182,9 @@ HDI float3 hull_support(const DModel& m, int g, const float l[3]) {
     if (best < 0) break;
     r0 = b0, r1 = b1, cd = nd;
   }
+#if defined(SOARM_DIAG_SUPPORT) && SOARM_DEVICE_PASS
+  diag_support(g, dcell, r0, dsteps);
+#endif
   return make_float3(fbits(r0.x), fbits(r0.y), fbits(r0.z));
 }
 
@@ -744,23 +777,26 @@ HDI bool gjk_enclose(const MPair& P, MSup q[4], float sep[3]) {
       q[k].v[c] = (float)p[k].v[c], q[k].v1[c] = p[k].v1[c], q[k].v2[c] = p[k].v1[c] - q[k].v[c];
   return true;
 }
-struct EpaFace {
-  uint32_t abc;  // vertex ids, 8 bits each
+// a face of the EPA polytope: unit outward normal and plane offset (one 16-byte load)
+struct alignas(16) EpaPlane {
   float n[3], d;
 };
-HDI void epa_face(EpaFace& f, const float (*V)[6], int a, int b, int c) {
+HDI EpaPlane epa_plane(const float (*V)[6], int a, int b, int c) {
+  EpaPlane f;
   float ab[3], ac[3];
   sub(ab, V[b], V[a]);
   sub(ac, V[c], V[a]);
   cross(f.n, ab, ac);
   nrm(f.n);
-  f.abc = (uint32_t)a | ((uint32_t)b << 8) | ((uint32_t)c << 16);
   f.d = dot3(f.n, V[a]);
+  return f;
 }
-// the polytope of one EPA run (2.1 KB)
+HDI uint32_t epa_abc(int a, int b, int c) { return (uint32_t)a | ((uint32_t)b << 8) | ((uint32_t)c << 16); }
+// the polytope of one EPA run (2.1 KB): faces as planes F and vertex ids A (8 bits each)
 struct EpaPoly {
   float V[EPA_KV][6];  // v (3), geom1 support point (3)
-  EpaFace F[EPA_KF];
+  EpaPlane F[EPA_KF];
+  uint32_t A[EPA_KF];
   uint8_t E[EPA_KE][2];
 };
 // k_collide<native>'s per-workgroup LDS slots for EPA polytopes (null on the host): an EPA run takes
@@ -771,7 +807,12 @@ struct EpaPool {
   int* used;
   int nslot;
 };
-// EPA from the enclosing tetrahedron p: 1 with depth / dir / pos
+// EPA from the enclosing tetrahedron p: 1 with depth / dir / pos.  Per expansion: the faces w sees
+// as a bit mask from one pass of independent loads (unrolled, so the face / vertex loads of
+// several faces are in flight together -- a face-by-face walk waited on two dependent LDS loads
+// per face), the horizon from the seen faces in face order, then compaction with the running
+// minimum, so the next closest face needs no scan of its own (same faces, same order and the same
+// first-minimum rule as a scan: bit-identical)
 HDI int epa(const MPair& P, const MSup p[4], float& depth, float dir[3], float pos[3], const EpaPool* pool = nullptr) {
   EpaPoly own;
   EpaPoly* Q = &own;
@@ -784,53 +825,54 @@ HDI int epa(const MPair& P, const MSup p[4], float& depth, float dir[3], float p
   (void)pool;
 #endif
   float (*V)[6] = Q->V;
-  EpaFace* F = Q->F;
+  EpaPlane* F = Q->F;
+  uint32_t* A = Q->A;
   uint8_t (*E)[2] = Q->E;
 #pragma unroll
   for (int k = 0; k < 4; k++) copy3(V[k], p[k].v), copy3(V[k] + 3, p[k].v1);
-  int nv = 4, nf = 0;
+  int nv = 4, nf = 0, best = 0;
+  float bd = 0.f;
 #pragma unroll
   for (int k = 0; k < 4; k++) {
-    epa_face(F[nf], V, TETF[k][0], TETF[k][1], TETF[k][2]);
+    int a = TETF[k][0], b = TETF[k][1], c = TETF[k][2];
+    EpaPlane f = epa_plane(V, a, b, c);
     float ak[3];
-    sub(ak, p[k].v, V[TETF[k][0]]);
-    if (dot3(F[nf].n, ak) > 0.f) epa_face(F[nf], V, TETF[k][0], TETF[k][2], TETF[k][1]);
+    sub(ak, p[k].v, V[a]);
+    if (dot3(f.n, ak) > 0.f) f = epa_plane(V, a, c, b), b = TETF[k][2], c = TETF[k][1];
+    F[nf] = f, A[nf] = epa_abc(a, b, c);
+    if (k == 0 || f.d < bd) bd = f.d, best = nf;
     nf++;
   }
-  int best = 0;
   float upper = 3.0e38f;
   for (int it = 0; it < CCD_ITERS; it++) {
-    // (the running minimum in a register: the loads of F[i].d are independent and pipeline, where
-    // re-reading F[best].d made every step wait for the previous one)
-    best = 0;
-    float bd = F[0].d;
-    for (int i = 1; i < nf; i++) {
-      const float di = F[i].d;
-      if (di < bd) bd = di, best = i;
-    }
+    const EpaPlane fb = F[best];
     MSup w;
-    P.sup(F[best].n, w);
-    upper = fminf(upper, dot3(F[best].n, w.v));
-    if (upper - F[best].d < MPR_TOLF || nv == EPA_KV) break;
+    P.sup(fb.n, w);
+    upper = fminf(upper, dot3(fb.n, w.v));
+    if (upper - fb.d < MPR_TOLF || nv == EPA_KV) break;
     // faces seen from w go; the edges they do not share bound the hole (the horizon).  The
     // polytope is left untouched until the expansion is known to fit (a budget exit keeps it and
     // its closest face intact).
     uint64_t vis = 0ull;
-    int ne = 0, nvis = 0;
-    bool full = false;
+#pragma unroll 8
     for (int i = 0; i < nf; i++) {
-      const int a = F[i].abc & 255, b = (F[i].abc >> 8) & 255, c = (F[i].abc >> 16) & 255;
+      const EpaPlane f = F[i];
       float aw[3];
-      sub(aw, w.v, V[a]);
-      if (dot3(F[i].n, aw) <= EPA_VIS) continue;  // (w on a face's plane does not see it)
-      vis |= 1ull << i;
-      nvis++;
+      sub(aw, w.v, V[A[i] & 255]);
+      if (dot3(f.n, aw) > EPA_VIS) vis |= 1ull << i;  // (w on a face's plane does not see it)
+    }
+    const int nvis = __builtin_popcountll(vis);
+    int ne = 0;
+    bool full = false;
+    for (uint64_t r = vis; r; r &= r - 1) {
+      const uint32_t abc = A[__builtin_ctzll(r)];
+      const int a = abc & 255, b = (abc >> 8) & 255, c = (abc >> 16) & 255;
       const int ed[3][2] = {{a, b}, {b, c}, {c, a}};
 #pragma unroll
       for (int q = 0; q < 3; q++) {
         int dup = -1;
-        for (int r = 0; r < ne; r++)
-          if (E[r][0] == ed[q][1] && E[r][1] == ed[q][0]) dup = r;
+        for (int k = 0; k < ne; k++)
+          if (E[k][0] == ed[q][1] && E[k][1] == ed[q][0]) dup = k;
         if (dup >= 0) {
           E[dup][0] = E[ne - 1][0], E[dup][1] = E[ne - 1][1];
           ne--;
@@ -844,24 +886,27 @@ HDI int epa(const MPair& P, const MSup p[4], float& depth, float dir[3], float p
     }
     if (ne == 0 || full || nf - nvis + ne > EPA_KF) break;  // (budget exhausted: the best face so far)
     int m = 0;
-    for (int i = 0; i < nf; i++)
-      if (!((vis >> i) & 1ull)) F[m++] = F[i];
+    best = -1;
+    for (int i = 0; i < nf; i++) {
+      if ((vis >> i) & 1ull) continue;
+      const EpaPlane f = F[i];
+      if (m != i) F[m] = f, A[m] = A[i];
+      if (best < 0 || f.d < bd) bd = f.d, best = m;
+      m++;
+    }
     nf = m;
     copy3(V[nv], w.v), copy3(V[nv] + 3, w.v1);
-    for (int r = 0; r < ne; r++) epa_face(F[nf++], V, E[r][0], E[r][1], nv);
-    nv++;
-    best = -1;
-  }
-  if (best < 0) {  // (a horizon pass compacted the faces: find the closest again)
-    best = 0;
-    float bd = F[0].d;
-    for (int i = 1; i < nf; i++) {
-      const float di = F[i].d;
-      if (di < bd) bd = di, best = i;
+    for (int r = 0; r < ne; r++) {
+      const EpaPlane f = epa_plane(V, E[r][0], E[r][1], nv);
+      F[nf] = f, A[nf] = epa_abc(E[r][0], E[r][1], nv);
+      if (best < 0 || f.d < bd) bd = f.d, best = nf;
+      nf++;
     }
+    nv++;
   }
-  const EpaFace f = F[best];
-  const int a = f.abc & 255, b = (f.abc >> 8) & 255, c = (f.abc >> 16) & 255;
+  const EpaPlane f = F[best];
+  const uint32_t abc = A[best];
+  const int a = abc & 255, b = (abc >> 8) & 255, c = (abc >> 16) & 255;
   const float pr[3] = {f.d * f.n[0], f.d * f.n[1], f.d * f.n[2]};
   float v0[3], v1[3], v2[3];
   sub(v0, V[b], V[a]);
@@ -883,6 +928,9 @@ HDI int epa(const MPair& P, const MSup p[4], float& depth, float dir[3], float p
 HDI int ccd_native(const MPair& P, float& depth, float dir[3], float pos[3], float sep[3], const EpaPool* pool = nullptr) {
   MSup p[4];
   if (!gjk_enclose(P, p, sep)) return 0;
+#if defined(SOARM_DIAG_NO_EPA) && SOARM_DEVICE_PASS
+  if (SOARM_DIAG_NO_EPA) return 0;  // (diagnostic build: GJK's cost alone)
+#endif
   return epa(P, p, depth, dir, pos, pool);
 }
 

@@ -21,6 +21,17 @@
 #include <vector>
 
 #include "../../include/soarm_sim.h"
+#ifdef SOARM_DIAG_SKIPP
+// (diagnostic build: SOARM_DIAG_SKIP names pairs k_collide returns from at once; SOARM_DIAG_STAGE:
+// 1 midphase only, 2 no mask atomics, 3 native GJK without EPA, else everything)
+__device__ uint32_t g_diag_skip[4];
+__device__ int g_diag_stage;
+#define SOARM_DIAG_NO_EPA (g_diag_stage == 3)
+#endif
+#ifdef SOARM_DIAG_SUPPORT
+__device__ unsigned long long g_diag_sup[16][4];  // (soarm_collide.h diag_support)
+__device__ uint32_t g_diag_prev[2][128 * 8192];
+#endif
 #include "soarm_collide.h"
 #include "soarm_env.h"
 #include "sim_internal.h"
@@ -166,10 +177,6 @@ struct sim_batch {
 // CCD: one instantiation per narrowphase, so the MPR kernel carries none of EPA's private-memory
 // polytope (2.2 KB of scratch per lane)
 __device__ __forceinline__ int m_pair_order(const DModel* dm, int y) { return dm->pair_order[y]; }
-#ifdef SOARM_DIAG_SKIPP
-__device__ uint32_t g_diag_skip[4];
-__device__ int g_diag_stage;  // (SOARM_DIAG_STAGE: 1 midphase only, 2 no mask atomics, else everything)
-#endif
 template <int CCD>
 __global__ __launch_bounds__(SOARM_COLLIDE_BLOCK, SOARM_COLLIDE_WAVES) void k_collide(const DModel* __restrict__ dm, int n,
                                                  const float* __restrict__ gpose,
@@ -984,6 +991,16 @@ void sim_batch_free(sim_batch* b) {
     return;
   }
   (void)hipSetDevice(b->device);
+#ifdef SOARM_DIAG_SUPPORT
+  {  // (diagnostic build: the support-query counters of every collide so far)
+    unsigned long long c[CON_MAXG][4];
+    (void)hipMemcpyFromSymbol(c, HIP_SYMBOL(g_diag_sup), sizeof(c), 0, hipMemcpyDeviceToHost);
+    for (int g = 0; g < CON_MAXG; g++)
+      if (c[g][0])
+        fprintf(stderr, "support geom %d: queries %llu, same cell %llu, same answer %llu, climb trips %llu\n", g,
+                c[g][0], c[g][1], c[g][2], c[g][3]);
+  }
+#endif
   (void)hipFree(b->d_scratch);
   (void)hipFree(b->d_gpose);
   (void)hipFree(b->d_cbuf);
