@@ -95,12 +95,13 @@ struct DModel {
   const int32_t* hull_adj;   // local neighbour ids
   const uint16_t* hull_lut;  // per mesh geom: HULL_LUT_CELLS start vertices (cube-map of directions)
   int geom_lutadr[MAXG];     // first LUT entry of each mesh geom (-1: not a mesh)
-  // hill-climbing records, 32 B per vertex (two uint4): [0] x, y, z (float bits), degree |
-  // overflow offset << 8; [1] the first 8 neighbour ids (local, uint16, padded with the
-  // vertex itself).  Neighbours past 8 live in hull_ovf.  hull_lutrec holds, per LUT cell
-  // (HULL_LUTREC uint4), a copy of its start vertex's record and the coordinates of its
-  // first 8 neighbours, so a query whose start cell already holds the maximum (the usual
-  // case) finishes in one round trip; each further climbing step is one more.
+  // hill-climbing records, 160 B per vertex (HULL_LUTREC uint4): [0] x, y, z (float bits),
+  // degree | overflow offset << 8; [1] the first 8 neighbour ids (local, uint16, padded with
+  // the vertex itself); [2..9] those neighbours' x, y, z and local id.  Neighbours past 8 live
+  // in hull_ovf.  hull_lutrec holds, per LUT cell, a copy of its start vertex's record, so a
+  // query whose start already holds the maximum (the usual case) finishes in one round trip
+  // and each climbing step costs one more (the record moved to carries its neighbours'
+  // coordinates: round 6, where a step had loaded the vertex and then its neighbours).
   const uint4* hull_rec;
   const uint4* hull_lutrec;
   const uint16_t* hull_ovf;
@@ -121,8 +122,8 @@ __host__ __device__ inline int pmask_words(const DModel& m) { return ((m.npair +
 // (115 MB of cell records for the 13 arm hulls) lands the start on the answer
 // more often: collide 0.287 (16) -> 0.251 (48) -> 0.231 (96) ms per env-step.
 constexpr int HULL_LUT_K = 96;
-// uint4 per LUT cell in hull_lutrec: the start vertex's two record words, then its first 8
-// neighbours as (x, y, z, local id) -- the first climbing step needs no second round trip
+// uint4 per climbing record (hull_rec, hull_lutrec): the vertex's two record words, then its
+// first 8 neighbours as (x, y, z, local id) -- a climbing step needs no second round trip
 constexpr int HULL_LUTREC = 10;
 constexpr int HULL_LUT_CELLS = 6 * HULL_LUT_K * HULL_LUT_K;
 

@@ -18,6 +18,10 @@
 // to the serial mj_collision order.
 #pragma once
 #include "soarm_step.h"
+#ifdef SOARM_DIAG_SUPPORT
+#include <atomic>
+#include <cstdio>
+#endif
 
 namespace soarm {
 
@@ -88,6 +92,29 @@ HDI uint4 ldg(gptr<uint4> p, int i) {  // (dword loads, merged into one 16-B loa
   const gptr<uint32_t> q = (gptr<uint32_t>)(p + i);
   return make_uint4(q[0], q[1], q[2], q[3]);
 }
+#if defined(SOARM_DIAG_SUPPORT) && !SOARM_DEVICE_PASS
+// (diagnostic build, CPU backend: the same counts with the lane's history reset per pair call --
+// what a cache that lives for one narrowphase call could reuse)
+struct DiagSupHost {
+  std::atomic<unsigned long long> c[CON_MAXG][4];
+  ~DiagSupHost() {
+    for (int g = 0; g < CON_MAXG; g++)
+      if (c[g][0])
+        fprintf(stderr, "host support geom %d: queries %llu, same cell %llu, same answer %llu, climb trips %llu\n", g,
+                c[g][0].load(), c[g][1].load(), c[g][2].load(), c[g][3].load());
+  }
+};
+inline DiagSupHost g_diag_sup_host;
+inline thread_local uint32_t g_diag_prev_host[2] = {~0u, ~0u};
+inline void diag_support(int g, int cell, uint4 r0, int steps) {
+  const uint32_t key = ((uint32_t)g << 20) | (uint32_t)cell, ans = r0.x ^ (r0.y * 3u) ^ (r0.z * 7u);
+  g_diag_sup_host.c[g][0]++;
+  if (g_diag_prev_host[0] == key) g_diag_sup_host.c[g][1]++;
+  if (g_diag_prev_host[1] == ans && (g_diag_prev_host[0] >> 20) == (uint32_t)g) g_diag_sup_host.c[g][2]++;
+  g_diag_sup_host.c[g][3] += steps;
+  g_diag_prev_host[0] = key, g_diag_prev_host[1] = ans;
+}
+#endif
 #if defined(SOARM_DIAG_SUPPORT) && SOARM_DEVICE_PASS
 // (diagnostic build: per geom, support queries, queries whose cube-map cell / answer repeats the
 // lane's previous query on that geom, and climbing round trips)
@@ -104,13 +131,16 @@ DEVI void diag_support(int g, int cell, uint4 r0, int steps) {
 }
 #endif
 HDI float3 hull_support(const DModel& m, int g, const float l[3]) {
-  const gptr<uint4> rec = (gptr<uint4>)m.hull_rec + 2 * m.geom_hulladr[g];
-#if defined(SOARM_DIAG_SUPPORT) && SOARM_DEVICE_PASS
+  const gptr<uint4> rec = (gptr<uint4>)m.hull_rec + HULL_LUTREC * m.geom_hulladr[g];
+#if defined(SOARM_DIAG_SUPPORT)
   const int dcell = lut_cell(l[0], l[1], l[2]);
   int dsteps = 0;
 #endif
+  // the cell's copy of its start vertex's record, then per climbing step the record of the vertex
+  // moved to: each carries its first 8 neighbours' coordinates, so a step is one round trip and
+  // the last (no neighbour improves) none
   const gptr<uint4> lr = (gptr<uint4>)m.hull_lutrec + HULL_LUTREC * (m.geom_lutadr[g] + lut_cell(l[0], l[1], l[2]));
-  uint4 r0 = ldg(lr, 0), r1 = ldg(lr, 1), nb[8];
+  uint4 r0 = ldg(lr, 0), nb[8];
 #pragma unroll
   for (int k = 0; k < 8; k++) nb[k] = ldg(lr, 2 + k);
   const int nvert = m.geom_hullnum[g];
@@ -118,7 +148,7 @@ HDI float3 hull_support(const DModel& m, int g, const float l[3]) {
     return l[0] * fbits(r.x) + l[1] * fbits(r.y) + l[2] * fbits(r.z);
   };
   float cd = dotr(r0);
-  if ((r0.w & 255u) <= 8) {  // first step from the cell's copy of the start's neighbours
+  for (int guard = 0; guard < nvert; guard++) {
     float nd = cd;
     int best = -1;
 #pragma unroll
@@ -126,63 +156,38 @@ HDI float3 hull_support(const DModel& m, int g, const float l[3]) {
       const float s = dotr(nb[k]);
       if (s > nd) nd = s, best = k;
     }
-    if (best < 0) {
-#if defined(SOARM_DIAG_SUPPORT) && SOARM_DEVICE_PASS
-      diag_support(g, dcell, r0, 0);
-#endif
-      return make_float3(fbits(r0.x), fbits(r0.y), fbits(r0.z));
-    }
     uint32_t u = 0;
 #pragma unroll
     for (int k = 0; k < 8; k++)
       if (k == best) u = nb[k].w;
-    r0 = ldg(rec, 2 * u), r1 = ldg(rec, 2 * u + 1), cd = nd;
-#if defined(SOARM_DIAG_SUPPORT) && SOARM_DEVICE_PASS
-    dsteps++;
-#endif
-  }
-  for (int guard = 0; guard < nvert; guard++) {
-#if defined(SOARM_DIAG_SUPPORT) && SOARM_DEVICE_PASS
-    dsteps++;
-#endif
-    const uint32_t ids[4] = {r1.x, r1.y, r1.z, r1.w};
-    uint4 c0[8], c1[8];
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const uint32_t u = (ids[k >> 1] >> (16 * (k & 1))) & 0xffffu;
-      c0[k] = ldg(rec, 2 * u), c1[k] = ldg(rec, 2 * u + 1);
-    }
-    float nd = cd;
-    int best = -1;
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const float s = dotr(c0[k]);
-      if (s > nd) nd = s, best = k;
-    }
-    uint4 b0 = r0, b1 = r1;
-#pragma unroll
-    for (int k = 0; k < 8; k++)
-      if (k == best) b0 = c0[k], b1 = c1[k];
     const int deg = (int)(r0.w & 255u);
     if (deg > 8) {  // hub vertex (~2%): the rest of its neighbours, 8 per round trip
       const gptr<uint16_t> ov = (gptr<uint16_t>)m.hull_ovf + (r0.w >> 8);
       for (int a = 8; a < deg; a += 8) {
+        uint32_t id[8];
+        uint4 c[8];
 #pragma unroll
         for (int k = 0; k < 8; k++) {
-          const uint32_t u = (a + k < deg) ? ov[a - 8 + k] : ov[a - 8];
-          c0[k] = ldg(rec, 2 * u), c1[k] = ldg(rec, 2 * u + 1);
+          id[k] = (a + k < deg) ? ov[a - 8 + k] : ov[a - 8];
+          c[k] = ldg(rec, HULL_LUTREC * id[k]);
         }
 #pragma unroll
         for (int k = 0; k < 8; k++) {
-          const float s = dotr(c0[k]);
-          if (s > nd) nd = s, b0 = c0[k], b1 = c1[k], best = 8;
+          const float s = dotr(c[k]);
+          if (s > nd) nd = s, u = id[k], best = 8;
         }
       }
     }
     if (best < 0) break;
-    r0 = b0, r1 = b1, cd = nd;
+    const gptr<uint4> r = rec + HULL_LUTREC * u;
+    r0 = ldg(r, 0), cd = nd;
+#pragma unroll
+    for (int k = 0; k < 8; k++) nb[k] = ldg(r, 2 + k);
+#if defined(SOARM_DIAG_SUPPORT)
+    dsteps++;
+#endif
   }
-#if defined(SOARM_DIAG_SUPPORT) && SOARM_DEVICE_PASS
+#if defined(SOARM_DIAG_SUPPORT)
   diag_support(g, dcell, r0, dsteps);
 #endif
   return make_float3(fbits(r0.x), fbits(r0.y), fbits(r0.z));
@@ -1482,6 +1487,9 @@ template <int CCD = -1>
 HDI void collide_pair(const DModel& m, int p, const float* __restrict__ gpose, int n, int e, PairOut& o,
                        const SepCache& sc = SepCache{nullptr, 0, 0}, const EpaPool* pool = nullptr) {
   o.n = 0;
+#if defined(SOARM_DIAG_SUPPORT) && !SOARM_DEVICE_PASS
+  g_diag_prev_host[0] = g_diag_prev_host[1] = ~0u;
+#endif
   GeomPose P1, P2;
   if (midphase(m, p, gpose, n, e, P1, P2)) narrowphase<CCD>(m, p, P1, P2, o, sc, pool);
 }

@@ -776,8 +776,9 @@ int sim_model_create(const sim_model_desc* desc, const float* hull_vert, const i
     for (auto& th : pool) th.join();
     k++;
   }
-  // climbing records: coordinates, degree and the first 8 neighbours in 32 B per vertex
-  M->hull_rec.assign((size_t)2 * std::max(desc->nhullvert, 1), make_uint4(0, 0, 0, 0));
+  // climbing records (HULL_LUTREC uint4 per vertex): coordinates and degree, the first 8 neighbour
+  // ids, then those neighbours' coordinates and ids
+  M->hull_rec.assign((size_t)HULL_LUTREC * std::max(desc->nhullvert, 1), make_uint4(0, 0, 0, 0));
   M->hull_ovf.assign(1, 0);
   for (int g = 0; g < desc->ngeom; g++) {
     if (desc->geom_type[g] != SIM_GEOM_MESH) continue;
@@ -793,11 +794,20 @@ int sim_model_create(const sim_model_desc* desc, const float* hull_vert, const i
       }
       uint32_t xb, yb, zb;
       memcpy(&xb, &hull_vert[3 * i], 4), memcpy(&yb, &hull_vert[3 * i + 1], 4), memcpy(&zb, &hull_vert[3 * i + 2], 4);
-      M->hull_rec[2 * i] = make_uint4(xb, yb, zb, (uint32_t)deg | (deg > 8 ? (uint32_t)ovf << 8 : 0u));
+      M->hull_rec[HULL_LUTREC * i] = make_uint4(xb, yb, zb, (uint32_t)deg | (deg > 8 ? (uint32_t)ovf << 8 : 0u));
       uint32_t id[8];
       for (int a = 0; a < 8; a++) id[a] = a < deg ? (uint32_t)M->hull_adj[a0 + a] : (uint32_t)li;
-      M->hull_rec[2 * i + 1] = make_uint4(id[0] | id[1] << 16, id[2] | id[3] << 16, id[4] | id[5] << 16, id[6] | id[7] << 16);
+      M->hull_rec[HULL_LUTREC * i + 1] =
+          make_uint4(id[0] | id[1] << 16, id[2] | id[3] << 16, id[4] | id[5] << 16, id[6] | id[7] << 16);
     }
+    for (int li = 0; li < desc->geom_hullnum[g]; li++)  // neighbour k in record order (padding = the vertex itself)
+      for (int k = 0; k < 8; k++) {
+        const uint4 ids = M->hull_rec[HULL_LUTREC * (base + li) + 1];
+        const uint32_t w[4] = {ids.x, ids.y, ids.z, ids.w};
+        const uint32_t u = (w[k >> 1] >> (16 * (k & 1))) & 0xffffu;
+        const uint4 r = M->hull_rec[HULL_LUTREC * (base + u)];
+        M->hull_rec[HULL_LUTREC * (base + li) + 2 + k] = make_uint4(r.x, r.y, r.z, u);
+      }
   }
   // support-bound table: exact support at every grid point, rounded up to the next float
   M->hull_sb.assign((size_t)std::max(nmesh, 1) * 6 * HULL_SB_FACE, 0.f);
@@ -832,16 +842,8 @@ int sim_model_create(const sim_model_desc* desc, const float* hull_vert, const i
     for (int c = 0; c < HULL_LUT_CELLS; c++) {
       const size_t cell = (size_t)M->lutadr[g] + c;
       const size_t v = base + M->hull_lut[cell];
-      uint4* out = &M->hull_lutrec[HULL_LUTREC * cell];
-      out[0] = M->hull_rec[2 * v];
-      out[1] = M->hull_rec[2 * v + 1];
-      const uint4 ids = out[1];
-      const uint32_t w[4] = {ids.x, ids.y, ids.z, ids.w};
-      for (int k = 0; k < 8; k++) {  // neighbour k in record order (padding = the vertex itself)
-        const uint32_t u = (w[k >> 1] >> (16 * (k & 1))) & 0xffffu;
-        const uint4 r = M->hull_rec[2 * (base + u)];
-        out[2 + k] = make_uint4(r.x, r.y, r.z, u);
-      }
+      for (int k = 0; k < HULL_LUTREC; k++)  // (a copy of its start vertex's record)
+        M->hull_lutrec[HULL_LUTREC * cell + k] = M->hull_rec[HULL_LUTREC * v + k];
     }
   }
   cpu_qpos0_contacts(M);  // (the hull tables above are its input)
