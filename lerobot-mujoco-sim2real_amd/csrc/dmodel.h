@@ -121,7 +121,10 @@ __host__ __device__ inline int pmask_words(const DModel& m) { return ((m.npair +
 // collide kernel is latency-bound on support round trips, and a finer map
 // (115 MB of cell records for the 13 arm hulls) lands the start on the answer
 // more often: collide 0.287 (16) -> 0.251 (48) -> 0.231 (96) ms per env-step.
-constexpr int HULL_LUT_K = 96;
+#ifndef SOARM_HULL_LUT_K
+#define SOARM_HULL_LUT_K 96
+#endif
+constexpr int HULL_LUT_K = SOARM_HULL_LUT_K;
 // uint4 per climbing record (hull_rec, hull_lutrec): the vertex's two record words, then its
 // first 8 neighbours as (x, y, z, local id) -- a climbing step needs no second round trip
 constexpr int HULL_LUTREC = 10;
