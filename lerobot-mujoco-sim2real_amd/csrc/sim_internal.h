@@ -39,6 +39,9 @@ struct CpuBatch;
 int cpu_batch_create(const sim_model* m, int n, CpuBatch** out);
 // the model's contacts at qpos0 (DModel c0_*: what a soft reset's mj_forward collides), at model creation
 int cpu_qpos0_contacts(sim_model* m);
+// test hook (not part of the C ABI): the kernels' hull support query (soarm_collide.h hull_support,
+// compiled for the host) of mesh geom g along nd local directions dirs [nd][3] -> out [nd][3]
+extern "C" int soarm_test_hull_support(const sim_model* m, int g, const float* dirs, int nd, float* out);
 void cpu_batch_free(CpuBatch* c);
 int cpu_reset(CpuBatch* c, const sim_state* s, const float* init_qpos, const float* init_qvel,
               const float* extra_qpos, uint64_t seed, int64_t env_offset, const uint8_t* mask, float* obs);

@@ -610,6 +610,20 @@ int cpu_qpos0_contacts(sim_model* m) {
   return SIM_OK;
 }
 
+extern "C" int soarm_test_hull_support(const sim_model* m, int g, const float* dirs, int nd, float* out) {
+  if (!m || !dirs || !out || nd < 0) return soarm_set_error(SIM_E_ARG, "null argument");
+  if (g < 0 || g >= m->desc.ngeom || m->desc.geom_type[g] != SIM_GEOM_MESH || m->lutadr[g] < 0)
+    return soarm_set_error(SIM_E_ARG, "not a mesh geom");
+  CpuBatch* c = nullptr;
+  cpu_batch_create(m, 1, &c);
+  for (int i = 0; i < nd; i++) {
+    const float3 v = hull_support(c->dm, g, dirs + 3 * i);
+    out[3 * i] = v.x, out[3 * i + 1] = v.y, out[3 * i + 2] = v.z;
+  }
+  cpu_batch_free(c);
+  return SIM_OK;
+}
+
 int cpu_reset(CpuBatch* c, const sim_state* s, const float* init_qpos, const float* init_qvel,
               const float* extra_qpos, uint64_t seed, int64_t env_offset, const uint8_t* mask, float* obs) {
   if (int rc = check(c, s)) return rc;
