@@ -512,9 +512,7 @@ void step_env(const CpuBatch& B, const sim_state& st, const sim_params& pp, cons
   CpuContact cl[SIM_MAXCON];
   float nsum = 0.f;
   for (int s = 0; s < nsub; s++) {
-    const int sb = S.status;
-    S.check_state();
-    if (applied && S.status != sb) zero_applied(applied, NV, n, e);
+    if (S.check_state() && applied) zero_applied(applied, NV, n, e);
     int nc = 0;
     if (con) {
       S.kinematics();

@@ -425,7 +425,9 @@ struct Sim {
 #pragma unroll
     for (int i = 0; i < NA; i++) ctrl[i] = 0.f;
   }
-  HDI void check_state() {
+  // true when it reset the env (the status bits are sticky: a second reset for the same cause
+  // leaves them as they were, so callers test this, not a status change)
+  HDI bool check_state() {
     const DModel& m = *mp;
     bool bq = false, bv = false;
 #pragma unroll
@@ -434,6 +436,7 @@ struct Sim {
 #pragma unroll
     for (int i = 0; i < NV; i++) bv |= bad(qvel[i]);
     if (bv) soft_reset(SIM_ST_BADQVEL);
+    return bq || bv;
   }
   HDI bool acc_bad() const {
     const DModel& m = *mp;

@@ -71,9 +71,7 @@ __global__ __launch_bounds__(64) void k_step(const DModel* __restrict__ dm, int 
   float* const applied = AP ? st.qfrc_applied : nullptr;
   for (int s = 0; s < nsub; s++) {
     S.relaunder();
-    const int sb = S.status;
-    S.check_state();
-    if (AP && S.status != sb) zero_applied(applied, Sim<NA, NF>::NV, n, e);
+    if (S.check_state() && AP) zero_applied(applied, Sim<NA, NF>::NV, n, e);
     forward<NA, NF, false, SOL>(S, nullptr, nullptr, nullptr, n, e, L, cr, applied);
     if (S.acc_bad()) {
       S.soft_reset(SIM_ST_BADQACC);
@@ -165,11 +163,10 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
   if constexpr (RS) L.rsw = s_rsw;
   const ContactRows<NA, NF> cr{scratch + e, n};
   const float ncon_prev = st.ncon ? st.ncon[e] : 0.f;  // issued early: consumed at the end
-  const int st0 = S.status;
-  S.check_state();
+  const bool reset = S.check_state();
   // positions / velocities are re-read from HBM after the solve instead of being held in
   // registers through it: a soft reset must reach HBM first
-  if (S.status != st0) {
+  if (reset) {
     store_state(S, st, n, e);
     if (AP) zero_applied(st.qfrc_applied, Sim<NA, NF>::NV, n, e);
   }
@@ -186,7 +183,7 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
   }
   PairMask pm;
   if (use) pm.load(pmask, m, n, e);  // (stays zero otherwise: no contact list)
-  if (use && S.status != st0) qpos0_contacts(m, const_cast<float*>(cbuf), n, e, pm);
+  if (use && reset) qpos0_contacts(m, const_cast<float*>(cbuf), n, e, pm);
 #ifdef SOARM_PHASE_PROF
   PHASE_T(t1);
   PSTAMP(0);

@@ -476,3 +476,12 @@ def test_cpu_soft_reset_contact_scene_limit_at_qpos0(cpu_lib):
     dv = np.abs(to_np(S.qvel).T - st["qvel"]).max(1)
     assert_pct(dv, *QVEL_BARS, what="qvel")
     assert dv[bad].max() < 1e-5, dv[bad]
+    # the same envs go bad again (status bits already set): reset, qpos0 contacts, as the oracle
+    S.qvel[2, bad] = float("nan")
+    st["qvel"][bad, 2] = np.nan
+    S.substeps(1)
+    orc.step(st, None, nsub=1)
+    assert (to_np(S.status).astype(int) == st["status"]).all()
+    np.testing.assert_allclose(to_np(S.qpos).T[bad], st["qpos"][bad], atol=5e-6)
+    dv = np.abs(to_np(S.qvel).T - st["qvel"]).max(1)
+    assert dv[bad].max() < 1e-5, dv[bad]

@@ -667,6 +667,26 @@ def test_soft_reset_contact_scene_limit_at_qpos0(gpu_lib, rs, monkeypatch):
     assert_pct(dv, *QVEL_BARS, what="qvel")
     assert dv[bad].max() < 1e-5, dv[bad]
     assert to_np(S.ncon).sum() == st["ncon"].sum()
+    # the same envs go bad again: their status bits are already set (sticky), the reset must still
+    # store the qpos0 state, take the contacts at qpos0 (the collide ran on the discarded qpos) and
+    # run its own kinematics
+    import torch
+    st = f32(st)  # (both sides from the same fp32 state again, the device's status bits kept)
+    status = S.status.clone()
+    load_state(S, st)
+    S.status.copy_(status)
+    S.qvel[2, bad] = torch.nan
+    st["qvel"][bad, 2] = np.nan
+    ncon0 = to_np(S.ncon).sum()
+    S.substeps(1)
+    orc.step(st, None, nsub=1)
+    stat = to_np(S.status).astype(int)
+    assert (stat == st["status"]).all()
+    np.testing.assert_allclose(to_np(S.qpos).T[bad], st["qpos"][bad], atol=5e-6)
+    dv = np.abs(to_np(S.qvel).T - st["qvel"]).max(1)
+    assert_pct(dv, *QVEL_BARS, what="qvel")
+    assert dv[bad].max() < 1e-5, dv[bad]
+    assert to_np(S.ncon).sum() - ncon0 == st["ncon"].sum() - ncon0
 
 
 def test_golden_fixture_gpu(gpu_lib, arm_model_nocontact):

@@ -2,7 +2,7 @@
 """Diagnostic: run the bench's contact workload for T env-steps with the library named by
 SOARM_SIM_LIB and save the per-step obs checksums and the final state, so two builds can be
 compared bit for bit (an exact change -- e.g. a cheaper separation proof -- must leave them
-identical).  usage: ab_state.py TAG [T] [solver]"""
+identical).  usage: ab_state.py TAG [T] [solver]; N=envs (default 4096: 8192 runs the quad PGS kernel)"""
 import os
 import sys
 
@@ -18,7 +18,7 @@ from lerobot_mujoco_sim2real_amd.sim import BatchSim  # noqa: E402
 tag = sys.argv[1]
 T = int(sys.argv[2]) if len(sys.argv) > 2 else 120
 solver = sys.argv[3] if len(sys.argv) > 3 else "PGS"
-n = 4096
+n = int(os.environ.get("N", "4096"))
 cm = W.model("contact", solver=solver, ccd=os.environ.get("CCD", W.BENCH_CCD))
 ids = np.arange(n)
 sim = BatchSim(cm, n, 0)
