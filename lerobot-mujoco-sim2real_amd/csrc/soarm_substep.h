@@ -163,7 +163,12 @@ __global__ __launch_bounds__(64) void k_substep(const DModel* __restrict__ dm, i
   if constexpr (RS) L.rsw = s_rsw;
   const ContactRows<NA, NF> cr{scratch + e, n};
   const float ncon_prev = st.ncon ? st.ncon[e] : 0.f;  // issued early: consumed at the end
-  const bool reset = S.check_state();
+  // (the status bits are sticky: a reset is this substep's when check_state sets a cleared bit)
+  const int st0 = S.status;
+  S.status = st0 & ~(SIM_ST_BADQPOS | SIM_ST_BADQVEL);
+  S.check_state();
+  const bool reset = S.status != (st0 & ~(SIM_ST_BADQPOS | SIM_ST_BADQVEL));
+  S.status |= st0;
   // positions / velocities are re-read from HBM after the solve instead of being held in
   // registers through it: a soft reset must reach HBM first
   if (reset) {
